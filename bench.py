@@ -1,0 +1,127 @@
+#!/usr/bin/env python
+"""Headline benchmark: images/sec (whole node), ResNet-18 224x224 training, 1/2/4/8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Config (BASELINE.json): ResNet-18 with the reference's 64,500-class head (utils.py:39),
+224x224 synthetic uint8 images (preprocessed on the GPU each step), random-init weights,
+bf16 compute with fp32 master weights, Adam (lr 4e-4, the reference optimizer,
+main.py:125), data-parallel over RCCL with per-GPU batch fixed (weak scaling).
+
+Timing: W untimed warmup steps, then EXACTLY K steps bracketed by barrier +
+torch.cuda.synchronize() on both sides; the max over ranks is reported.  The timed region
+includes the data path (ring acquire, H2D, preprocess kernel), forward, backward, the
+gradient all-reduce and the optimizer step.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_IMG_S = 8.06  # reference FLOP-equivalent img/s at 224^2 (best, 4 ranks)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--model", default="resnet18")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--classes", type=int, default=64500)
+    p.add_argument("--optimizer", default="adam")
+    p.add_argument("--lr", type=float, default=4e-4)
+    p.add_argument("--graph", default="auto", choices=["auto", "on", "off"])
+    p.add_argument("--bucket-mb", type=float, default=64.0)
+    p.add_argument("--comm-dtype", default="fp32")
+    p.add_argument("--profile-steps", type=int, default=0)
+    args = p.parse_args(argv)
+
+    from mpi_pytorch_amd.parallel import init_world, barrier, get_world
+    from mpi_pytorch_amd.engine import build_training
+    from mpi_pytorch_amd.data import DevicePrefetcher
+
+    world = init_world("cuda")
+    if world.world_size != args.gpus and world.rank == 0:
+        print("warning: --gpus {} but WORLD_SIZE {}".format(args.gpus, world.world_size),
+              file=sys.stderr)
+    torch.manual_seed(0)
+    dev = world.device
+    hw = (args.image_size, args.image_size)
+    model, opt, step, _ = build_training(args.model, args.classes, dev, world, args.lr,
+                                         args.optimizer, bucket_mb=args.bucket_mb,
+                                         comm_dtype=args.comm_dtype)
+    data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
+                            world=world.world_size, depth=6, threads=4)
+
+    use_graph = args.graph == "on" or (args.graph == "auto" and world.world_size == 1)
+    if use_graph:
+        x, y = data.next()
+        use_graph = step.capture(x, y)
+    for _ in range(args.warmup):
+        x, y = data.next()
+        step(x, y)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x, y = data.next()
+        step(x, y)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = step.mean_loss()
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world.world_size > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    imgs = args.steps * args.batch * world.world_size
+    value = imgs / dt
+    if world.rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1000.0 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_IMG_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": args.model,
+                "global_batch": args.batch * world.world_size,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "image_size": args.image_size,
+                "num_classes": args.classes,
+                "optimizer": args.optimizer,
+                "parallelism": "dp{}".format(world.world_size),
+                "hip_graph": bool(use_graph),
+                "mean_loss": round(loss, 4),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    data.close()
+    from mpi_pytorch_amd.parallel import shutdown
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,521 @@
+// Torch-facing binding layer for the gfx950 kernel library (module mpi_pytorch_amd._C).
+//
+// Responsibilities: validate dtypes/shapes/contiguity (so a kernel never sees operands its
+// grid does not expect), allocate outputs on the caller's device, build the implicit-GEMM
+// tap tables, and launch on the current HIP stream (so everything composes with HIP
+// graphs and the RCCL comm stream).  The function set mirrors ops/ref.py one-to-one.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <vector>
+
+#include "kernels/api.h"
+#include "runtime/runtime.h"
+
+using torch::Tensor;
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_BF16(x) \
+  TORCH_CHECK((x).scalar_type() == torch::kBFloat16, #x " must be bfloat16, got ", (x).scalar_type())
+#define CHECK_F32(x) \
+  TORCH_CHECK((x).scalar_type() == torch::kFloat32, #x " must be float32, got ", (x).scalar_type())
+#define CHECK_ACT(x) \
+  CHECK_CUDA(x);     \
+  CHECK_CONTIG(x);   \
+  CHECK_BF16(x)
+
+inline const mpa::bf16_raw* bp(const Tensor& t) {
+  return reinterpret_cast<const mpa::bf16_raw*>(t.data_ptr());
+}
+inline mpa::bf16_raw* bpm(const Tensor& t) { return reinterpret_cast<mpa::bf16_raw*>(t.data_ptr()); }
+inline bool has(const Tensor& t) { return t.defined() && t.numel() > 0; }
+inline const float* fopt(const Tensor& t) {
+  if (!has(t)) return nullptr;
+  CHECK_CUDA(t);
+  CHECK_F32(t);
+  CHECK_CONTIG(t);
+  return t.data_ptr<float>();
+}
+inline float* fopt_mut(const Tensor& t) { return const_cast<float*>(fopt(t)); }
+inline const mpa::bf16_raw* bopt(const Tensor& t) {
+  if (!has(t)) return nullptr;
+  CHECK_ACT(t);
+  return bp(t);
+}
+
+inline int vec_width(int64_t c) { return (c % 8 == 0) ? 8 : ((c % 4 == 0) ? 4 : 1); }
+
+Tensor empty_like_shape(const Tensor& ref, at::IntArrayRef shape, torch::Dtype dt) {
+  return torch::empty(shape, ref.options().dtype(dt));
+}
+
+// ------------------------------------------------------------------------------- conv
+Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                bool relu, Tensor stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: x NHWC, w KRSC");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "conv_fwd: channel mismatch");
+  TORCH_CHECK(R * S <= mpa::MAXT, "conv_fwd: too many taps");
+  const int P = (H + 2 * ph - R) / sh + 1, Q = (W + 2 * pw - S) / sw + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "conv_fwd: empty output");
+  if (has(bias)) TORCH_CHECK(bias.numel() == K, "conv_fwd: bias size");
+  if (has(stats)) TORCH_CHECK(stats.numel() == 2 * K, "conv_fwd: stats size");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = empty_like_shape(x, {N, P, Q, K}, torch::kBFloat16);
+  mpa::IGemmArgs a{};
+  a.A = bp(x); a.aH = H; a.aW = W; a.aC = C;
+  a.oH = P; a.oW = Q; a.M = N * P * Q;
+  a.Uh = sh; a.Uw = sw; a.Oh = -ph; a.Ow = -pw;
+  a.T = R * S;
+  for (int r = 0; r < R; ++r)
+    for (int s = 0; s < S; ++s) {
+      const int t = r * S + s;
+      a.taps.dh[t] = r; a.taps.dw[t] = s; a.taps.bt[t] = t;
+    }
+  a.Ktot = a.T * C;
+  a.B = bp(w); a.N = K; a.RS = R * S; a.ldb = a.Ktot;
+  a.C = y.data_ptr(); a.ldc = K;
+  a.dH = P; a.dW = Q; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
+  a.bias = fopt(bias);
+  a.stats = fopt_mut(stats);
+  a.relu = relu ? 1 : 0;
+  Tensor ws;
+  float* wsp = nullptr;
+  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
+    ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  mpa::igemm_rows(a, vec_width(C), wsp, cur_stream());
+  return y;
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
+                  int64_t pw) {
+  CHECK_ACT(dy);
+  CHECK_ACT(w);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  const int Kw = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(Kw == K, "conv_dgrad: channel mismatch");
+  TORCH_CHECK(R * S <= mpa::MAXT, "conv_dgrad: too many taps");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, (int64_t)H, (int64_t)W, C}, torch::kBFloat16);
+  const int vw = std::min(vec_width(K), vec_width(C));
+  for (int a_ = 0; a_ < sh; ++a_)
+    for (int b_ = 0; b_ < sw; ++b_) {
+      const int Hp = (H - a_ + sh - 1) / sh, Wp = (W - b_ + sw - 1) / sw;
+      if (Hp <= 0 || Wp <= 0) continue;
+      mpa::IGemmArgs a{};
+      a.A = bp(dy); a.aH = P; a.aW = Q; a.aC = K;
+      a.oH = Hp; a.oW = Wp; a.M = N * Hp * Wp;
+      a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+      int T = 0;
+      for (int r = 0; r < R; ++r) {
+        if (((a_ + ph - r) % sh) != 0) continue;
+        for (int s = 0; s < S; ++s) {
+          if (((b_ + pw - s) % sw) != 0) continue;
+          a.taps.dh[T] = (a_ + ph - r) / sh;
+          a.taps.dw[T] = (b_ + pw - s) / sw;
+          a.taps.bt[T] = r * S + s;
+          ++T;
+        }
+      }
+      a.T = T;
+      a.Ktot = T * K;
+      a.B = bp(w); a.N = C; a.RS = R * S; a.ldb = C;
+      a.C = dx.data_ptr(); a.ldc = C;
+      a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw; a.Poh = a_; a.Pow = b_;
+      a.bias = nullptr; a.stats = nullptr; a.relu = 0;
+      Tensor ws;
+      float* wsp = nullptr;
+      if (sh == 1 && sw == 1 && mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
+        ws = torch::empty({(int64_t)a.M * a.N}, dy.options().dtype(torch::kFloat32));
+        wsp = ws.data_ptr<float>();
+      }
+      mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream());
+    }
+  return dx;
+}
+
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  CHECK_CUDA(dw);
+  CHECK_F32(dw);
+  CHECK_CONTIG(dw);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  TORCH_CHECK(dw.dim() == 4 && dw.size(0) == K && dw.size(3) == C, "conv_wgrad: dw shape");
+  const int R = dw.size(1), S = dw.size(2);
+  TORCH_CHECK(dy.size(0) == N, "conv_wgrad: batch mismatch");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  mpa::WGradArgs a{};
+  a.dy = bp(dy); a.x = bp(x); a.dw = dw.data_ptr<float>();
+  a.Kout = K; a.C = C; a.H = H; a.W = W; a.P = P; a.Q = Q; a.R = R; a.S = S;
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
+  a.Mpix = N * P * Q;
+  a.Ncols = R * S * C;
+  mpa::igemm_wgrad(a, vec_width(K), (C % 8 == 0) ? 8 : 1, cur_stream());
+}
+
+Tensor act_bwd(Tensor dy, Tensor y, Tensor dbias) {
+  CHECK_ACT(dy);
+  const int C = dy.size(-1);
+  const int M = dy.numel() / C;
+  const bool hy = has(y);
+  if (!hy && !has(dbias)) return dy;
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor out = hy ? torch::empty_like(dy) : dy;
+  mpa::act_bwd(bp(dy), hy ? bopt(y) : nullptr, fopt_mut(dbias), M, C, hy ? bpm(out) : nullptr,
+               cur_stream());
+  return out;
+}
+
+// -------------------------------------------------------------------------------- BN
+std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
+                                 Tensor rvar, double momentum, double eps, Tensor res, bool relu) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor st = stats;
+  if (!has(st)) {
+    st = torch::zeros({2, C}, x.options().dtype(torch::kFloat32));
+    mpa::bn_stats(bp(x), M, C, st.data_ptr<float>(), cur_stream());
+  }
+  Tensor y = torch::empty_like(x);
+  Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
+  Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
+  mpa::bn_fwd_train(bp(x), fopt(st), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
+                    (float)momentum, (float)eps, bopt(res), relu ? 1 : 0, M, C, bpm(y),
+                    mean.data_ptr<float>(), rstd.data_ptr<float>(), cur_stream());
+  return {y, mean, rstd};
+}
+
+Tensor bn_fwd_eval(Tensor x, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar, double eps,
+                   Tensor res, bool relu) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = torch::empty_like(x);
+  mpa::bn_fwd_eval(bp(x), fopt(gamma), fopt(beta), fopt(rmean), fopt(rvar), (float)eps,
+                   bopt(res), relu ? 1 : 0, M, C, bpm(y), cur_stream());
+  return y;
+}
+
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd, Tensor gamma,
+                           Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd: dy/x shape mismatch");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
+  Tensor gout = want_g ? torch::empty_like(x) : Tensor();
+  Tensor ws = torch::empty({2 * C}, x.options().dtype(torch::kFloat32));
+  mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
+              fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr, want_g ? bpm(gout) : nullptr,
+              ws.data_ptr<float>(), cur_stream());
+  return {dx, gout};
+}
+
+Tensor relu_fwd(Tensor x) {
+  CHECK_ACT(x);
+  TORCH_CHECK(x.numel() % 8 == 0, "relu: numel must be a multiple of 8");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = torch::empty_like(x);
+  mpa::relu_fwd(bp(x), x.numel(), bpm(y), cur_stream());
+  return y;
+}
+
+// ------------------------------------------------------------------------------ pools
+int pool_out(int H, int k, int s, int p, bool ceil) {
+  int o;
+  if (ceil) {
+    o = (H + 2 * p - k + s - 1) / s + 1;
+    if ((o - 1) * s >= H + p) --o;
+  } else {
+    o = (H + 2 * p - k) / s + 1;
+  }
+  return o;
+}
+
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                                int64_t ph, int64_t pw, bool ceil) {
+  CHECK_ACT(x);
+  TORCH_CHECK(kh * kw <= 256, "maxpool: window too large for uint8 argmax");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = pool_out(H, kh, sh, ph, ceil), Q = pool_out(W, kw, sw, pw, ceil);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = empty_like_shape(x, {N, P, Q, C}, torch::kBFloat16);
+  Tensor idx = empty_like_shape(x, {N, P, Q, C}, torch::kUInt8);
+  mpa::maxpool_fwd(bp(x), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, bpm(y), idx.data_ptr<uint8_t>(),
+                   cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh,
+                   int64_t sw, int64_t ph, int64_t pw, bool ceil) {
+  CHECK_ACT(dy);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  (void)ceil;
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  mpa::maxpool_bwd(bp(dy), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw,
+                   bpm(dx), cur_stream());
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+                   int64_t pw, bool ceil, bool cip) {
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = pool_out(H, kh, sh, ph, ceil), Q = pool_out(W, kw, sw, pw, ceil);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = empty_like_shape(x, {N, P, Q, C}, torch::kBFloat16);
+  mpa::avgpool_fwd(bp(x), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, cip ? 1 : 0, bpm(y),
+                   cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh,
+                   int64_t sw, int64_t ph, int64_t pw, bool ceil, bool cip) {
+  CHECK_ACT(dy);
+  (void)ceil;
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  mpa::avgpool_bwd(bp(dy), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, cip ? 1 : 0, bpm(dx),
+                   cur_stream());
+  return dx;
+}
+
+Tensor adaptive_avgpool_fwd(Tensor x, int64_t P, int64_t Q) {
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = empty_like_shape(x, {N, P, Q, C}, torch::kBFloat16);
+  mpa::adaptive_avgpool_fwd(bp(x), N, H, W, C, P, Q, bpm(y), cur_stream());
+  return y;
+}
+
+Tensor adaptive_avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
+  CHECK_ACT(dy);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  mpa::adaptive_avgpool_bwd(bp(dy), N, H, W, C, P, Q, bpm(dx), cur_stream());
+  return dx;
+}
+
+// ----------------------------------------------------------------------------- linear
+Tensor linear_fwd(Tensor x, Tensor w, Tensor bias, bool relu) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear_fwd: shapes");
+  const int B = x.size(0), Cin = x.size(1), Cout = w.size(0);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = empty_like_shape(x, {B, Cout}, torch::kBFloat16);
+  mpa::IGemmArgs a{};
+  a.A = bp(x); a.aH = 1; a.aW = 1; a.aC = Cin;
+  a.oH = 1; a.oW = 1; a.M = B;
+  a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+  a.T = 1; a.taps.dh[0] = 0; a.taps.dw[0] = 0; a.taps.bt[0] = 0;
+  a.Ktot = Cin;
+  a.B = bp(w); a.N = Cout; a.RS = 1; a.ldb = Cin;
+  a.C = y.data_ptr(); a.ldc = Cout;
+  a.dH = 1; a.dW = 1; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
+  a.bias = fopt(bias); a.stats = nullptr; a.relu = relu ? 1 : 0;
+  Tensor ws;
+  float* wsp = nullptr;
+  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
+    ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  mpa::igemm_rows(a, vec_width(Cin), wsp, cur_stream());
+  return y;
+}
+
+Tensor linear_dgrad(Tensor dy, Tensor w) {
+  CHECK_ACT(dy);
+  CHECK_ACT(w);
+  const int B = dy.size(0), Cout = dy.size(1), Cin = w.size(1);
+  TORCH_CHECK(w.size(0) == Cout, "linear_dgrad: shapes");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {B, Cin}, torch::kBFloat16);
+  mpa::IGemmArgs a{};
+  a.A = bp(dy); a.aH = 1; a.aW = 1; a.aC = Cout;
+  a.oH = 1; a.oW = 1; a.M = B;
+  a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+  a.T = 1; a.taps.dh[0] = 0; a.taps.dw[0] = 0; a.taps.bt[0] = 0;
+  a.Ktot = Cout;
+  a.B = bp(w); a.N = Cin; a.RS = 1; a.ldb = Cin;
+  a.C = dx.data_ptr(); a.ldc = Cin;
+  a.dH = 1; a.dW = 1; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
+  Tensor ws;
+  float* wsp = nullptr;
+  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
+    ws = torch::empty({(int64_t)a.M * a.N}, dy.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
+  mpa::igemm_rows_dgrad(a, std::min(vec_width(Cout), vec_width(Cin)), wsp, cur_stream());
+  return dx;
+}
+
+void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  CHECK_CUDA(dw);
+  CHECK_F32(dw);
+  const int B = dy.size(0), Cout = dy.size(1), Cin = x.size(1);
+  TORCH_CHECK(dw.size(0) == Cout && dw.size(1) == Cin, "linear_wgrad: dw shape");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  mpa::WGradArgs a{};
+  a.dy = bp(dy); a.x = bp(x); a.dw = dw.data_ptr<float>();
+  a.Kout = Cout; a.C = Cin; a.H = 1; a.W = 1; a.P = 1; a.Q = 1; a.R = 1; a.S = 1;
+  a.sh = 1; a.sw = 1; a.ph = 0; a.pw = 0;
+  a.Mpix = B; a.Ncols = Cin;
+  mpa::igemm_wgrad(a, vec_width(Cout), (Cin % 8 == 0) ? 8 : 1, cur_stream());
+}
+
+// ------------------------------------------------------------------------ loss / acc
+std::vector<Tensor> ce_fwd(Tensor logits, Tensor labels) {
+  CHECK_ACT(logits);
+  CHECK_CUDA(labels);
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64, "labels must be int64");
+  const int B = logits.size(0), NC = logits.size(1);
+  const c10::OptionalDeviceGuard g(device_of(logits));
+  Tensor loss = torch::empty({1}, logits.options().dtype(torch::kFloat32));
+  Tensor lse = torch::empty({B}, logits.options().dtype(torch::kFloat32));
+  mpa::ce_fwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), B, NC, loss.data_ptr<float>(),
+              lse.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+Tensor ce_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor grad_out) {
+  CHECK_ACT(logits);
+  const int B = logits.size(0), NC = logits.size(1);
+  const c10::OptionalDeviceGuard g(device_of(logits));
+  Tensor d = torch::empty_like(logits);
+  mpa::ce_bwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), fopt(lse), fopt(grad_out), B,
+              NC, bpm(d), cur_stream());
+  return d;
+}
+
+void argmax_correct(Tensor logits, Tensor labels, Tensor count) {
+  CHECK_ACT(logits);
+  TORCH_CHECK(count.scalar_type() == torch::kInt64, "count must be int64");
+  const c10::OptionalDeviceGuard g(device_of(logits));
+  mpa::argmax_correct(bp(logits), labels.contiguous().data_ptr<int64_t>(), logits.size(0),
+                      logits.size(1), count.data_ptr<int64_t>(), cur_stream());
+}
+
+// ----------------------------------------------------------------------------- optim
+void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor shadow, Tensor step, double lr,
+               double b1, double b2, double eps, double wd, double gs) {
+  CHECK_F32(p);
+  TORCH_CHECK(p.numel() % 4 == 0 && g.numel() >= p.numel(), "adam: sizes");
+  const c10::OptionalDeviceGuard gd(device_of(p));
+  mpa::adam_step(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                 v.data_ptr<float>(), has(shadow) ? bpm(shadow) : nullptr, step.data_ptr<float>(),
+                 p.numel(), lr, b1, b2, eps, wd, gs, cur_stream());
+}
+
+void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor shadow, Tensor step, double lr,
+              double momentum, double dampening, double wd, bool nesterov, double gs) {
+  CHECK_F32(p);
+  TORCH_CHECK(p.numel() % 4 == 0, "sgd: sizes");
+  const c10::OptionalDeviceGuard gd(device_of(p));
+  mpa::sgd_step(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(),
+                has(shadow) ? bpm(shadow) : nullptr, step.data_ptr<float>(), p.numel(), lr,
+                momentum, dampening, wd, nesterov ? 1 : 0, gs, cur_stream());
+}
+
+void cast_f32_bf16(Tensor x, Tensor y) {
+  CHECK_F32(x);
+  CHECK_BF16(y);
+  TORCH_CHECK(x.numel() % 4 == 0 && y.numel() == x.numel(), "cast: sizes");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  mpa::cast_f32_bf16(x.data_ptr<float>(), bpm(y), x.numel(), cur_stream());
+}
+
+// ------------------------------------------------------------------------ preprocess
+Tensor preprocess(Tensor img, int64_t OH, int64_t OW, std::vector<double> mean,
+                  std::vector<double> stdv, int64_t mode, int64_t cpad) {
+  CHECK_CUDA(img);
+  CHECK_CONTIG(img);
+  TORCH_CHECK(img.scalar_type() == torch::kUInt8 && img.dim() == 4 && img.size(3) == 3,
+              "preprocess: expects uint8 [B,H,W,3]");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3 && cpad >= 3, "preprocess: args");
+  const c10::OptionalDeviceGuard g(device_of(img));
+  const int B = img.size(0), H = img.size(1), W = img.size(2);
+  Tensor out = empty_like_shape(img, {B, OH, OW, cpad}, torch::kBFloat16);
+  mpa::Norm3 n;
+  for (int i = 0; i < 3; ++i) { n.mean[i] = mean[i]; n.std[i] = stdv[i]; }
+  mpa::preprocess(img.data_ptr<uint8_t>(), B, H, W, OH, OW, n, mode, cpad, bpm(out), cur_stream());
+  return out;
+}
+
+std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset) {
+  CHECK_ACT(x);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = torch::empty_like(x);
+  Tensor mask = torch::empty(x.sizes(), x.options().dtype(torch::kUInt8));
+  mpa::dropout_fwd(bp(x), x.numel(), p, seed, offset, bpm(y), mask.data_ptr<uint8_t>(),
+                   cur_stream());
+  return {y, mask};
+}
+
+Tensor dropout_bwd(Tensor dy, Tensor mask, double p) {
+  CHECK_ACT(dy);
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = torch::empty_like(dy);
+  mpa::dropout_bwd(bp(dy), mask.data_ptr<uint8_t>(), dy.numel(), p, bpm(dx), cur_stream());
+  return dx;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "mpi_pytorch_amd native gfx950 kernels + runtime";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("act_bwd", &act_bwd);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_eval", &bn_fwd_eval);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("relu_fwd", &relu_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("adaptive_avgpool_fwd", &adaptive_avgpool_fwd);
+  m.def("adaptive_avgpool_bwd", &adaptive_avgpool_bwd);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_dgrad", &linear_dgrad);
+  m.def("linear_wgrad", &linear_wgrad);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("argmax_correct", &argmax_correct);
+  m.def("adam_step", &adam_step);
+  m.def("sgd_step", &sgd_step);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("preprocess", &preprocess);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd", &dropout_bwd);
+  mpa_runtime::register_bindings(m);
+}

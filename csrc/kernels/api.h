@@ -1,0 +1,122 @@
+// Host-side launcher API of the gfx950 kernel library.  Plain pointers + POD argument
+// structs, no torch headers: the .hip translation units compile in seconds and the
+// torch-facing binding layer (csrc/bindings.cpp) validates shapes and allocates.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpa {
+
+typedef uint16_t bf16_raw;
+constexpr int MAXT = 128;  // max taps in one implicit-GEMM launch (11x11 = 121)
+
+struct Taps {
+  short dh[MAXT];
+  short dw[MAXT];
+  short bt[MAXT];
+};
+
+// implicit GEMM whose rows are pixels of a gathered NHWC tensor (conv fwd / dgrad / linear)
+struct IGemmArgs {
+  const bf16_raw* A;
+  int aH, aW, aC;
+  int oH, oW;
+  int M;
+  int Uh, Uw, Oh, Ow;
+  int T;
+  int Ktot;
+  const bf16_raw* B;
+  int N;
+  int RS;
+  int ldb;
+  void* C;
+  int ldc;
+  int dH, dW, Uoh, Uow, Poh, Pow;
+  const float* bias;
+  float* stats;
+  int relu;
+  int ktiles_per_split;
+  int tiles_n;
+  int tiles_total;
+  Taps taps;
+};
+
+struct WGradArgs {
+  const bf16_raw* dy;
+  const bf16_raw* x;
+  float* dw;
+  int Kout, C, H, W, P, Q, R, S, sh, sw, ph, pw;
+  int Mpix;
+  int Ncols;
+  int ktiles_per_split;
+  int tiles_n, tiles_total;
+};
+
+// igemm.hip
+void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s);        // B K-contiguous
+void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-contiguous
+void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
+bool igemm_wants_split(int M, int N, int Ktot);  // true => pass an M*N fp32 workspace
+
+// bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
+void bn_stats(const bf16_raw* x, int M, int C, float* stats, hipStream_t s);
+void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
+                  float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
+                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s);
+void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
+                 const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
+                 bf16_raw* y, hipStream_t s);
+void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
+            const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
+            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s);
+void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
+             hipStream_t s);
+void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s);
+
+// pool.hip  (NHWC)
+void maxpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                 int sh, int sw, int ph, int pw, bf16_raw* y, uint8_t* idx, hipStream_t s);
+void maxpool_bwd(const bf16_raw* dy, const uint8_t* idx, int N, int H, int W, int C, int P,
+                 int Q, int kh, int kw, int sh, int sw, int ph, int pw, bf16_raw* dx,
+                 hipStream_t s);
+void avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                 int sh, int sw, int ph, int pw, int count_include_pad, bf16_raw* y,
+                 hipStream_t s);
+void avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                 int sh, int sw, int ph, int pw, int count_include_pad, bf16_raw* dx,
+                 hipStream_t s);
+void adaptive_avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q,
+                          bf16_raw* y, hipStream_t s);
+void adaptive_avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q,
+                          bf16_raw* dx, hipStream_t s);
+
+// loss.hip
+void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, float* loss,
+            float* lse, hipStream_t s);
+void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,
+            const float* grad_out, int B, int NC, bf16_raw* dlogits, hipStream_t s);
+void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC,
+                    int64_t* count, hipStream_t s);
+
+// optim.hip (flat fp32 arenas)
+void adam_step(float* p, const float* g, float* m, float* v, bf16_raw* shadow,
+               const float* step, int64_t n, float lr, float b1, float b2, float eps, float wd,
+               float grad_scale, hipStream_t s);
+void sgd_step(float* p, const float* g, float* buf, bf16_raw* shadow, const float* step,
+              int64_t n, float lr, float momentum, float dampening, float wd, int nesterov,
+              float grad_scale, hipStream_t s);
+void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s);
+
+// preprocess.hip
+struct Norm3 {
+  float mean[3];
+  float std[3];
+};
+void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
+                int cpad, bf16_raw* out, hipStream_t s);
+void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,
+                 bf16_raw* y, uint8_t* mask, hipStream_t s);
+void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,
+                 hipStream_t s);
+
+}  // namespace mpa

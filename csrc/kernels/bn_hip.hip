@@ -1,0 +1,375 @@
+#include "hip/hip_runtime.h"
+// BatchNorm (train/eval, fwd/bwd) with fused residual add + ReLU, activation backward with
+// fused bias-gradient reduction, and ReLU.  NHWC => a [M][C] row-major matrix with C
+// contiguous; every kernel moves 16-B (8 x bf16) chunks.
+//
+// Thread mapping (all kernels): a block owns up to 256 8-channel chunk columns
+// (blockIdx.y selects the column window) and sweeps rows; each thread keeps the SAME 8
+// channels for its whole life, so per-channel coefficients live in registers and
+// per-channel sums accumulate in registers, reduced once per block through LDS and
+// added with one fp32 atomic per channel per block.
+//
+// Reference ops replaced: ATen batch_norm train/eval + backward, relu, residual add
+// (SURVEY.md §2.5, K4/K5/K8).  BN statistics of conv outputs arrive pre-reduced from the
+// implicit-GEMM epilogue (igemm.hip), so the forward is a single read+write pass.
+#include "common.h"
+#include "api.h"
+#include <algorithm>
+
+namespace mpa {
+
+struct ColMap {
+  int cw, rpi, cc, r0;
+  bool active;
+};
+
+__device__ __forceinline__ ColMap colmap(int cpr) {
+  ColMap m;
+  const int y0 = blockIdx.y * 256;
+  m.cw = min(256, cpr - y0);
+  m.rpi = 256 / m.cw;
+  m.cc = y0 + (int)threadIdx.x % m.cw;
+  m.r0 = (int)threadIdx.x / m.cw;
+  m.active = m.r0 < m.rpi;
+  return m;
+}
+
+static dim3 grid_for(int M, int C, int target = 2048) {
+  const int cpr = C / 8;
+  const int gy = (cpr + 255) / 256;
+  const int cw = std::min(256, cpr);
+  const int rpi = 256 / cw;
+  int gx = (M + rpi - 1) / rpi;
+  gx = std::max(1, std::min(gx, std::max(1, target / gy)));
+  return dim3(gx, gy);
+}
+
+// block-reduce 8-channel partials held per thread; returns sums in threads with r0 == 0
+__device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float* red) {
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = cm.active ? v[j] : 0.f;
+  __syncthreads();
+  if (cm.active && cm.r0 == 0) {
+    for (int r = 1; r < cm.rpi; ++r) {
+      const int t = r * cm.cw + (threadIdx.x % cm.cw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += red[t * 8 + j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------- statistics
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, int M,
+                                                        int C, float* __restrict__ stats) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  if (cm.active) {
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+      float f[8];
+      unpack8(*(const uint4*)(x + (size_t)r * C + cm.cc * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+    }
+  }
+  block_reduce8(s, cm, red);
+  block_reduce8(q, cm, red);
+  if (cm.active && cm.r0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(stats + cm.cc * 8 + j, s[j]);
+      atomicAdd(stats + C + cm.cc * 8 + j, q[j]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------- forward (train)
+__global__ __launch_bounds__(256) void bn_fwd_train_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
+    bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float sc[8], sh[8];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float mu = stats[c0 + j] * invM;
+    const float var = fmaxf(stats[C + c0 + j] * invM - mu * mu, 0.f);
+    const float rs = rsqrtf(var + eps);
+    sc[j] = gamma[c0 + j] * rs;
+    sh[j] = beta[c0 + j] - mu * sc[j];
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+      mean_out[c0 + j] = mu;
+      rstd_out[c0 + j] = rs;
+      const float unb = var * ((float)M / (float)max(M - 1, 1));
+      rmean[c0 + j] = (1.f - momentum) * rmean[c0 + j] + momentum * mu;
+      rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
+    }
+  }
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+    const size_t off = (size_t)r * C + c0;
+    float f[8];
+    unpack8(*(const uint4*)(x + off), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+    if (res) {
+      float g[8];
+      unpack8(*(const uint4*)(res + off), g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += g[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *(uint4*)(y + off) = pack8(f);
+  }
+}
+
+// -------------------------------------------------------------------- forward (eval)
+__global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
+    const bf16_t* __restrict__ res, int relu, int M, int C, bf16_t* __restrict__ y) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float rs = rsqrtf(rvar[c0 + j] + eps);
+    sc[j] = gamma[c0 + j] * rs;
+    sh[j] = beta[c0 + j] - rmean[c0 + j] * sc[j];
+  }
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+    const size_t off = (size_t)r * C + c0;
+    float f[8];
+    unpack8(*(const uint4*)(x + off), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+    if (res) {
+      float g[8];
+      unpack8(*(const uint4*)(res + off), g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += g[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *(uint4*)(y + off) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------------- backward
+// pass 1: ws[0:C] += sum(g), ws[C:2C] += sum(g * xhat), g = dy * (y > 0 if relu)
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd, int M, int C,
+    float* __restrict__ ws) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    float mu[8], rs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+      const size_t off = (size_t)r * C + c0;
+      float g[8], xv[8];
+      unpack8(*(const uint4*)(dy + off), g);
+      unpack8(*(const uint4*)(x + off), xv);
+      if (y) {
+        float yv[8];
+        unpack8(*(const uint4*)(y + off), yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] += g[j];
+        sgx[j] += g[j] * (xv[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  block_reduce8(sg, cm, red);
+  block_reduce8(sgx, cm, red);
+  if (cm.active && cm.r0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(ws + cm.cc * 8 + j, sg[j]);
+      atomicAdd(ws + C + cm.cc * 8 + j, sgx[j]);
+    }
+  }
+}
+
+// pass 2: dx = a*g + b + c*x ; optionally write g (residual-branch gradient); block 0
+// folds the sums into dgamma/dbeta.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ ws, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int M, int C, bf16_t* __restrict__ dx, bf16_t* __restrict__ gout) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float a[8], b[8], cco[8];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sg = ws[c0 + j], sgx = ws[C + c0 + j];
+    const float rs = rstd[c0 + j];
+    const float sc = gamma[c0 + j] * rs;
+    a[j] = sc;
+    cco[j] = -sc * rs * sgx * invM;
+    b[j] = -sc * sg * invM - cco[j] * mean[c0 + j];
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+      if (dgamma) dgamma[c0 + j] += sgx;
+      if (dbeta) dbeta[c0 + j] += sg;
+    }
+  }
+  if (!dx && !gout) return;
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+    const size_t off = (size_t)r * C + c0;
+    float g[8];
+    const uint4 graw = *(const uint4*)(dy + off);
+    unpack8(graw, g);
+    if (y) {
+      float yv[8];
+      unpack8(*(const uint4*)(y + off), yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      if (gout) *(uint4*)(gout + off) = pack8(g);
+    } else if (gout) {
+      *(uint4*)(gout + off) = graw;
+    }
+    if (dx) {
+      float xv[8];
+      unpack8(*(const uint4*)(x + off), xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
+      *(uint4*)(dx + off) = pack8(xv);
+    }
+  }
+}
+
+// g = dy * (y > 0) ; dbias += colsum(g)
+__global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                       const bf16_t* __restrict__ y,
+                                                       float* __restrict__ dbias, int M, int C,
+                                                       bf16_t* __restrict__ g) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+      const size_t off = (size_t)r * C + c0;
+      float f[8];
+      unpack8(*(const uint4*)(dy + off), f);
+      if (y) {
+        float yv[8];
+        unpack8(*(const uint4*)(y + off), yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = yv[j] > 0.f ? f[j] : 0.f;
+        *(uint4*)(g + off) = pack8(f);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+  if (!dbias) return;
+  block_reduce8(s, cm, red);
+  if (cm.active && cm.r0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(dbias + cm.cc * 8 + j, s[j]);
+  }
+}
+
+// any C (e.g. a 64,500-wide classifier head): one thread per column, rows in a loop
+__global__ __launch_bounds__(256) void act_bwd_generic_kernel(const bf16_t* __restrict__ dy,
+                                                               const bf16_t* __restrict__ y,
+                                                               float* __restrict__ dbias, int M,
+                                                               int C, bf16_t* __restrict__ g) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < M; ++r) {
+    const size_t off = (size_t)r * C + c;
+    float f = bf2f(dy[off]);
+    if (y) {
+      f = bf2f(y[off]) > 0.f ? f : 0.f;
+      g[off] = f2bf(f);
+    }
+    s += f;
+  }
+  if (dbias) dbias[c] += s;
+}
+
+__global__ void relu_kernel(const bf16_t* __restrict__ x, int64_t n8, bf16_t* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(((const uint4*)x)[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    ((uint4*)y)[i] = pack8(f);
+  }
+}
+
+// ------------------------------------------------------------------------ launchers
+void bn_stats(const bf16_raw* x, int M, int C, float* stats, hipStream_t s) {
+  hipLaunchKernelGGL(bn_stats_kernel, grid_for(M, C), dim3(256), 0, s, x, M, C, stats);
+}
+
+void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
+                  float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
+                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_train_kernel, grid_for(M, C), dim3(256), 0, s, x, stats, gamma,
+                     beta, rmean, rvar, momentum, eps, res, relu, M, C, y, mean, rstd);
+}
+
+void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
+                 const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
+                 bf16_raw* y, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_eval_kernel, grid_for(M, C), dim3(256), 0, s, x, gamma, beta, rmean,
+                     rvar, eps, res, relu, M, C, y);
+}
+
+void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
+            const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
+            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s) {
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C, s);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid_for(M, C), dim3(256), 0, s, dy, x, y, mean, rstd,
+                     M, C, ws);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid_for(M, C), dim3(256), 0, s, dy, x, y, mean, rstd,
+                     gamma, ws, dgamma, dbeta, M, C, dx, g);
+}
+
+void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
+             hipStream_t s) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(act_bwd_kernel, grid_for(M, C), dim3(256), 0, s, dy, y, dbias, M, C, g);
+  else
+    hipLaunchKernelGGL(act_bwd_generic_kernel, dim3((C + 255) / 256), dim3(256), 0, s, dy, y,
+                       dbias, M, C, g);
+}
+
+void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+  hipLaunchKernelGGL(relu_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, s, x, n8, y);
+}
+
+}  // namespace mpa

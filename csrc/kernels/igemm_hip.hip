@@ -1,0 +1,773 @@
+#include "hip/hip_runtime.h"
+// Implicit-GEMM convolution / linear engine on CDNA4 MFMA (gfx950, wave64).
+//
+// One engine serves every GEMM-shaped op the reference reaches through ATen
+// (SURVEY.md §2.7 K1/K2/K3/K9): conv forward, conv dgrad, conv wgrad and Linear
+// fwd/dgrad/wgrad.  Activations are NHWC bf16, conv weights KRSC bf16, accumulation fp32
+// on v_mfma_f32_16x16x32_bf16.
+//
+//  * fwd / dgrad kernel ("igemm_rows"): GEMM rows = output pixels (gathered im2col rows of
+//    an NHWC tensor, K-contiguous), GEMM cols = output channels.  A per-launch TAP TABLE
+//    (dh, dw, weight-tap) describes the gather, so one kernel covers every kernel shape
+//    (7x7, 11x11, 1x7/7x1 asymmetric, 1x1) and, for dgrad, every stride phase of a strided
+//    conv (sub-pixel decomposition: each output phase is a stride-1 conv over the valid
+//    taps only - no zero-stuffed MFMA work).  Weights are read K-contiguous (fwd, [K][RSC])
+//    or N-contiguous (dgrad: B(kk=(tap,k), n=c) = w[k][tap][c]) through the hardware
+//    transpose read ds_read_b64_tr_b16 - no transposed weight copy is ever materialised.
+//    Epilogue: +bias, ReLU, bf16 store of 4 consecutive channels per lane (the MFMA is
+//    issued with the channel operand first so each lane owns 4 adjacent channels), and
+//    per-channel BatchNorm sum / sum-of-squares reduced in-wave and added with one fp32
+//    atomic per channel per wave (K4's statistics pass disappears).
+//  * wgrad kernel ("igemm_wgrad"): GEMM rows = output channels, cols = (r,s,c), reduction
+//    over pixels.  Both operands are pixel-major in memory, so both are staged
+//    [pixel][channel] in LDS and read as MFMA fragments with ds_read_b64_tr_b16.  Split-K
+//    over pixels with fp32 atomic accumulation straight into the flat gradient arena.
+//
+// LDS images are XOR-swizzled so fragment reads are bank-conflict free (derivation in
+// docs/KERNELS.md); staging is register double-buffered: global loads for tile k+1 are in
+// flight while tile k's MFMAs run, one barrier per K-step.  Blocks are remapped so tiles
+// sharing an operand panel land on the same XCD (private L2).
+#include <algorithm>
+#include "common.h"
+#include "api.h"
+
+namespace mpa {
+
+__device__ __forceinline__ u32x4 u32x4_make(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return u32x4{a, b, c, d};
+}
+
+constexpr int BK = 32;
+
+// ---------------------------------------------------------------------- LDS swizzles
+// K-contiguous image: [rows][32] bf16, 64-B rows, 4 x 16-B chunks per row.
+__device__ __forceinline__ int kc_off(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((4 - ((row >> 2) & 3)) & 3)) << 4);
+}
+
+// N-contiguous image: [32 k-rows][COLS] bf16.  Chunk XOR keeps 8-B granules intact for
+// the transposed read and spreads the 8 rows read by one 32-lane half over all banks.
+template <int COLS>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (COLS >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else if constexpr (COLS == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  else return 2 * ((k >> 3) & 1);
+}
+template <int COLS>
+__device__ __forceinline__ int mn_off(int k, int col) {
+  const int chunk = col >> 3;
+  return k * (COLS * 2) + (((chunk ^ mn_swz<COLS>(k))) << 4) + ((col & 7) << 1);
+}
+
+// fragment (8 consecutive k of one row) from a K-contiguous image
+__device__ __forceinline__ bf16x8 frag_kc(const char* img, int row, int lane) {
+  const u32x4 v = *LDS_PTR(const u32x4, img + kc_off(row, lane >> 4));
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// fragment (8 consecutive k of one column) from an N-contiguous image, two tr reads
+template <int COLS>
+__device__ __forceinline__ bf16x8 frag_mn(const char* img, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int col = col0 + 4 * pp;
+  const int k0 = 8 * g + q;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0 + 4, col)));
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------- vector loaders
+// Load 8 consecutive bf16 (one 16-B chunk) with VW-wide accesses.  `nv` = number of
+// valid leading elements (0..8); VW=8 callers guarantee nv is 0 or 8 (alignment).
+template <int VW>
+__device__ __forceinline__ u32x4 ld_chunk(const bf16_t* p, int nv) {
+  u32x4 r = u32x4{0, 0, 0, 0};
+  if constexpr (VW == 8) {
+    if (nv >= 8) r = *(const u32x4*)p;
+  } else if constexpr (VW == 4) {
+    if (nv >= 4) {
+      const u32x2 a = *(const u32x2*)p;
+      r.x = a.x; r.y = a.y;
+    }
+    if (nv >= 8) {
+      const u32x2 b = *(const u32x2*)(p + 4);
+      r.z = b.x; r.w = b.y;
+    }
+  } else {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < nv) w[i >> 1] |= (uint32_t)p[i] << (16 * (i & 1));
+    r = u32x4{w[0], w[1], w[2], w[3]};
+  }
+  return r;
+}
+
+__device__ __forceinline__ int nvalid(int idx, int lim) {
+  const int d = lim - idx;
+  return d <= 0 ? 0 : (d >= 8 ? 8 : d);
+}
+
+// ======================================================================================
+//  fwd / dgrad kernel
+// ======================================================================================
+template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
+__global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
+  constexpr int NA = BM / 64;                 // A chunks / thread
+  constexpr int A_BYTES = BM * 64;
+  constexpr int B_BYTES = BN * 64;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  constexpr int NB_KC = (BN * 4 + 255) / 256;  // B chunks / thread (K-contig)
+  constexpr int CPR = BN / 8;                  // N-contig: chunks per k-row
+  constexpr int NB_MN = (BK * CPR + 255) / 256;
+  constexpr int NB = BKC ? NB_KC : NB_MN;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int ktiles = (p.Ktot + BK - 1) / BK;
+  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+
+  // ---- per-thread A rows (fixed for the whole K loop)
+  const int akc = tid & 3;
+  int a_img[NA], a_bh[NA], a_bw[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + (tid >> 2) + 64 * i;
+    if (m < p.M) {
+      const int hw = p.oH * p.oW;
+      const int img = m / hw;
+      const int r = m - img * hw;
+      const int oh = r / p.oW;
+      const int ow = r - oh * p.oW;
+      a_img[i] = img * p.aH * p.aW;
+      a_bh[i] = oh * p.Uh + p.Oh;
+      a_bw[i] = ow * p.Uw + p.Ow;
+    } else {
+      a_img[i] = -1;
+      a_bh[i] = 0;
+      a_bw[i] = 0;
+    }
+  }
+
+  u32x4 ra[NA], rb[NB];
+
+  auto load_A = [&](int kt) {
+    const int kk0 = kt * BK + akc * 8;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (VW == 8) {
+        const int t = kk0 / p.aC;
+        const int c = kk0 - t * p.aC;
+        bool ok = (a_img[i] >= 0) && (kk0 < p.Ktot);
+        int ih = 0, iw = 0;
+        if (ok) {
+          ih = a_bh[i] + p.taps.dh[t];
+          iw = a_bw[i] + p.taps.dw[t];
+          ok = (unsigned)ih < (unsigned)p.aH && (unsigned)iw < (unsigned)p.aW;
+        }
+        ra[i] = ld_chunk<8>(p.A + (size_t)(a_img[i] + ih * p.aW + iw) * p.aC + c, ok ? 8 : 0);
+      } else {
+        constexpr int SUB = (VW == 4) ? 2 : 8;
+        constexpr int SW = 8 / SUB;
+        uint16_t e[8];
+#pragma unroll
+        for (int s = 0; s < SUB; ++s) {
+          const int kk = kk0 + s * SW;
+          const int t = kk / p.aC;
+          const int c = kk - t * p.aC;
+          bool ok = (a_img[i] >= 0) && (kk < p.Ktot);
+          int ih = 0, iw = 0;
+          if (ok) {
+            ih = a_bh[i] + p.taps.dh[t];
+            iw = a_bw[i] + p.taps.dw[t];
+            ok = (unsigned)ih < (unsigned)p.aH && (unsigned)iw < (unsigned)p.aW;
+          }
+          const bf16_t* src = p.A + (size_t)(a_img[i] + ih * p.aW + iw) * p.aC + c;
+          if constexpr (SW == 4) {
+            u32x2 v = u32x2{0u, 0u};
+            if (ok) v = *(const u32x2*)src;
+            e[4 * s] = v.x & 0xffff; e[4 * s + 1] = v.x >> 16;
+            e[4 * s + 2] = v.y & 0xffff; e[4 * s + 3] = v.y >> 16;
+          } else {
+            e[s] = ok ? src[0] : (uint16_t)0;
+          }
+        }
+        ra[i] = u32x4_make(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
+                           e[6] | (e[7] << 16));
+      }
+    }
+  };
+
+  auto load_B = [&](int kt) {
+    if constexpr (BKC) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = tid + 256 * i;
+        const int row = c >> 2, kc = c & 3;
+        const int n = n0 + row;
+        const int kk = kt * BK + kc * 8;
+        if constexpr (VW == 1) {
+          uint16_t e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            e[j] = (row < BN && n < p.N && kk + j < p.Ktot) ? p.B[(size_t)n * p.ldb + kk + j] : 0;
+          rb[i] = u32x4_make(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
+                             e[6] | (e[7] << 16));
+        } else {
+          const bool ok = (row < BN) && (n < p.N);
+          rb[i] = ld_chunk<VW>(p.B + (size_t)n * p.ldb + kk, ok ? nvalid(kk, p.Ktot) : 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = tid + 256 * i;
+        const int krow = c / CPR, cc = c % CPR;
+        const int kk = kt * BK + krow;
+        const int n = n0 + cc * 8;
+        const bool ok = (krow < BK) && (kk < p.Ktot) && (n < p.N);
+        int t = 0, k = 0;
+        if (ok) {
+          t = kk / p.aC;
+          k = kk - t * p.aC;
+        }
+        rb[i] = ld_chunk<VW>(p.B + ((size_t)k * p.RS + p.taps.bt[t]) * p.ldb + n,
+                              ok ? nvalid(n, p.N) : 0);
+      }
+    }
+  };
+
+  auto store_tiles = [&](char* st) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = (tid >> 2) + 64 * i;
+      *LDS_PTR(u32x4, st + kc_off(row, akc)) = ra[i];
+    }
+    char* bimg = st + A_BYTES;
+    if constexpr (BKC) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = tid + 256 * i;
+        const int row = c >> 2, kc = c & 3;
+        if (row < BN) *LDS_PTR(u32x4, bimg + kc_off(row, kc)) = rb[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = tid + 256 * i;
+        const int krow = c / CPR, cc = c % CPR;
+        if (krow < BK) *LDS_PTR(u32x4, bimg + mn_off<BN>(krow, cc * 8)) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wrow0 = wm * (BM / WM);
+  const int wcol0 = wn * (BN / WN);
+
+  if (kbeg < kend) {
+    load_A(kbeg);
+    load_B(kbeg);
+    store_tiles(smem);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+      const bool more = kt + 1 < kend;
+      if (more) {
+        load_A(kt + 1);
+        load_B(kt + 1);
+      }
+      const char* st = smem + cur * STAGE;
+      const char* bimg = st + A_BYTES;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_kc(st, wrow0 + i * 16 + (lane & 15), lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (BKC) bfr[j] = frag_kc(bimg, wcol0 + j * 16 + (lane & 15), lane);
+        else bfr[j] = frag_mn<BN>(bimg, wcol0 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      if (more) store_tiles(smem + (cur ^ 1) * STAGE);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---- epilogue: lane owns D[n = nb + r][m = lane&15], r = 0..3
+  const int nl = (lane >> 4) * 4;
+  if constexpr (SPLIT) {
+    float* out = (float*)p.C;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wrow0 + i * 16 + (lane & 15);
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wcol0 + j * 16 + nl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) atomicAdd(out + (size_t)m * p.ldc + n + r, acc[i][j][r]);
+      }
+    }
+    return;
+  } else {
+    bf16_t* out = (bf16_t*)p.C;
+    float s[TN][4], q[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
+    f32x4 bias[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int n = n0 + wcol0 + j * 16 + nl;
+      if (p.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? p.bias[n + r] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wrow0 + i * 16 + (lane & 15);
+      const bool mok = m < p.M;
+      size_t orow = 0;
+      if (mok) {
+        const int hw = p.oH * p.oW;
+        const int img = m / hw;
+        const int rr = m - img * hw;
+        const int oh = rr / p.oW;
+        const int ow = rr - oh * p.oW;
+        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + p.Poh) * p.dW +
+                (ow * p.Uow + p.Pow)) * p.ldc;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wcol0 + j * 16 + nl;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[i][j][r] + bias[j][r];
+          if (p.relu) t = fmaxf(t, 0.f);
+          v[r] = t;
+        }
+        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+        if (mok) {
+          if (n + 3 < p.N) {
+            *(uint2*)(out + orow + n) = make_uint2(lo, hi);
+          } else {
+            const uint16_t e[4] = {(uint16_t)(lo & 0xffff), (uint16_t)(lo >> 16),
+                                   (uint16_t)(hi & 0xffff), (uint16_t)(hi >> 16)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) out[orow + n + r] = e[r];
+          }
+          // statistics on the bf16-rounded values BN will read
+          const float rv[4] = {bf2f(lo & 0xffff), bf2f(lo >> 16), bf2f(hi & 0xffff),
+                               bf2f(hi >> 16)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[j][r] += rv[r];
+            q[j][r] += rv[r] * rv[r];
+          }
+        }
+      }
+    }
+    if (p.stats) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = s[j][r], b = q[j][r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+          }
+          s[j][r] = a;
+          q[j][r] = b;
+        }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wcol0 + j * 16 + nl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) {
+              atomicAdd(p.stats + n + r, s[j][r]);
+              atomicAdd(p.stats + p.N + n + r, q[j][r]);
+            }
+        }
+      }
+    }
+  }
+}
+
+// ======================================================================================
+//  wgrad kernel: dW[m = kout][n = (r,s,c)] += sum_pix dy[pix][m] * im2col(x)[pix][n]
+// ======================================================================================
+template <int BM, int BN, int WM, int WN, int VWA, int VWB>
+__global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
+  constexpr int A_BYTES = BK * BM * 2;
+  constexpr int B_BYTES = BK * BN * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CPRA = BM / 8, CPRB = BN / 8;
+  constexpr int NA = (BK * CPRA + 255) / 256;
+  constexpr int NB = (BK * CPRB + 255) / 256;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (p.Mpix + BK - 1) / BK;
+  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+  if (kbeg >= kend) return;
+
+  // ---- B column decode (fixed per thread): n -> (r, s, c)
+  constexpr int NE = (VWB == 1) ? 8 : 1;
+  int b_dh[NB][NE], b_dw[NB][NE], b_c[NB][NE];
+  bool b_ok[NB][NE];
+  // pixel iterators (incremental), one per B chunk
+  int pix_img[NB], pix_oh[NB], pix_ow[NB];
+  const int PQ = p.P * p.Q;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int c = tid + 256 * i;
+    const int krow = c / CPRB, cc = c % CPRB;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int n = n0 + cc * 8 + e;
+      const int tap = n / p.C;
+      const int ch = n - tap * p.C;
+      const int r = tap / p.S, s = tap - (tap / p.S) * p.S;
+      b_dh[i][e] = r - p.ph;
+      b_dw[i][e] = s - p.pw;
+      b_c[i][e] = ch;
+      b_ok[i][e] = (krow < BK) && (n < p.Ncols);
+    }
+    const int pix = kbeg * BK + krow;
+    const int img = pix / PQ;
+    const int rr = pix - img * PQ;
+    pix_img[i] = img;
+    pix_oh[i] = rr / p.Q;
+    pix_ow[i] = rr - (rr / p.Q) * p.Q;
+  }
+
+  u32x4 ra[NA], rb[NB];
+
+  auto load_A = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + 256 * i;
+      const int krow = c / CPRA, cc = c % CPRA;
+      const int pix = kt * BK + krow;
+      const int m = m0 + cc * 8;
+      const bool ok = (krow < BK) && (pix < p.Mpix);
+      ra[i] = ld_chunk<VWA>(p.dy + (size_t)pix * p.Kout + m, ok ? nvalid(m, p.Kout) : 0);
+    }
+  };
+
+  auto load_B = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + 256 * i;
+      const int krow = c / CPRB;
+      const int pix = kt * BK + krow;
+      const bool pok = (krow < BK) && (pix < p.Mpix);
+      const int bh = pix_oh[i] * p.sh, bw = pix_ow[i] * p.sw;
+      const size_t ibase = (size_t)pix_img[i] * p.H * p.W;
+      if constexpr (VWB == 1) {
+        uint16_t e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ih = bh + b_dh[i][j], iw = bw + b_dw[i][j];
+          const bool ok = pok && b_ok[i][j] && (unsigned)ih < (unsigned)p.H &&
+                          (unsigned)iw < (unsigned)p.W;
+          e[j] = ok ? p.x[(ibase + ih * p.W + iw) * p.C + b_c[i][j]] : (uint16_t)0;
+        }
+        rb[i] = u32x4_make(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
+                           e[6] | (e[7] << 16));
+      } else {
+        const int ih = bh + b_dh[i][0], iw = bw + b_dw[i][0];
+        const bool ok = pok && b_ok[i][0] && (unsigned)ih < (unsigned)p.H &&
+                        (unsigned)iw < (unsigned)p.W;
+        rb[i] = ld_chunk<VWB>(p.x + (ibase + ih * p.W + iw) * p.C + b_c[i][0], ok ? 8 : 0);
+      }
+      // advance this chunk's pixel by BK for the next K-step
+      int ow = pix_ow[i] + BK, oh = pix_oh[i], img = pix_img[i];
+      while (ow >= p.Q) { ow -= p.Q; ++oh; }
+      while (oh >= p.P) { oh -= p.P; ++img; }
+      pix_ow[i] = ow; pix_oh[i] = oh; pix_img[i] = img;
+    }
+  };
+
+  auto store_tiles = [&](char* st) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + 256 * i;
+      const int krow = c / CPRA, cc = c % CPRA;
+      if (krow < BK) *LDS_PTR(u32x4, st + mn_off<BM>(krow, cc * 8)) = ra[i];
+    }
+    char* bimg = st + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + 256 * i;
+      const int krow = c / CPRB, cc = c % CPRB;
+      if (krow < BK) *LDS_PTR(u32x4, bimg + mn_off<BN>(krow, cc * 8)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wrow0 = wm * (BM / WM);
+  const int wcol0 = wn * (BN / WN);
+
+  load_A(kbeg);
+  load_B(kbeg);
+  store_tiles(smem);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = kbeg; kt < kend; ++kt) {
+    const bool more = kt + 1 < kend;
+    if (more) {
+      load_A(kt + 1);
+      load_B(kt + 1);
+    }
+    const char* st = smem + cur * STAGE;
+    const char* bimg = st + A_BYTES;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag_mn<BM>(st, wrow0 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag_mn<BN>(bimg, wcol0 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    if (more) store_tiles(smem + (cur ^ 1) * STAGE);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // lane owns D[m = mb + r][n = lane&15]
+  const int ml = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wcol0 + j * 16 + (lane & 15);
+      if (n >= p.Ncols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wrow0 + i * 16 + ml + r;
+        if (m < p.Kout) atomicAdd(p.dw + (size_t)m * p.Ncols + n, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------- split-K finalize (fp32->bf16)
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
+                                       int M, int N, const float* __restrict__ bias, int relu,
+                                       float* __restrict__ stats) {
+  // one block per 64 columns x (rows strided by gridDim.y)
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * 4 + (threadIdx.x >> 6);
+  float s = 0.f, q = 0.f;
+  const float b = (bias && n < N) ? bias[n] : 0.f;
+  if (n < N) {
+    for (int m = r0; m < M; m += gridDim.y * 4) {
+      float v = ws[(size_t)m * N + n] + b;
+      if (relu) v = fmaxf(v, 0.f);
+      const bf16_t o = f2bf(v);
+      out[(size_t)m * N + n] = o;
+      const float rv = bf2f(o);
+      s += rv;
+      q += rv * rv;
+    }
+    if (stats) {
+      atomicAdd(stats + n, s);
+      atomicAdd(stats + N + n, q);
+    }
+  }
+}
+
+// ======================================================================================
+//  host-side launch logic
+// ======================================================================================
+template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
+static void launch_rows(const IGemmArgs& a, int splits, hipStream_t s) {
+  dim3 grid(a.tiles_total, 1, splits);
+  hipLaunchKernelGGL((igemm_rows_kernel<BM, BN, WM, WN, VW, BKC, SPLIT>), grid, dim3(256), 0, s,
+                     a);
+}
+
+template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT>
+static void dispatch_vw(const IGemmArgs& a, int vw, int splits, hipStream_t s) {
+  if (vw == 8) launch_rows<BM, BN, WM, WN, 8, BKC, SPLIT>(a, splits, s);
+  else if (vw == 4) launch_rows<BM, BN, WM, WN, 4, BKC, SPLIT>(a, splits, s);
+  else launch_rows<BM, BN, WM, WN, 1, BKC, SPLIT>(a, splits, s);
+}
+
+template <int BM, int BN, int WM, int WN, bool BKC>
+static void dispatch_split(const IGemmArgs& a, int vw, int splits, hipStream_t s) {
+  if (splits > 1) dispatch_vw<BM, BN, WM, WN, BKC, true>(a, vw, splits, s);
+  else dispatch_vw<BM, BN, WM, WN, BKC, false>(a, vw, splits, s);
+}
+
+static int choose_bn(int N) {
+  if (N <= 32) return 32;
+  if (N <= 64 || (N % 128 != 0 && N % 64 == 0 && N < 256)) return 64;
+  return 128;
+}
+
+// rows engine: fills tiling fields, picks split-K, launches.  `ws` is an fp32 workspace
+// of M*N floats (zeroed here) used when split-K is chosen; when ws == nullptr split-K is
+// disabled (strided output mappings).
+// Split-K only while the fp32-atomic reduction bytes stay well below the MFMA work:
+// FLOP per atomic byte = Ktot / (2*splits) must exceed ~2.5 PF / 1.3 TB/s (atomic rate,
+// MI355X_MICROARCH.md "Global float atomics") => splits <= Ktot / 2048.
+static int choose_splits(int tiles, int ktiles, int Ktot) {
+  if (tiles >= 512 || ktiles < 16) return 1;
+  int s = (1024 + tiles - 1) / tiles;
+  s = std::min(s, ktiles / 8);
+  s = std::min(s, std::max(1, Ktot / 2048));
+  return std::max(s, 1);
+}
+
+bool igemm_wants_split(int M, int N, int Ktot) {
+  const int BN = choose_bn(N);
+  const int BM = (BN == 64) ? 256 : 128;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  return choose_splits(tiles, (Ktot + BK - 1) / BK, Ktot) > 1;
+}
+
+void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s) {
+  const int BN = choose_bn(a.N);
+  const int BM = (BN == 64) ? 256 : 128;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_total = tiles_m * a.tiles_n;
+  const int ktiles = (a.Ktot + BK - 1) / BK;
+  int splits = ws != nullptr ? choose_splits(a.tiles_total, ktiles, a.Ktot) : 1;
+  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
+  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
+  void* final_out = a.C;
+  float* stats = a.stats;
+  if (splits > 1) {
+    (void)hipMemsetAsync(ws, 0, (size_t)a.M * a.N * sizeof(float), s);
+    a.C = ws;
+    a.ldc = a.N;
+  }
+  if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
+  else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);
+  else dispatch_split<128, 32, 4, 1, true>(a, vw, splits, s);
+  if (splits > 1) {
+    dim3 grid((a.N + 63) / 64, std::min(64, (a.M + 3) / 4));
+    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
+                       a.M, a.N, a.bias, a.relu, stats);
+  }
+}
+
+void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
+  const int BN = choose_bn(a.N);
+  const int BM = (BN == 64) ? 256 : 128;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_total = tiles_m * a.tiles_n;
+  const int ktiles = (a.Ktot + BK - 1) / BK;
+  int splits = ws != nullptr ? choose_splits(a.tiles_total, ktiles, a.Ktot) : 1;
+  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
+  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
+  void* final_out = a.C;
+  if (splits > 1) {
+    (void)hipMemsetAsync(ws, 0, (size_t)a.M * a.N * sizeof(float), s);
+    a.C = ws;
+    a.ldc = a.N;
+  }
+  if (BN == 128) dispatch_split<128, 128, 2, 2, false>(a, vw, splits, s);
+  else if (BN == 64) dispatch_split<256, 64, 4, 1, false>(a, vw, splits, s);
+  else dispatch_split<128, 32, 4, 1, false>(a, vw, splits, s);
+  if (splits > 1) {
+    dim3 grid((a.N + 63) / 64, std::min(64, (a.M + 3) / 4));
+    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
+                       a.M, a.N, (const float*)nullptr, 0, (float*)nullptr);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int VWA, int VWB>
+static void launch_wgrad(const WGradArgs& a, int splits, hipStream_t s) {
+  dim3 grid(a.tiles_total, 1, splits);
+  hipLaunchKernelGGL((igemm_wgrad_kernel<BM, BN, WM, WN, VWA, VWB>), grid, dim3(256), 0, s, a);
+}
+
+template <int BM, int BN>
+static void wgrad_vw(const WGradArgs& a, int vwa, int vwb, int splits, hipStream_t s) {
+  if (vwb == 1) {
+    if (vwa == 8) launch_wgrad<BM, BN, 2, 2, 8, 1>(a, splits, s);
+    else if (vwa == 4) launch_wgrad<BM, BN, 2, 2, 4, 1>(a, splits, s);
+    else launch_wgrad<BM, BN, 2, 2, 1, 1>(a, splits, s);
+  } else {
+    if (vwa == 8) launch_wgrad<BM, BN, 2, 2, 8, 8>(a, splits, s);
+    else if (vwa == 4) launch_wgrad<BM, BN, 2, 2, 4, 8>(a, splits, s);
+    else launch_wgrad<BM, BN, 2, 2, 1, 8>(a, splits, s);
+  }
+}
+
+void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
+  const int BM = (a.Kout <= 64) ? 64 : 128;
+  const int BN = 128;
+  a.tiles_n = (a.Ncols + BN - 1) / BN;
+  const int tiles_m = (a.Kout + BM - 1) / BM;
+  a.tiles_total = tiles_m * a.tiles_n;
+  const int ktiles = (a.Mpix + BK - 1) / BK;
+  // enough blocks to fill 256 CUs several times over; >= 16 K-steps per block so the
+  // fp32 atomic epilogue stays well under the chip-wide atomic rate
+  int splits = std::max(1, (2048 + a.tiles_total - 1) / a.tiles_total);
+  splits = std::min(splits, std::max(1, ktiles / 16));
+  splits = std::min(splits, std::max(1, a.Mpix / 2048));
+  a.ktiles_per_split = (ktiles + splits - 1) / splits;
+  splits = (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split;
+  if (BM == 64) wgrad_vw<64, 128>(a, vwa, vwb, splits, s);
+  else wgrad_vw<128, 128>(a, vwa, vwb, splits, s);
+}
+
+}  // namespace mpa

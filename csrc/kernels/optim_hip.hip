@@ -1,0 +1,113 @@
+#include "hip/hip_runtime.h"
+// Fused flat-arena optimizers (K11): ONE streaming pass over the fp32 master weights,
+// gradients and optimizer state of the whole model.  Applies the data-parallel 1/N
+// gradient scale (the average of mpi_tools.py:36 folded in), L2 weight decay, the
+// torch.optim.Adam / torch.optim.SGD update rule, and writes the bf16 weight shadow the
+// MFMA kernels read (no separate cast pass).  The step counter lives on the device so the
+// update is HIP-graph capturable.  Reference: Adam(lr=4e-4) at main.py:125,155.
+#include "common.h"
+#include "api.h"
+#include <algorithm>
+
+namespace mpa {
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16_t* __restrict__ shadow,
+                                                    const float* __restrict__ step, int64_t n4,
+                                                    float lr, float b1, float b2, float eps,
+                                                    float wd, float gs) {
+  const float t = step[0] + 1.f;
+  const float bc1 = 1.f - powf(b1, t);
+  const float bc2s = sqrtf(1.f - powf(b2, t));
+  const float step_size = lr / bc1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = ((float4*)p)[i];
+    const float4 gg = ((const float4*)g)[i];
+    float4 mm = ((float4*)m)[i];
+    float4 vv = ((float4*)v)[i];
+    float* pf = (float*)&pp;
+    const float* gf = (const float*)&gg;
+    float* mf = (float*)&mm;
+    float* vf = (float*)&vv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = gf[j] * gs;
+      if (wd != 0.f) gr += wd * pf[j];
+      mf[j] = b1 * mf[j] + (1.f - b1) * gr;
+      vf[j] = b2 * vf[j] + (1.f - b2) * gr * gr;
+      const float denom = sqrtf(vf[j]) / bc2s + eps;
+      pf[j] -= step_size * mf[j] / denom;
+    }
+    ((float4*)p)[i] = pp;
+    ((float4*)m)[i] = mm;
+    ((float4*)v)[i] = vv;
+    if (shadow) ((uint2*)shadow)[i] = make_uint2(pack2(pf[0], pf[1]), pack2(pf[2], pf[3]));
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ buf, bf16_t* __restrict__ shadow,
+                                                   const float* __restrict__ step, int64_t n4,
+                                                   float lr, float momentum, float dampening,
+                                                   float wd, int nesterov, float gs) {
+  const bool first = step[0] == 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = ((float4*)p)[i];
+    const float4 gg = ((const float4*)g)[i];
+    float4 bb = ((float4*)buf)[i];
+    float* pf = (float*)&pp;
+    const float* gf = (const float*)&gg;
+    float* bf = (float*)&bb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gr = gf[j] * gs;
+      if (wd != 0.f) gr += wd * pf[j];
+      if (momentum != 0.f) {
+        bf[j] = first ? gr : momentum * bf[j] + (1.f - dampening) * gr;
+        gr = nesterov ? gr + momentum * bf[j] : bf[j];
+      }
+      pf[j] -= lr * gr;
+    }
+    ((float4*)p)[i] = pp;
+    if (momentum != 0.f) ((float4*)buf)[i] = bb;
+    if (shadow) ((uint2*)shadow)[i] = make_uint2(pack2(pf[0], pf[1]), pack2(pf[2], pf[3]));
+  }
+}
+
+__global__ void cast_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 f = ((const float4*)x)[i];
+    ((uint2*)y)[i] = make_uint2(pack2(f.x, f.y), pack2(f.z, f.w));
+  }
+}
+
+static int blocks_for(int64_t n4) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 4096));
+}
+
+void adam_step(float* p, const float* g, float* m, float* v, bf16_raw* shadow, const float* step,
+               int64_t n, float lr, float b1, float b2, float eps, float wd, float gs,
+               hipStream_t s) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, p, g, m, v, shadow, step,
+                     n4, lr, b1, b2, eps, wd, gs);
+}
+
+void sgd_step(float* p, const float* g, float* buf, bf16_raw* shadow, const float* step,
+              int64_t n, float lr, float momentum, float dampening, float wd, int nesterov,
+              float gs, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(sgd_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, p, g, buf, shadow, step,
+                     n4, lr, momentum, dampening, wd, nesterov, gs);
+}
+
+void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(cast_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, x, y, n4);
+}
+
+}  // namespace mpa

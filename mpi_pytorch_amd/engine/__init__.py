@@ -1,0 +1,1 @@
+from .step import TrainStep, build_model, build_training, loss_fn  # noqa: F401

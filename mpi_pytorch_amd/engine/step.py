@@ -1,0 +1,132 @@
+"""The data-parallel training step (the engine's hot loop), shared by ``main.py``,
+``bench.py`` and ``__graft_entry__.smoke``.
+
+Reference hot loop (``/root/reference/main.py:142-156``): forward -> CE loss ->
+zero_grad -> backward -> per-tensor blocking Allreduce average -> Adam.step ->
+``loss.item()`` (a host sync every step).
+
+Here:
+  zero the flat gradient arena (one memset) -> forward on fused NHWC/bf16 MFMA ops ->
+  fused CE -> backward, during which each gradient bucket's RCCL all-reduce starts as
+  soon as its last gradient lands (overlap) -> wait for outstanding buckets -> ONE fused
+  optimizer kernel (1/N average folded in, bf16 weights written) -> loss accumulated on
+  the device (no per-step host sync).
+
+With ``graph=True`` the whole step (forward, backward, optimizer) is captured once into a
+HIP graph and replayed, removing per-kernel launch overhead (single-process only: the
+RCCL collectives of the multi-GPU path run eagerly and overlap with backward).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from ..models import initialize_model, InceptionOutputs
+from ..ops import functional as Fn
+from ..optim import build_optimizer
+from ..parallel import ParamArena, GradBucketer, sync_params, World
+
+
+def build_model(name: str, num_classes: int, feature_extract: bool, device: torch.device,
+                world: World, use_pretrained: bool = False, bucket_mb: float = 64.0,
+                overlap: bool = True, comm_dtype: str = "fp32"):
+    model, input_size = initialize_model(name, num_classes, feature_extract, use_pretrained)
+    model = model.to(device)
+    arena = ParamArena(model, device)
+    model._mpa_arena = arena
+    model._mpa_bucketer = GradBucketer(arena, world.world_size, bucket_mb, overlap, comm_dtype)
+    return model, input_size
+
+
+def loss_fn(out, labels):
+    """CE; Inception's train-mode (logits, aux) uses loss + 0.4 * aux_loss (the documented
+    fix of the reference's broken Inception path)."""
+    if isinstance(out, (tuple, InceptionOutputs)):
+        logits, aux = out[0], out[1]
+        loss = Fn.cross_entropy(logits, labels)
+        if aux is not None:
+            loss = loss + 0.4 * Fn.cross_entropy(aux, labels)
+        return loss
+    return Fn.cross_entropy(out, labels)
+
+
+class TrainStep:
+    def __init__(self, model: nn.Module, optimizer, world: World):
+        self.model = model
+        self.opt = optimizer
+        self.world = world
+        self.arena: ParamArena = model._mpa_arena
+        self.bucketer: GradBucketer = model._mpa_bucketer
+        self.opt.grad_scale = 1.0 / world.world_size
+        self.loss_sum: Optional[torch.Tensor] = None
+        self.steps = 0
+        self._graph = None
+        self._static_x = None
+        self._static_y = None
+        self._static_loss = None
+
+    def _eager(self, x, y):
+        self.arena.zero_grad()
+        out = self.model(x)
+        loss = loss_fn(out, y)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step()
+        return loss.detach()
+
+    def __call__(self, x, y) -> torch.Tensor:
+        if self._graph is not None:
+            self._static_x.copy_(x)
+            self._static_y.copy_(y)
+            self._graph.replay()
+            loss = self._static_loss
+        else:
+            loss = self._eager(x, y)
+        self._accumulate(loss)
+        return loss
+
+    def _accumulate(self, loss):
+        if self.loss_sum is None:
+            self.loss_sum = torch.zeros((), dtype=torch.float32, device=loss.device)
+        self.loss_sum += loss.float()
+        self.steps += 1
+
+    def mean_loss(self, reset: bool = True) -> float:
+        v = float(self.loss_sum.item()) / max(self.steps, 1) if self.loss_sum is not None else 0.0
+        if reset:
+            self.loss_sum = None
+            self.steps = 0
+        return v
+
+    # --------------------------------------------------------------------- HIP graphs
+    def capture(self, x, y, warmup: int = 2) -> bool:
+        """Capture one full step into a HIP graph (world size 1 only)."""
+        if self.world.world_size != 1 or not x.is_cuda:
+            return False
+        self._static_x = x.clone()
+        self._static_y = y.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._eager(self._static_x, self._static_y)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_loss = self._eager(self._static_x, self._static_y)
+        self._graph = g
+        return True
+
+
+def build_training(name: str, num_classes: int, device, world: World, lr: float,
+                   optimizer: str = "adam", momentum: float = 0.9, weight_decay: float = 0.0,
+                   feature_extract: bool = False, bucket_mb: float = 64.0, overlap: bool = True,
+                   comm_dtype: str = "fp32"):
+    model, input_size = build_model(name, num_classes, feature_extract, device, world,
+                                    bucket_mb=bucket_mb, overlap=overlap, comm_dtype=comm_dtype)
+    opt = build_optimizer(optimizer, model, lr, momentum, weight_decay)
+    sync_params(model)
+    model.train()
+    return model, opt, TrainStep(model, opt, world), input_size

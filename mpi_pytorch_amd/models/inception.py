@@ -1,0 +1,215 @@
+"""Inception-v3 with auxiliary head, NHWC, torchvision parameter names.
+
+Reference: ``models.inception_v3`` with ``AuxLogits.fc`` and ``fc`` replaced by
+``nn.Linear(., num_classes)`` (``/root/reference/models.py:83-95``).  In train mode the
+model returns ``(logits, aux_logits)``; the trainer uses ``loss = CE(logits) + 0.4 *
+CE(aux)`` - the reference feeds the tuple straight into ``criterion`` (``main.py:149-150``)
+which cannot work; this is the documented fix.  Every BasicConv2d
+(conv + BN(eps=1e-3) + ReLU) is one fused op; asymmetric 1x7/7x1/1x3/3x1 kernels go
+through the same implicit-GEMM engine via its tap table.
+"""
+from __future__ import annotations
+
+from collections import namedtuple
+
+import torch
+import torch.nn as nn
+
+from .layers import (Conv2d, BatchNorm2d, Linear, MaxPool2d, AdaptiveAvgPool2d, Dropout)
+from ..ops import functional as Fn
+
+InceptionOutputs = namedtuple("InceptionOutputs", ["logits", "aux_logits"])
+
+
+class BasicConv2d(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0):
+        super().__init__()
+        self.conv = Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False)
+        self.bn = BatchNorm2d(out_channels, eps=0.001)
+
+    def forward(self, x):
+        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True)
+
+
+def _avg3(x):
+    return Fn.avg_pool2d(x, (3, 3), (1, 1), (1, 1), False, True)
+
+
+def _max3s2(x):
+    return Fn.max_pool2d(x, (3, 3), (2, 2), (0, 0), False)
+
+
+def _cat(xs):
+    return torch.cat(xs, dim=-1)
+
+
+class InceptionA(nn.Module):
+    def __init__(self, in_channels, pool_features):
+        super().__init__()
+        self.branch1x1 = BasicConv2d(in_channels, 64, 1)
+        self.branch5x5_1 = BasicConv2d(in_channels, 48, 1)
+        self.branch5x5_2 = BasicConv2d(48, 64, 5, padding=2)
+        self.branch3x3dbl_1 = BasicConv2d(in_channels, 64, 1)
+        self.branch3x3dbl_2 = BasicConv2d(64, 96, 3, padding=1)
+        self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, padding=1)
+        self.branch_pool = BasicConv2d(in_channels, pool_features, 1)
+
+    def forward(self, x):
+        b1 = self.branch1x1(x)
+        b5 = self.branch5x5_2(self.branch5x5_1(x))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
+        bp = self.branch_pool(_avg3(x))
+        return _cat([b1, b5, b3, bp])
+
+
+class InceptionB(nn.Module):
+    def __init__(self, in_channels):
+        super().__init__()
+        self.branch3x3 = BasicConv2d(in_channels, 384, 3, stride=2)
+        self.branch3x3dbl_1 = BasicConv2d(in_channels, 64, 1)
+        self.branch3x3dbl_2 = BasicConv2d(64, 96, 3, padding=1)
+        self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, stride=2)
+
+    def forward(self, x):
+        b3 = self.branch3x3(x)
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
+        return _cat([b3, bd, _max3s2(x)])
+
+
+class InceptionC(nn.Module):
+    def __init__(self, in_channels, channels_7x7):
+        super().__init__()
+        c7 = channels_7x7
+        self.branch1x1 = BasicConv2d(in_channels, 192, 1)
+        self.branch7x7_1 = BasicConv2d(in_channels, c7, 1)
+        self.branch7x7_2 = BasicConv2d(c7, c7, (1, 7), padding=(0, 3))
+        self.branch7x7_3 = BasicConv2d(c7, 192, (7, 1), padding=(3, 0))
+        self.branch7x7dbl_1 = BasicConv2d(in_channels, c7, 1)
+        self.branch7x7dbl_2 = BasicConv2d(c7, c7, (7, 1), padding=(3, 0))
+        self.branch7x7dbl_3 = BasicConv2d(c7, c7, (1, 7), padding=(0, 3))
+        self.branch7x7dbl_4 = BasicConv2d(c7, c7, (7, 1), padding=(3, 0))
+        self.branch7x7dbl_5 = BasicConv2d(c7, 192, (1, 7), padding=(0, 3))
+        self.branch_pool = BasicConv2d(in_channels, 192, 1)
+
+    def forward(self, x):
+        b1 = self.branch1x1(x)
+        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x)))
+        bd = self.branch7x7dbl_1(x)
+        for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
+                  self.branch7x7dbl_5):
+            bd = m(bd)
+        bp = self.branch_pool(_avg3(x))
+        return _cat([b1, b7, bd, bp])
+
+
+class InceptionD(nn.Module):
+    def __init__(self, in_channels):
+        super().__init__()
+        self.branch3x3_1 = BasicConv2d(in_channels, 192, 1)
+        self.branch3x3_2 = BasicConv2d(192, 320, 3, stride=2)
+        self.branch7x7x3_1 = BasicConv2d(in_channels, 192, 1)
+        self.branch7x7x3_2 = BasicConv2d(192, 192, (1, 7), padding=(0, 3))
+        self.branch7x7x3_3 = BasicConv2d(192, 192, (7, 1), padding=(3, 0))
+        self.branch7x7x3_4 = BasicConv2d(192, 192, 3, stride=2)
+
+    def forward(self, x):
+        b3 = self.branch3x3_2(self.branch3x3_1(x))
+        b7 = self.branch7x7x3_1(x)
+        for m in (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4):
+            b7 = m(b7)
+        return _cat([b3, b7, _max3s2(x)])
+
+
+class InceptionE(nn.Module):
+    def __init__(self, in_channels):
+        super().__init__()
+        self.branch1x1 = BasicConv2d(in_channels, 320, 1)
+        self.branch3x3_1 = BasicConv2d(in_channels, 384, 1)
+        self.branch3x3_2a = BasicConv2d(384, 384, (1, 3), padding=(0, 1))
+        self.branch3x3_2b = BasicConv2d(384, 384, (3, 1), padding=(1, 0))
+        self.branch3x3dbl_1 = BasicConv2d(in_channels, 448, 1)
+        self.branch3x3dbl_2 = BasicConv2d(448, 384, 3, padding=1)
+        self.branch3x3dbl_3a = BasicConv2d(384, 384, (1, 3), padding=(0, 1))
+        self.branch3x3dbl_3b = BasicConv2d(384, 384, (3, 1), padding=(1, 0))
+        self.branch_pool = BasicConv2d(in_channels, 192, 1)
+
+    def forward(self, x):
+        b1 = self.branch1x1(x)
+        b3 = self.branch3x3_1(x)
+        b3 = _cat([self.branch3x3_2a(b3), self.branch3x3_2b(b3)])
+        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x))
+        bd = _cat([self.branch3x3dbl_3a(bd), self.branch3x3dbl_3b(bd)])
+        bp = self.branch_pool(_avg3(x))
+        return _cat([b1, b3, bd, bp])
+
+
+class InceptionAux(nn.Module):
+    def __init__(self, in_channels, num_classes):
+        super().__init__()
+        self.conv0 = BasicConv2d(in_channels, 128, 1)
+        self.conv1 = BasicConv2d(128, 768, 5)
+        self.conv1.stddev = 0.01
+        self.fc = Linear(768, num_classes)
+        self.fc.stddev = 0.001
+        self.avgpool = AdaptiveAvgPool2d((1, 1))
+
+    def forward(self, x):
+        x = Fn.avg_pool2d(x, (5, 5), (3, 3), (0, 0), False, True)
+        x = self.conv1(self.conv0(x))
+        x = self.avgpool(x).reshape(x.shape[0], -1)
+        return self.fc(x)
+
+
+class Inception3(nn.Module):
+    def __init__(self, num_classes: int = 1000, aux_logits: bool = True, dropout: float = 0.5):
+        super().__init__()
+        self.aux_logits = aux_logits
+        self.transform_input = False
+        self.Conv2d_1a_3x3 = BasicConv2d(3, 32, 3, stride=2)
+        self.Conv2d_2a_3x3 = BasicConv2d(32, 32, 3)
+        self.Conv2d_2b_3x3 = BasicConv2d(32, 64, 3, padding=1)
+        self.maxpool1 = MaxPool2d(3, 2)
+        self.Conv2d_3b_1x1 = BasicConv2d(64, 80, 1)
+        self.Conv2d_4a_3x3 = BasicConv2d(80, 192, 3)
+        self.maxpool2 = MaxPool2d(3, 2)
+        self.Mixed_5b = InceptionA(192, 32)
+        self.Mixed_5c = InceptionA(256, 64)
+        self.Mixed_5d = InceptionA(288, 64)
+        self.Mixed_6a = InceptionB(288)
+        self.Mixed_6b = InceptionC(768, 128)
+        self.Mixed_6c = InceptionC(768, 160)
+        self.Mixed_6d = InceptionC(768, 160)
+        self.Mixed_6e = InceptionC(768, 192)
+        self.AuxLogits = InceptionAux(768, num_classes) if aux_logits else None
+        self.Mixed_7a = InceptionD(768)
+        self.Mixed_7b = InceptionE(1280)
+        self.Mixed_7c = InceptionE(2048)
+        self.avgpool = AdaptiveAvgPool2d((1, 1))
+        self.dropout = Dropout(dropout)
+        self.fc = Linear(2048, num_classes)
+        for m in self.modules():
+            if isinstance(m, (Conv2d, Linear)):
+                std = float(getattr(m, "stddev", 0.1))
+                m.init_(lambda w, s=std: nn.init.trunc_normal_(w, 0.0, s, -2, 2))
+
+    def forward(self, x):
+        for m in (self.Conv2d_1a_3x3, self.Conv2d_2a_3x3, self.Conv2d_2b_3x3, self.maxpool1,
+                  self.Conv2d_3b_1x1, self.Conv2d_4a_3x3, self.maxpool2, self.Mixed_5b,
+                  self.Mixed_5c, self.Mixed_5d, self.Mixed_6a, self.Mixed_6b, self.Mixed_6c,
+                  self.Mixed_6d, self.Mixed_6e):
+            x = m(x)
+        aux = None
+        if self.AuxLogits is not None and self.training:
+            aux = self.AuxLogits(x)
+        for m in (self.Mixed_7a, self.Mixed_7b, self.Mixed_7c):
+            x = m(x)
+        x = self.avgpool(x).reshape(x.shape[0], -1)
+        x = self.dropout(x)
+        x = self.fc(x)
+        if self.training and self.aux_logits:
+            return InceptionOutputs(x, aux)
+        return x
+
+
+def inception_v3(num_classes: int = 1000) -> Inception3:
+    return Inception3(num_classes)

@@ -1,0 +1,287 @@
+"""NHWC building blocks with torchvision-compatible parameter names and state_dict layout.
+
+Internally conv weights are stored ``[K, R, S, C]`` ("KRSC", the layout the implicit-GEMM
+MFMA kernels read with 16-byte vector loads along C) and activations are NHWC.  The
+state_dict converts to/from torchvision's OIHW at save/load time, so checkpoints keep the
+reference contract (``main.py:163-168``: ``model.state_dict()`` of a torchvision model;
+loaded by ``evaluation_pipeline.py:142-144`` / ``helpers.py:13``).
+
+``FusedSequential`` keeps torchvision's ``nn.Sequential`` indices (``features.0``,
+``features.1`` ...) but executes Conv->BN->ReLU and Conv->ReLU runs as single fused ops.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import functional as Fn
+
+
+def _pair(v) -> Tuple[int, int]:
+    if isinstance(v, (tuple, list)):
+        return int(v[0]), int(v[1])
+    return int(v), int(v)
+
+
+def _krsc_to_oihw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def _oihw_to_krsc(t):
+    return t.permute(0, 2, 3, 1)
+
+
+class Conv2d(nn.Module):
+    """Conv2d with KRSC weight storage. ``state_dict`` exposes OIHW like ``nn.Conv2d``."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size, stride=1, padding=0,
+                 bias: bool = True):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.kernel_size = _pair(kernel_size)
+        self.stride = _pair(stride)
+        self.padding = _pair(padding)
+        kh, kw = self.kernel_size
+        w = torch.empty(out_channels, in_channels, kh, kw)
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = nn.Parameter(_oihw_to_krsc(w).contiguous())
+        self.weight._mpa_export = _krsc_to_oihw
+        self.weight._mpa_import = _oihw_to_krsc
+        if bias:
+            fan_in = in_channels * kh * kw
+            bound = 1 / math.sqrt(fan_in)
+            self.bias = nn.Parameter(torch.empty(out_channels).uniform_(-bound, bound))
+        else:
+            self.register_parameter("bias", None)
+
+    # init helpers operate in OIHW space so the distributions match torchvision
+    def init_(self, fn) -> "Conv2d":
+        with torch.no_grad():
+            w = torch.empty(self.out_channels, self.in_channels, *self.kernel_size)
+            fn(w)
+            self.weight.copy_(_oihw_to_krsc(w))
+        return self
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        k = prefix + "weight"
+        if k in destination:
+            w = destination[k]
+            destination[k] = _krsc_to_oihw(w) if keep_vars else _krsc_to_oihw(w).contiguous()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        k = prefix + "weight"
+        if k in state_dict:
+            w = state_dict[k]
+            if tuple(w.shape) == (self.out_channels, self.in_channels, *self.kernel_size):
+                state_dict[k] = _oihw_to_krsc(w)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
+    def forward(self, x, relu: bool = False):
+        return Fn.conv_act(x, self, relu=relu)
+
+    def extra_repr(self):
+        return "{}, {}, kernel_size={}, stride={}, padding={}, bias={}".format(
+            self.in_channels, self.out_channels, self.kernel_size, self.stride, self.padding,
+            self.bias is not None)
+
+
+class BatchNorm2d(nn.Module):
+    """BatchNorm over the channel (last, NHWC) dim; same names/buffers as nn.BatchNorm2d."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1):
+        super().__init__()
+        self.num_features = num_features
+        self.eps = eps
+        self.momentum = momentum
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def momentum_value(self) -> float:
+        return float(self.momentum) if self.momentum is not None else 0.1
+
+    def forward(self, x, relu: bool = False):
+        return Fn.bn_act(x, self, relu=relu)
+
+    def extra_repr(self):
+        return "{}, eps={}, momentum={}".format(self.num_features, self.eps, self.momentum)
+
+
+class Linear(nn.Module):
+    """Linear layer.  ``in_chw=(C,H,W)`` marks a layer fed by an NHWC flatten: its input
+    columns are stored in (h,w,c) order internally and exported in torchvision's
+    NCHW-flatten (c,h,w) order."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True,
+                 in_chw: Optional[Tuple[int, int, int]] = None):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.in_chw = in_chw
+        w = torch.empty(out_features, in_features)
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = nn.Parameter(self._imp(w).contiguous())
+        if in_chw is not None:
+            self.weight._mpa_export = self._exp
+            self.weight._mpa_import = self._imp
+        if bias:
+            bound = 1 / math.sqrt(in_features)
+            self.bias = nn.Parameter(torch.empty(out_features).uniform_(-bound, bound))
+        else:
+            self.register_parameter("bias", None)
+
+    def _exp(self, t):  # internal (o, h*w*c) -> torchvision (o, c*h*w)
+        if self.in_chw is None:
+            return t
+        C, H, W = self.in_chw
+        return t.reshape(t.shape[0], H, W, C).permute(0, 3, 1, 2).reshape(t.shape[0], C * H * W)
+
+    def _imp(self, t):
+        if self.in_chw is None:
+            return t
+        C, H, W = self.in_chw
+        return t.reshape(t.shape[0], C, H, W).permute(0, 2, 3, 1).reshape(t.shape[0], H * W * C)
+
+    def init_(self, fn) -> "Linear":
+        with torch.no_grad():
+            w = torch.empty(self.out_features, self.in_features)
+            fn(w)
+            self.weight.copy_(self._imp(w))
+        return self
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        k = prefix + "weight"
+        if k in destination and self.in_chw is not None:
+            w = destination[k]
+            destination[k] = self._exp(w) if keep_vars else self._exp(w).contiguous()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        k = prefix + "weight"
+        if k in state_dict and self.in_chw is not None:
+            state_dict[k] = self._imp(state_dict[k])
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
+    def forward(self, x, relu: bool = False):
+        return Fn.linear_act(x, self, relu=relu)
+
+    def extra_repr(self):
+        return "in_features={}, out_features={}, bias={}".format(
+            self.in_features, self.out_features, self.bias is not None)
+
+
+class ReLU(nn.Module):
+    def __init__(self, inplace: bool = False):
+        super().__init__()
+
+    def forward(self, x):
+        # only reached when not fused into a producer; keep it a kernel op
+        return Fn.K(x).relu_fwd(x) if not x.requires_grad else _relu_autograd(x)
+
+
+def _relu_autograd(x):
+    return _ReLUFn.apply(x)
+
+
+class _ReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = Fn.K(x).relu_fwd(x)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return Fn.K(dy).act_bwd(dy.contiguous(), y, Fn._empty(dy))
+
+
+class MaxPool2d(nn.Module):
+    def __init__(self, kernel_size, stride=None, padding=0, ceil_mode=False):
+        super().__init__()
+        self.kernel_size = _pair(kernel_size)
+        self.stride = _pair(stride if stride is not None else kernel_size)
+        self.padding = _pair(padding)
+        self.ceil_mode = ceil_mode
+
+    def forward(self, x):
+        return Fn.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
+
+
+class AvgPool2d(nn.Module):
+    def __init__(self, kernel_size, stride=None, padding=0, ceil_mode=False,
+                 count_include_pad=True):
+        super().__init__()
+        self.kernel_size = _pair(kernel_size)
+        self.stride = _pair(stride if stride is not None else kernel_size)
+        self.padding = _pair(padding)
+        self.ceil_mode = ceil_mode
+        self.count_include_pad = count_include_pad
+
+    def forward(self, x):
+        return Fn.avg_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode,
+                             self.count_include_pad)
+
+
+class AdaptiveAvgPool2d(nn.Module):
+    def __init__(self, output_size):
+        super().__init__()
+        self.output_size = _pair(output_size)
+
+    def forward(self, x):
+        return Fn.adaptive_avg_pool2d(x, self.output_size)
+
+
+class Dropout(nn.Module):
+    def __init__(self, p: float = 0.5, inplace: bool = False):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        return Fn.dropout(x, self.p, self.training)
+
+
+class Flatten(nn.Module):
+    def forward(self, x):
+        return x.reshape(x.shape[0], -1)
+
+
+class FusedSequential(nn.Sequential):
+    """``nn.Sequential`` with torchvision indices, executed with producer fusion:
+    Conv(no bias)->BN[->ReLU] => conv_bn_act; Conv->ReLU => conv_act(relu); Linear->ReLU
+    => linear_act(relu)."""
+
+    def forward(self, x):
+        mods = list(self._modules.values())
+        i = 0
+        n = len(mods)
+        while i < n:
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < n else None
+            nxt2 = mods[i + 2] if i + 2 < n else None
+            if isinstance(m, Conv2d) and isinstance(nxt, BatchNorm2d):
+                relu = isinstance(nxt2, ReLU)
+                x = Fn.conv_bn_act(x, m, nxt, relu=relu)
+                i += 3 if relu else 2
+            elif isinstance(m, (Conv2d, Linear)) and isinstance(nxt, ReLU):
+                x = m(x, relu=True)
+                i += 2
+            elif isinstance(m, BatchNorm2d) and isinstance(nxt, ReLU):
+                x = m(x, relu=True)
+                i += 2
+            else:
+                x = m(x)
+                i += 1
+        return x

@@ -1,0 +1,87 @@
+"""ResNet-18/34 (BasicBlock), NHWC, torchvision parameter names.
+
+Reference: ``models.resnet18`` / ``models.resnet34`` with ``fc`` replaced by
+``nn.Linear(512, num_classes)`` (``/root/reference/models.py:30-45``).  Each
+conv->bn(->add)->relu runs as one fused op (``conv_bn_act``), the residual add folded
+into the BN-apply kernel.
+"""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from .layers import Conv2d, BatchNorm2d, Linear, MaxPool2d, AdaptiveAvgPool2d, ReLU
+from ..ops import functional as Fn
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample=None):
+        super().__init__()
+        self.conv1 = Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = BatchNorm2d(planes)
+        self.relu = ReLU(inplace=True)
+        self.conv2 = Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        out = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        if self.downsample is not None:
+            identity = Fn.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
+        else:
+            identity = x
+        return Fn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=identity)
+
+
+class Downsample(nn.Sequential):
+    pass
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers, num_classes: int = 1000):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = BatchNorm2d(64)
+        self.relu = ReLU(inplace=True)
+        self.maxpool = MaxPool2d(3, 2, 1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.avgpool = AdaptiveAvgPool2d((1, 1))
+        self.fc = Linear(512, num_classes)
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                m.init_(lambda w: nn.init.kaiming_normal_(w, mode="fan_out", nonlinearity="relu"))
+
+    def _make_layer(self, planes: int, blocks: int, stride: int = 1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes:
+            downsample = Downsample(Conv2d(self.inplanes, planes, 1, stride, 0, bias=False),
+                                    BatchNorm2d(planes))
+        layers = [BasicBlock(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes
+        for _ in range(1, blocks):
+            layers.append(BasicBlock(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        x = self.maxpool(x)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk(x)
+        x = self.avgpool(x)
+        x = x.reshape(x.shape[0], -1)
+        return self.fc(x)
+
+
+def resnet18(num_classes: int = 1000) -> ResNet:
+    return ResNet([2, 2, 2, 2], num_classes)
+
+
+def resnet34(num_classes: int = 1000) -> ResNet:
+    return ResNet([3, 4, 6, 3], num_classes)

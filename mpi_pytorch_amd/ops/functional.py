@@ -1,0 +1,370 @@
+"""Autograd functions over the kernel API (NHWC activations, fused epilogues).
+
+Each function dispatches on the activation's device: CUDA/HIP tensors go to the native
+gfx950 kernels (``mpi_pytorch_amd._C``; missing extension => loud error), CPU tensors to
+``ops/ref.py``.  The ops the reference reaches through ATen map to:
+
+* ``conv_bn_act``   conv (implicit-GEMM MFMA, BN batch statistics accumulated in the conv
+                    epilogue) -> BN apply (+ residual add) (+ ReLU)  [K1-K5, K8]
+* ``conv_act``      conv + bias (+ ReLU) epilogue                     [K1, K5]
+* ``bn_act``        standalone BN (+ReLU) for pre-activation nets (DenseNet)  [K4]
+* ``linear_act``    Linear + bias (+ ReLU) on the same MFMA engine   [K9]
+* ``max_pool2d``, ``avg_pool2d``, ``adaptive_avg_pool2d``            [K6, K7]
+* ``dropout``                                                        [K14]
+* ``cross_entropy`` fused log-softmax + NLL (mean), grad recomputed from saved LSE  [K10]
+
+Parameter gradients never travel through autograd: backward kernels accumulate them in
+fp32 directly into the flat gradient arena (``p.grad``) and then signal the DP bucketer
+(``grad_done``), which may start that bucket's all-reduce immediately.  Parameters are
+still autograd *inputs* so that backward reaches the first layer even though the image
+tensor does not require grad.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import ref
+from . import _ext
+from ..parallel.arena import weight_of, grad_sink, grad_done
+
+_EMPTY = {}
+
+
+def K(t: torch.Tensor):
+    """Kernel namespace for a tensor's device."""
+    if t.is_cuda:
+        return _ext.ext()
+    return ref
+
+
+def _empty(t: torch.Tensor) -> torch.Tensor:
+    key = (t.device, torch.float32)
+    e = _EMPTY.get(key)
+    if e is None:
+        e = torch.empty(0, device=t.device, dtype=torch.float32)
+        _EMPTY[key] = e
+    return e
+
+
+def _or_empty(x: Optional[torch.Tensor], like: torch.Tensor) -> torch.Tensor:
+    return x if x is not None else _empty(like)
+
+
+def _sink(p: Optional[torch.nn.Parameter], like: torch.Tensor) -> torch.Tensor:
+    if p is None:
+        return _empty(like)
+    s = grad_sink(p)
+    return s if s is not None else _empty(like)
+
+
+def _done(*ps) -> None:
+    for p in ps:
+        if p is not None:
+            grad_done(p)
+
+
+# =============================================================================== conv+BN
+class _ConvBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu):
+        k = K(x)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        C = w.shape[0]
+        stats = torch.zeros(2, C, device=x.device, dtype=torch.float32)
+        z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats)
+        y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
+                                       bn.momentum_value(), bn.eps,
+                                       _or_empty(residual, x), relu)
+        bn.num_batches_tracked.add_(1)
+        ctx.conv = conv
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.bias = b
+        ctx.params = (w, gamma, beta)
+        ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, z, y if relu else None, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, mean, rstd = ctx.saved_tensors
+        w, gamma, beta = ctx.params
+        conv = ctx.conv
+        k = K(dy)
+        dy = dy.contiguous()
+        want_g = bool(ctx.has_res and ctx.needs_input_grad[1])
+        dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
+                         _sink(beta, dy), True, want_g)
+        _done(gamma, beta)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        if w.requires_grad:
+            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            _done(w)
+        _done(ctx.bias)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw)
+        dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
+        return dx, dres, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None):
+    """relu(bn(conv(x)) [+ residual]); BN in train or eval mode per ``bn.training``.
+
+    A conv bias in front of a train-mode BN (VGG11_bn) is added before the statistics, so
+    forward and running stats are exact; its gradient is exactly zero in exact arithmetic
+    (BN removes any per-channel constant) and is left at zero instead of accumulating
+    rounding noise."""
+    if bn.training:
+        return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
+                                bn, relu)
+    k = K(x)
+    sh, sw = conv.stride
+    ph, pw = conv.padding
+    z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,
+                   _empty(x))
+    return k.bn_fwd_eval(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                         _or_empty(residual, x), relu)
+
+
+# ============================================================================ conv + bias
+class _ConvAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, conv, relu):
+        k = K(x)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu, _empty(x))
+        ctx.conv = conv
+        ctx.relu = relu
+        ctx.params = (w, b)
+        ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        w, b = ctx.params
+        conv = ctx.conv
+        k = K(dy)
+        dy = dy.contiguous()
+        g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
+        _done(b)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        if w.requires_grad:
+            k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw)
+            _done(w)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k.conv_dgrad(g, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw)
+        return dx, None, None, None, None
+
+
+def conv_act(x, conv, relu: bool = False):
+    if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
+        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu)
+    k = K(x)
+    sh, sw = conv.stride
+    ph, pw = conv.padding
+    return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,
+                      _empty(x))
+
+
+# =========================================================================== standalone BN
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, relu):
+        k = K(x)
+        y, mean, rstd = k.bn_fwd_train(x, _empty(x), gamma, beta, bn.running_mean,
+                                       bn.running_var, bn.momentum_value(), bn.eps, _empty(x),
+                                       relu)
+        bn.num_batches_tracked.add_(1)
+        ctx.params = (gamma, beta)
+        ctx.save_for_backward(x, y if relu else None, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.params
+        k = K(dy)
+        dy = dy.contiguous()
+        dx, _g = k.bn_bwd(dy, x, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
+                          _sink(beta, dy), bool(ctx.needs_input_grad[0]), False)
+        _done(gamma, beta)
+        return dx, None, None, None, None
+
+
+def bn_act(x, bn, relu: bool = True):
+    if bn.training:
+        return _BNAct.apply(x, bn.weight, bn.bias, bn, relu)
+    return K(x).bn_fwd_eval(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                            _empty(x), relu)
+
+
+# ================================================================================ linear
+class _LinearAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        k = K(x)
+        y = k.linear_fwd(x, weight_of(w), _or_empty(b, x), relu)
+        ctx.relu = relu
+        ctx.params = (w, b)
+        ctx.save_for_backward(x, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        w, b = ctx.params
+        k = K(dy)
+        dy = dy.contiguous()
+        g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
+        _done(b)
+        if w.requires_grad:
+            k.linear_wgrad(g, x, w.grad)
+            _done(w)
+        dx = k.linear_dgrad(g, weight_of(w)) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None
+
+
+def linear_act(x, lin, relu: bool = False):
+    if torch.is_grad_enabled() and (lin.weight.requires_grad or x.requires_grad):
+        return _LinearAct.apply(x, lin.weight, lin.bias, relu)
+    return K(x).linear_fwd(x, weight_of(lin.weight), _or_empty(lin.bias, x), relu)
+
+
+# ================================================================================= pools
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cfg):
+        y, idx = K(x).maxpool_fwd(x, *cfg)
+        ctx.cfg = cfg
+        ctx.hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        dx = K(dy).maxpool_bwd(dy.contiguous(), idx, ctx.hw[0], ctx.hw[1], *ctx.cfg)
+        return dx, None
+
+
+def max_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False):
+    cfg = (kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], bool(ceil_mode))
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _MaxPool.apply(x, cfg)
+    return K(x).maxpool_fwd(x, *cfg)[0]
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cfg):
+        ctx.cfg = cfg
+        ctx.hw = (x.shape[1], x.shape[2])
+        return K(x).avgpool_fwd(x, *cfg)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K(dy).avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1], *ctx.cfg), None
+
+
+def avg_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False, count_include_pad=True):
+    cfg = (kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], bool(ceil_mode),
+           bool(count_include_pad))
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _AvgPool.apply(x, cfg)
+    return K(x).avgpool_fwd(x, *cfg)
+
+
+class _AdaptiveAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return K(x).adaptive_avgpool_fwd(x, oh, ow)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K(dy).adaptive_avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1]), None, None
+
+
+def adaptive_avg_pool2d(x, out_hw):
+    oh, ow = out_hw
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _AdaptiveAvgPool.apply(x, oh, ow)
+    return K(x).adaptive_avgpool_fwd(x, oh, ow)
+
+
+# =============================================================================== dropout
+class DropoutRNG:
+    """Per-device counter so every dropout call draws a fresh mask (graph-safe: the seed
+    is a host constant, the offset a per-call counter)."""
+    seed = 0
+    offset = 0
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        DropoutRNG.offset += 1
+        y, mask = K(x).dropout_fwd(x, p, DropoutRNG.seed, DropoutRNG.offset)
+        ctx.p = p
+        ctx.save_for_backward(mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        return K(dy).dropout_bwd(dy.contiguous(), mask, ctx.p), None
+
+
+def dropout(x, p: float, training: bool):
+    if not training or p == 0.0:
+        return x
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _Dropout.apply(x, p)
+    DropoutRNG.offset += 1
+    return K(x).dropout_fwd(x, p, DropoutRNG.seed, DropoutRNG.offset)[0]
+
+
+# ========================================================================= cross-entropy
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        loss, lse = K(logits).ce_fwd(logits, labels)
+        ctx.save_for_backward(logits, labels, lse)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, go):
+        logits, labels, lse = ctx.saved_tensors
+        g = K(logits).ce_bwd(logits, labels, lse, go.reshape(1).float().contiguous())
+        return g, None
+
+
+def cross_entropy(logits, labels):
+    """Mean softmax cross-entropy (``nn.CrossEntropyLoss()`` at main.py:134,150)."""
+    if torch.is_grad_enabled() and logits.requires_grad:
+        return _CrossEntropy.apply(logits, labels)
+    return K(logits).ce_fwd(logits, labels)[0].reshape(())
+
+
+def count_correct(logits, labels, count: torch.Tensor) -> None:
+    """count += #(argmax(logits) == labels)  (main.py:182-183)."""
+    K(logits).argmax_correct(logits, labels, count)
+
+
+def preprocess(img_u8, out_hw, mean, std, mode: int = 0, cpad: int = 3,
+               out_dtype=torch.bfloat16):
+    k = K(img_u8)
+    if img_u8.is_cuda:
+        return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad)
+    return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad,
+                        out_dtype)

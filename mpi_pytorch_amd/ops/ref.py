@@ -1,0 +1,311 @@
+"""Plain-PyTorch implementation of the native kernel API (NHWC layout).
+
+Two roles:
+1. CPU execution path.  The reference framework is CPU-only (``main.py:50-51``), and
+   BASELINE.json config 1 is a single-process CPU plumbing run, so CPU tensors run here.
+2. Test oracle for every HIP kernel: the GPU tests call the same function here on the
+   same inputs (computed in fp32) and compare.
+
+It is NEVER used as a runtime fallback for GPU tensors (see ``ops/_ext.py``).
+
+Every function mirrors a function of ``mpi_pytorch_amd._C`` with the same signature and
+output dtypes: activations keep the input dtype (bf16 on GPU, fp32 on CPU), statistics
+and gradient sinks are fp32.  Layouts: activations NHWC ``[N,H,W,C]``; conv weights
+``[K,R,S,C]`` ("KRSC"); linear weights ``[out,in]``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+
+
+def _f(x: Tensor) -> Tensor:
+    return x.float()
+
+
+def _nchw(x: Tensor) -> Tensor:
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x: Tensor) -> Tensor:
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _opt(t: Optional[Tensor]) -> Optional[Tensor]:
+    if t is None or t.numel() == 0:
+        return None
+    return t
+
+
+# ----------------------------------------------------------------------------------- conv
+def conv_out_hw(H, W, R, S, sh, sw, ph, pw):
+    return (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1
+
+
+def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats):
+    y = F.conv2d(_nchw(_f(x)), _f(w).permute(0, 3, 1, 2), None if _opt(bias) is None else _f(bias),
+                 (sh, sw), (ph, pw))
+    y = _nhwc(y)
+    if relu:
+        y = torch.relu(y)
+    y = y.to(x.dtype)
+    st = _opt(stats)
+    if st is not None:
+        yf = y.float().reshape(-1, y.shape[-1])
+        st[0].add_(yf.sum(0))
+        st[1].add_((yf * yf).sum(0))
+    return y
+
+
+def conv_dgrad(dy, w, H, W, sh, sw, ph, pw):
+    N, P, Q, K = dy.shape
+    Kw, R, S, C = w.shape
+    gi = torch.ops.aten.convolution_backward(
+        _nchw(_f(dy)).contiguous(), torch.empty(N, C, H, W, device=dy.device),
+        _f(w).permute(0, 3, 1, 2).contiguous(), None, [sh, sw], [ph, pw], [1, 1], False,
+        [0, 0], 1, [True, False, False])[0]
+    return _nhwc(gi).to(dy.dtype)
+
+
+def conv_wgrad(dy, x, dw, sh, sw, ph, pw):
+    K, R, S, C = dw.shape
+    gw = torch.ops.aten.convolution_backward(
+        _nchw(_f(dy)).contiguous(), _nchw(_f(x)).contiguous(),
+        torch.empty(K, C, R, S, device=dy.device), None, [sh, sw], [ph, pw], [1, 1], False,
+        [0, 0], 1, [False, True, False])[1]
+    dw.add_(gw.permute(0, 2, 3, 1))
+
+
+def act_bwd(dy, y, dbias):
+    """g = dy * (y > 0) if y given else dy; dbias += sum_rows(g)."""
+    g = dy if _opt(y) is None else (_f(dy) * (_f(y) > 0)).to(dy.dtype)
+    db = _opt(dbias)
+    if db is not None:
+        db.add_(_f(g).reshape(-1, g.shape[-1]).sum(0))
+    return g
+
+
+# ------------------------------------------------------------------------------------ BN
+def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu):
+    C = x.shape[-1]
+    xf = _f(x).reshape(-1, C)
+    M = xf.shape[0]
+    st = _opt(stats)
+    if st is not None:
+        mean = st[0] / M
+        var = (st[1] / M - mean * mean).clamp_min(0)
+    else:
+        mean = xf.mean(0)
+        var = xf.var(0, unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    y = (xf - mean) * (rstd * gamma) + beta
+    if _opt(residual) is not None:
+        y = y + _f(residual).reshape(-1, C)
+    if relu:
+        y = torch.relu(y)
+    with torch.no_grad():
+        unbiased = var * (M / max(M - 1, 1))
+        rmean.mul_(1 - momentum).add_(mean, alpha=momentum)
+        rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+    return y.reshape(x.shape).to(x.dtype), mean.contiguous(), rstd.contiguous()
+
+
+def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
+    C = x.shape[-1]
+    xf = _f(x).reshape(-1, C)
+    rstd = torch.rsqrt(rvar + eps)
+    y = (xf - rmean) * (rstd * gamma) + beta
+    if _opt(residual) is not None:
+        y = y + _f(residual).reshape(-1, C)
+    if relu:
+        y = torch.relu(y)
+    return y.reshape(x.shape).to(x.dtype)
+
+
+def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True):
+    """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient)."""
+    C = x.shape[-1]
+    g = _f(dy).reshape(-1, C)
+    if _opt(y) is not None:
+        g = g * (_f(y).reshape(-1, C) > 0)
+    M = g.shape[0]
+    xhat = (_f(x).reshape(-1, C) - mean) * rstd
+    sg = g.sum(0)
+    sgx = (g * xhat).sum(0)
+    if _opt(dgamma) is not None:
+        dgamma.add_(sgx)
+    if _opt(dbeta) is not None:
+        dbeta.add_(sg)
+    dx = None
+    if want_dx:
+        dx = (gamma * rstd) * (g - sg / M - xhat * (sgx / M))
+        dx = dx.reshape(x.shape).to(dy.dtype)
+    return dx, g.reshape(x.shape).to(dy.dtype)
+
+
+# ---------------------------------------------------------------------------------- pool
+def _pool_out(H, k, s, p, ceil):
+    if ceil:
+        o = -(-(H + 2 * p - k) // s) + 1
+        if (o - 1) * s >= H + p:
+            o -= 1
+    else:
+        o = (H + 2 * p - k) // s + 1
+    return o
+
+
+def maxpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil):
+    y, idx = F.max_pool2d(_nchw(_f(x)), (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
+                          return_indices=True)
+    return _nhwc(y).to(x.dtype), _nhwc(idx.to(torch.int32))
+
+
+def maxpool_bwd(dy, idx, H, W, kh, kw, sh, sw, ph, pw, ceil):
+    N, P, Q, C = dy.shape
+    out = torch.zeros(N, C, H * W, device=dy.device, dtype=torch.float32)
+    out.scatter_add_(2, _nchw(idx).reshape(N, C, -1).long(), _nchw(_f(dy)).reshape(N, C, -1))
+    return _nhwc(out.reshape(N, C, H, W)).to(dy.dtype)
+
+
+def avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
+    y = F.avg_pool2d(_nchw(_f(x)), (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
+                     count_include_pad=count_include_pad)
+    return _nhwc(y).to(x.dtype)
+
+
+def avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
+    N, P, Q, C = dy.shape
+    xin = torch.zeros(N, C, H, W, device=dy.device, requires_grad=True)
+    with torch.enable_grad():
+        y = F.avg_pool2d(xin, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
+                         count_include_pad=count_include_pad)
+        (gx,) = torch.autograd.grad(y, xin, _nchw(_f(dy)))
+    return _nhwc(gx).to(dy.dtype)
+
+
+def adaptive_avgpool_fwd(x, oh, ow):
+    return _nhwc(F.adaptive_avg_pool2d(_nchw(_f(x)), (oh, ow))).to(x.dtype)
+
+
+def adaptive_avgpool_bwd(dy, H, W):
+    N, P, Q, C = dy.shape
+    xin = torch.zeros(N, C, H, W, device=dy.device, requires_grad=True)
+    with torch.enable_grad():
+        y = F.adaptive_avg_pool2d(xin, (P, Q))
+        (gx,) = torch.autograd.grad(y, xin, _nchw(_f(dy)))
+    return _nhwc(gx).to(dy.dtype)
+
+
+# ------------------------------------------------------------------------------- linear
+def linear_fwd(x, w, bias, relu):
+    y = _f(x) @ _f(w).t()
+    if _opt(bias) is not None:
+        y = y + _f(bias)
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def linear_dgrad(dy, w):
+    return (_f(dy) @ _f(w)).to(dy.dtype)
+
+
+def linear_wgrad(dy, x, dw):
+    dw.add_(_f(dy).t() @ _f(x))
+
+
+# --------------------------------------------------------------------------- loss / acc
+def ce_fwd(logits, labels):
+    lf = _f(logits)
+    lse = torch.logsumexp(lf, dim=1)
+    picked = lf.gather(1, labels.view(-1, 1).long()).squeeze(1)
+    loss = (lse - picked).mean().reshape(1)
+    return loss, lse
+
+
+def ce_bwd(logits, labels, lse, grad_out):
+    B = logits.shape[0]
+    p = torch.exp(_f(logits) - lse[:, None])
+    p[torch.arange(B, device=logits.device), labels.long()] -= 1.0
+    return (p * (_f(grad_out).reshape(()) / B)).to(logits.dtype)
+
+
+def argmax_correct(logits, labels, count):
+    pred = _f(logits).argmax(1)
+    count.add_((pred == labels.long()).sum().to(count.dtype))
+
+
+# ----------------------------------------------------------------------------- optimizer
+def adam_step(master, grad, m, v, shadow, step_t, lr, b1, b2, eps, wd, grad_scale):
+    step = float(step_t.item()) + 1.0
+    g = grad * grad_scale
+    if wd != 0.0:
+        g = g + wd * master
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    master.addcdiv_(m, denom, value=-lr / bc1)
+    if _opt(shadow) is not None:
+        shadow.copy_(master)
+
+
+def sgd_step(master, grad, buf, shadow, step_t, lr, momentum, dampening, wd, nesterov, grad_scale):
+    first = float(step_t.item()) == 0.0
+    g = grad * grad_scale
+    if wd != 0.0:
+        g = g + wd * master
+    if momentum != 0.0:
+        if first:
+            buf.copy_(g)
+        else:
+            buf.mul_(momentum).add_(g, alpha=1 - dampening)
+        g = g + momentum * buf if nesterov else buf
+    master.add_(g, alpha=-lr)
+    if _opt(shadow) is not None:
+        shadow.copy_(master)
+
+
+# ------------------------------------------------------------------------ preprocessing
+def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype):
+    """u8 NHWC [B,H,W,3] -> normalized NHWC [B,oh,ow,cpad] (zero padded channels).
+
+    mode 0: bilinear, no antialias  (train path: ToTensor -> Resize on tensor, main.py:62-65)
+    mode 1: bicubic with antialias  (eval path: PIL resize, evaluation_pipeline.py:89)
+    """
+    x = _nchw(img_u8.float() / 255.0)
+    if (oh, ow) != tuple(x.shape[-2:]):
+        if mode == 0:
+            x = F.interpolate(x, size=(oh, ow), mode="bilinear", align_corners=False)
+        else:
+            x = F.interpolate(x, size=(oh, ow), mode="bicubic", align_corners=False,
+                              antialias=True)
+    m = torch.tensor(mean, device=x.device).view(1, 3, 1, 1)
+    s = torch.tensor(std, device=x.device).view(1, 3, 1, 1)
+    x = _nhwc((x - m) / s)
+    if cpad > 3:
+        x = F.pad(x, (0, cpad - 3))
+    return x.to(out_dtype)
+
+
+# ---------------------------------------------------------------------------- dropout
+def dropout_fwd(x, p, seed, offset):
+    g = torch.Generator(device=x.device)
+    g.manual_seed(int(seed) * 1000003 + int(offset))
+    keep = (torch.rand(x.shape, generator=g, device=x.device) >= p)
+    y = (_f(x) * keep / (1 - p)).to(x.dtype)
+    return y, keep.to(torch.uint8)
+
+
+def dropout_bwd(dy, mask, p):
+    return (_f(dy) * mask.float() / (1 - p)).to(dy.dtype)
+
+
+def relu_fwd(x):
+    return torch.relu(x)

@@ -1,0 +1,132 @@
+"""Flat parameter / gradient arena.
+
+Every parameter of a model is re-homed into ONE contiguous fp32 master buffer, and every
+trainable parameter's ``.grad`` becomes a view into ONE contiguous fp32 gradient buffer.
+On the GPU a bf16 shadow of the master buffer holds the weights the MFMA kernels read.
+
+Why (MI355X-first, not a translation of ``mpi_tools.py``):
+
+* The reference all-reduces one tensor at a time (62 blocking calls/step for ResNet-18,
+  ``/root/reference/mpi_tools.py:30-37``) and broadcasts one tensor at a time
+  (``mpi_tools.py:47-53``).  With a flat arena the broadcast is one RCCL call and the
+  gradient all-reduce is a handful of large buckets cut from one buffer, which is what a
+  per-link-bound xGMI ring wants.
+* The optimizer (Adam/SGD) becomes ONE streaming HIP kernel over the flat buffers that
+  also writes the bf16 shadow - no per-tensor launches, no separate cast pass.
+* Layout: trainable parameters come first, in *reverse registration order*, so the
+  gradients produced first by backward (the classifier head) sit at the front of the
+  gradient buffer and close the first bucket while the conv stack still back-propagates.
+  Frozen parameters (``feature_extract``, ``models.py:5-13`` of the reference) sit after
+  the trainable region and get no gradient storage.
+
+Backward kernels write weight gradients straight into ``p.grad`` (atomic fp32
+accumulation into the zeroed arena), then call :meth:`ParamArena.notify` so the
+bucketer can launch the bucket's all-reduce as soon as its last gradient lands.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64  # elements (256 B fp32) - keeps every slice 16-B aligned for dwordx4 access
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class ParamArena:
+    def __init__(self, model: nn.Module, device: torch.device, shadow: Optional[bool] = None):
+        self.device = torch.device(device)
+        if shadow is None:
+            shadow = self.device.type == "cuda"
+        seen = set()
+        params: List[nn.Parameter] = []
+        names: Dict[int, str] = {}
+        for n, p in model.named_parameters():
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            params.append(p)
+            names[id(p)] = n
+        trainable = [p for p in params if p.requires_grad][::-1]
+        frozen = [p for p in params if not p.requires_grad]
+        self.params: List[nn.Parameter] = trainable + frozen
+        self.trainable: List[nn.Parameter] = trainable
+        self.names = names
+        self.offsets: Dict[int, int] = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = off
+            off += _align(p.numel())
+        self.numel = off
+        self.n_train = sum(_align(p.numel()) for p in trainable)
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(max(self.n_train, ALIGN), dtype=torch.float32, device=self.device)
+        self.shadow = (torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
+                       if shadow else None)
+        with torch.no_grad():
+            for p in self.params:
+                o = self.offsets[id(p)]
+                view = self.master[o:o + p.numel()].view_as(p)
+                view.copy_(p.data.to(self.device, torch.float32))
+                p.data = view
+                if self.shadow is not None:
+                    p._mpa_shadow = self.shadow[o:o + p.numel()].view(p.shape)
+                else:
+                    p._mpa_shadow = None
+                if p.requires_grad:
+                    p.grad = self.grad[o:o + p.numel()].view_as(p)
+                p._mpa_arena = self
+        self._listeners: List[Callable[[nn.Parameter], None]] = []
+        self.sync_shadow()
+
+    # ------------------------------------------------------------------------------
+    def slice_of(self, p: nn.Parameter):
+        o = self.offsets[id(p)]
+        return o, o + p.numel()
+
+    def sync_shadow(self) -> None:
+        """Refresh the bf16 weight shadow from the fp32 masters (after init/load)."""
+        if self.shadow is not None:
+            with torch.no_grad():
+                self.shadow.copy_(self.master)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def add_listener(self, fn: Callable[[nn.Parameter], None]) -> None:
+        self._listeners.append(fn)
+
+    def notify(self, p: nn.Parameter) -> None:
+        for fn in self._listeners:
+            fn(p)
+
+    def train_master(self) -> torch.Tensor:
+        return self.master[:self.n_train]
+
+    def train_shadow(self) -> Optional[torch.Tensor]:
+        return None if self.shadow is None else self.shadow[:self.n_train]
+
+
+def weight_of(p: nn.Parameter) -> torch.Tensor:
+    """The tensor a compute kernel should read for parameter ``p`` (bf16 on GPU)."""
+    s = getattr(p, "_mpa_shadow", None)
+    return s if s is not None else p
+
+
+def grad_sink(p: nn.Parameter) -> Optional[torch.Tensor]:
+    """Where a backward kernel accumulates ``p``'s gradient (None when frozen)."""
+    if not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, dtype=torch.float32)
+    return p.grad
+
+
+def grad_done(p: nn.Parameter) -> None:
+    a = getattr(p, "_mpa_arena", None)
+    if a is not None and p.requires_grad:
+        a.notify(p)

@@ -1,0 +1,109 @@
+"""Process-group bring-up: one process per GPU, RCCL (torch backend ``nccl``) over xGMI.
+
+The reference gets its world from ``mpi4py`` at import time (``/root/reference/main.py:1,16-18``,
+``mpi_tools.py:1``).  MPI is not available on the MI355X image, so ranks come from the
+environment set by our launcher (``python -m mpi_pytorch_amd.launch``), by
+``torch.distributed.run`` (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*), or by an MPI launcher
+(OMPI_COMM_WORLD_* / PMI_*).  World size 1 needs no process group at all, mirroring the
+reference's ``num_processes() == 1`` short-circuits (``mpi_tools.py:32-33,49-50``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_dist(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+
+_WORLD: Optional[World] = None
+
+
+def _env_int(*names: str, default: int = -1) -> int:
+    for n in names:
+        v = os.environ.get(n)
+        if v is not None and v != "":
+            return int(v)
+    return default
+
+
+def env_rank_info():
+    rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", default=0)
+    world = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", default=1)
+    local = _env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
+                     "SLURM_LOCALID", default=-1)
+    if local < 0:
+        local = rank
+    return rank, world, local
+
+
+def init_world(device: str = "auto", timeout_s: float = 1800.0,
+               backend: Optional[str] = None) -> World:
+    """Initialise (idempotently) the process group and pick this rank's device."""
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    rank, world, local = env_rank_info()
+    use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    if use_cuda:
+        ndev = torch.cuda.device_count()
+        dev = torch.device("cuda", local % max(ndev, 1))
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    be = "none"
+    if world > 1:
+        be = backend or os.environ.get("MPA_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if not dist.is_initialized():
+            kw = dict(backend=be, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if be == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+    _WORLD = World(rank=rank, world_size=world, local_rank=local, device=dev, backend=be)
+    return _WORLD
+
+
+def get_world() -> World:
+    return _WORLD if _WORLD is not None else init_world()
+
+
+def shutdown() -> None:
+    global _WORLD
+    if dist.is_available() and dist.is_initialized():
+        try:
+            dist.barrier()
+        except Exception:
+            pass
+        dist.destroy_process_group()
+    _WORLD = None
+
+
+def barrier() -> None:
+    w = get_world()
+    if w.is_dist:
+        if w.backend == "nccl":
+            dist.barrier(device_ids=[w.device.index])
+        else:
+            dist.barrier()

@@ -1,0 +1,284 @@
+"""Numerics of every native gfx950 kernel against the plain-PyTorch fp32 oracle
+(``mpi_pytorch_amd/ops/ref.py``) on identical bf16 inputs."""
+import math
+
+import pytest
+import torch
+
+from mpi_pytorch_amd.ops import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    from mpi_pytorch_amd.ops import _ext
+    return _ext.ext()
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-6))
+
+
+def bf(*shape, dev, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, S, stride, pad
+    (2, 32, 32, 3, 64, 7, 7, 2, 3),       # stem (C=3 scalar path)
+    (2, 14, 14, 64, 64, 3, 3, 1, 1),
+    (2, 14, 14, 64, 128, 3, 3, 2, 1),
+    (2, 14, 14, 64, 128, 1, 1, 2, 0),      # downsample
+    (3, 9, 11, 96, 48, 3, 3, 1, 1),        # odd spatial, BN=64 tile
+    (2, 12, 12, 32, 32, 1, 7, 1, (0, 3)),  # asymmetric 1x7
+    (2, 12, 12, 40, 24, 7, 1, 1, (3, 0)),  # asymmetric 7x1, BN=32 tile, C%8==0
+    (2, 17, 17, 64, 200, 3, 3, 2, 0),      # K not multiple of tile, stride 2 no pad
+    (2, 8, 8, 256, 512, 3, 3, 1, 1),       # deep K (split-K candidate)
+    (1, 13, 13, 12, 20, 5, 5, 1, 2),       # C%8 != 0 (VW=4)
+    (2, 20, 20, 16, 64, 11, 11, 4, 2),     # AlexNet-style 11x11 s4
+]
+
+
+def _pair(v):
+    return v if isinstance(v, tuple) else (v, v)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(gpu, case):
+    torch.manual_seed(0)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * Cc))
+    b = torch.randn(K, device=gpu)
+    st_c = torch.zeros(2, K, device=gpu)
+    st_r = torch.zeros(2, K, device=gpu)
+    y = C().conv_fwd(x, w, b, st, st, ph, pw, True, st_c)
+    yr = ref.conv_fwd(x, w, b, st, st, ph, pw, True, st_r)
+    torch.cuda.synchronize()
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 2e-2
+    assert rel(st_c, st_r) < 2e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad(gpu, case):
+    torch.manual_seed(1)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * K))
+    dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
+    dxr = ref.conv_dgrad(dy, w, H, W, st, st, ph, pw)
+    torch.cuda.synchronize()
+    assert rel(dx, dxr) < 2e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad(gpu, case):
+    torch.manual_seed(2)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    x = bf(N, H, W, Cc, dev=gpu)
+    dw = torch.full((K, R, S, Cc), 0.5, device=gpu)   # accumulates into existing contents
+    dwr = dw.clone()
+    C().conv_wgrad(dy, x, dw, st, st, ph, pw)
+    ref.conv_wgrad(dy, x, dwr, st, st, ph, pw)
+    torch.cuda.synchronize()
+    assert rel(dw, dwr) < 1e-2
+
+
+@pytest.mark.parametrize("B,Cin,Cout", [(8, 512, 1000), (128, 512, 64500), (16, 72, 36),
+                                        (32, 4096, 4096)])
+def test_linear(gpu, B, Cin, Cout):
+    torch.manual_seed(3)
+    x = bf(B, Cin, dev=gpu)
+    w = bf(Cout, Cin, dev=gpu, scale=1.0 / math.sqrt(Cin))
+    b = torch.randn(Cout, device=gpu)
+    y = C().linear_fwd(x, w, b, False)
+    assert rel(y, ref.linear_fwd(x, w, b, False)) < 2e-2
+    dy = bf(B, Cout, dev=gpu)
+    assert rel(C().linear_dgrad(dy, w), ref.linear_dgrad(dy, w)) < 2e-2
+    dw = torch.zeros(Cout, Cin, device=gpu)
+    dwr = torch.zeros(Cout, Cin, device=gpu)
+    C().linear_wgrad(dy, x, dw)
+    ref.linear_wgrad(dy, x, dwr)
+    assert rel(dw, dwr) < 1e-2
+
+
+@pytest.mark.parametrize("M,Cc", [(4096, 64), (1000, 96), (37, 2048), (5000, 24)])
+@pytest.mark.parametrize("relu,res", [(True, True), (False, False), (True, False)])
+def test_bn(gpu, M, Cc, relu, res):
+    torch.manual_seed(4)
+    x = bf(M, Cc, dev=gpu, scale=2.0) + 0.5
+    x = x.to(torch.bfloat16)
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu)
+    r = bf(M, Cc, dev=gpu) if res else torch.empty(0, device=gpu)
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    rm2, rv2 = rm.clone(), rv.clone()
+    e = torch.empty(0, device=gpu)
+    y, mean, rstd = C().bn_fwd_train(x, e, g, b, rm, rv, 0.1, 1e-5, r, relu)
+    yr, meanr, rstdr = ref.bn_fwd_train(x, e, g, b, rm2, rv2, 0.1, 1e-5, r, relu)
+    assert rel(y, yr) < 2e-2
+    assert rel(mean, meanr) < 1e-3 and rel(rstd, rstdr) < 1e-3
+    assert rel(rm, rm2) < 1e-3 and rel(rv, rv2) < 1e-3
+    ye = C().bn_fwd_eval(x, g, b, rm, rv, 1e-5, r, relu)
+    assert rel(ye, ref.bn_fwd_eval(x, g, b, rm2, rv2, 1e-5, r, relu)) < 2e-2
+    dy = bf(M, Cc, dev=gpu)
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    yy = y if relu else e
+    dx, gg = C().bn_bwd(dy, x, yy, mean, rstd, g, dg, db, True, True)
+    dxr, ggr = ref.bn_bwd(dy, x, yr if relu else e, meanr, rstdr, g, dg2, db2, True)
+    assert rel(dx, dxr) < 3e-2
+    assert rel(gg, ggr) < 2e-2
+    assert rel(dg, dg2) < 1e-2 and rel(db, db2) < 1e-2
+
+
+def test_bn_stats_from_conv(gpu):
+    """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
+    torch.manual_seed(5)
+    x = bf(4, 16, 16, 64, dev=gpu)
+    w = bf(128, 3, 3, 64, dev=gpu, scale=0.05)
+    st = torch.zeros(2, 128, device=gpu)
+    z = C().conv_fwd(x, w, torch.empty(0, device=gpu), 1, 1, 1, 1, False, st)
+    g, b = torch.ones(128, device=gpu), torch.zeros(128, device=gpu)
+    e = torch.empty(0, device=gpu)
+    y1 = C().bn_fwd_train(z, st, g, b, torch.zeros(128, device=gpu), torch.ones(128, device=gpu),
+                          0.1, 1e-5, e, True)[0]
+    y2 = C().bn_fwd_train(z, e, g, b, torch.zeros(128, device=gpu), torch.ones(128, device=gpu),
+                          0.1, 1e-5, e, True)[0]
+    assert rel(y1, y2) < 1e-2
+
+
+@pytest.mark.parametrize("Cc", [64, 20])
+def test_act_bwd(gpu, Cc):
+    dy = bf(300, Cc, dev=gpu)
+    y = bf(300, Cc, dev=gpu)
+    db = torch.zeros(Cc, device=gpu)
+    db2 = db.clone()
+    g = C().act_bwd(dy, y, db)
+    g2 = ref.act_bwd(dy, y, db2)
+    assert rel(g, g2) < 1e-2 and rel(db, db2) < 1e-2
+
+
+POOL_CASES = [
+    (2, 112, 112, 64, 3, 3, 2, 2, 1, 1, False),   # resnet maxpool
+    (2, 55, 55, 96, 3, 3, 2, 2, 0, 0, True),      # squeezenet ceil
+    (2, 14, 14, 32, 2, 2, 2, 2, 0, 0, False),     # vgg
+    (2, 9, 9, 12, 3, 3, 2, 2, 0, 0, False),       # scalar channels
+]
+
+
+@pytest.mark.parametrize("case", POOL_CASES)
+def test_maxpool(gpu, case):
+    N, H, W, Cc, kh, kw, sh, sw, ph, pw, ceil = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    y, idx = C().maxpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil)
+    yr, idxr = ref.maxpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil)
+    assert y.shape == yr.shape and rel(y, yr) < 1e-6
+    dy = bf(*y.shape, dev=gpu)
+    dx = C().maxpool_bwd(dy, idx, H, W, kh, kw, sh, sw, ph, pw, ceil)
+    dxr = ref.maxpool_bwd(dy, idxr, H, W, kh, kw, sh, sw, ph, pw, ceil)
+    assert rel(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("case", POOL_CASES + [(2, 35, 35, 64, 3, 3, 1, 1, 1, 1, False),
+                                               (2, 17, 17, 64, 5, 5, 3, 3, 0, 0, False)])
+@pytest.mark.parametrize("cip", [True, False])
+def test_avgpool(gpu, case, cip):
+    N, H, W, Cc, kh, kw, sh, sw, ph, pw, ceil = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    y = C().avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, cip)
+    yr = ref.avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, cip)
+    assert y.shape == yr.shape and rel(y, yr) < 1e-2
+    dy = bf(*y.shape, dev=gpu)
+    dx = C().avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, cip)
+    assert rel(dx, ref.avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, cip)) < 1e-2
+
+
+@pytest.mark.parametrize("shape,out", [((2, 7, 7, 512), (1, 1)), ((2, 13, 13, 100), (1, 1)),
+                                       ((2, 14, 14, 64), (7, 7)), ((2, 13, 13, 16), (6, 6)),
+                                       ((2, 5, 5, 8), (7, 7))])
+def test_adaptive_avgpool(gpu, shape, out):
+    x = bf(*shape, dev=gpu)
+    y = C().adaptive_avgpool_fwd(x, *out)
+    assert rel(y, ref.adaptive_avgpool_fwd(x, *out)) < 1e-2
+    dy = bf(*y.shape, dev=gpu)
+    dx = C().adaptive_avgpool_bwd(dy, shape[1], shape[2])
+    assert rel(dx, ref.adaptive_avgpool_bwd(dy, shape[1], shape[2])) < 1e-2
+
+
+@pytest.mark.parametrize("B,NC", [(128, 64500), (7, 1000), (5, 33)])
+def test_cross_entropy(gpu, B, NC):
+    logits = bf(B, NC, dev=gpu, scale=3.0)
+    labels = torch.randint(0, NC, (B,), device=gpu)
+    loss, lse = C().ce_fwd(logits, labels)
+    lr_, lser = ref.ce_fwd(logits, labels)
+    assert abs(float(loss) - float(lr_)) < 1e-3 * max(1.0, abs(float(lr_)))
+    assert rel(lse, lser) < 1e-4
+    go = torch.full((1,), 0.7, device=gpu)
+    d = C().ce_bwd(logits, labels, lse, go)
+    assert rel(d, ref.ce_bwd(logits, labels, lser, go)) < 2e-2
+    cnt = torch.zeros(1, dtype=torch.int64, device=gpu)
+    cnt2 = cnt.clone()
+    logits2 = logits.clone()
+    logits2[torch.arange(B), labels] = 100.0
+    logits2[0, (int(labels[0]) + 1) % NC] = 200.0
+    C().argmax_correct(logits2, labels, cnt)
+    ref.argmax_correct(logits2, labels, cnt2)
+    assert int(cnt) == int(cnt2) == B - 1
+
+
+def test_adam_sgd(gpu):
+    n = 4096 + 64
+    for kind in ("adam", "sgd"):
+        p = torch.randn(n, device=gpu)
+        g = torch.randn(n, device=gpu)
+        s1 = torch.zeros(n, device=gpu)
+        s2 = torch.zeros(n, device=gpu)
+        sh = torch.zeros(n, dtype=torch.bfloat16, device=gpu)
+        p2, s1b, s2b, shb = p.clone(), s1.clone(), s2.clone(), sh.clone()
+        for it in range(3):
+            st = torch.full((1,), float(it), device=gpu)
+            if kind == "adam":
+                C().adam_step(p, g, s1, s2, sh, st, 1e-2, 0.9, 0.999, 1e-8, 0.01, 0.5)
+                ref.adam_step(p2, g, s1b, s2b, shb, st, 1e-2, 0.9, 0.999, 1e-8, 0.01, 0.5)
+            else:
+                C().sgd_step(p, g, s1, sh, st, 1e-2, 0.9, 0.0, 0.01, it == 1, 0.5)
+                ref.sgd_step(p2, g, s1b, shb, st, 1e-2, 0.9, 0.0, 0.01, it == 1, 0.5)
+        assert rel(p, p2) < 1e-5
+        assert rel(sh.float(), p2) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("src,dst", [((64, 80), (32, 32)), ((224, 224), (224, 224)),
+                                     ((100, 60), (128, 128))])
+def test_preprocess(gpu, mode, src, dst):
+    img = torch.randint(0, 256, (2, src[0], src[1], 3), dtype=torch.uint8, device=gpu)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    out = C().preprocess(img, dst[0], dst[1], list(mean), list(std), mode, 8)
+    r = ref.preprocess(img, dst[0], dst[1], mean, std, mode, 8, torch.float32)
+    assert out.shape == (2, dst[0], dst[1], 8)
+    assert float((out.float() - r).abs().max()) < 0.05
+    assert float(out[..., 3:].float().abs().max()) == 0.0
+
+
+def test_dropout(gpu):
+    x = torch.ones(1 << 16, device=gpu, dtype=torch.bfloat16)
+    y, m = C().dropout_fwd(x, 0.5, 7, 1)
+    keep = m.float().mean().item()
+    assert 0.47 < keep < 0.53
+    assert torch.allclose(y.float(), m.float() * 2.0)
+    y2, m2 = C().dropout_fwd(x, 0.5, 7, 2)
+    assert not torch.equal(m, m2)
+    dx = C().dropout_bwd(torch.ones_like(x), m, 0.5)
+    assert torch.allclose(dx.float(), m.float() * 2.0)
