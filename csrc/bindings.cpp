@@ -94,7 +94,11 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
     ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
     wsp = ws.data_ptr<float>();
   }
-  mpa::igemm_rows(a, vec_width(C), wsp, cur_stream());
+  Tensor slab;
+  if (a.stats)
+    slab = torch::empty({mpa::igemm_slab_floats(a.M, a.N)}, x.options().dtype(torch::kFloat32));
+  mpa::igemm_rows(a, vec_width(C), wsp, a.stats ? slab.data_ptr<float>() : nullptr,
+                  cur_stream());
   return y;
 }
 
@@ -174,8 +178,14 @@ Tensor act_bwd(Tensor dy, Tensor y, Tensor dbias) {
   if (!hy && !has(dbias)) return dy;
   const c10::OptionalDeviceGuard g(device_of(dy));
   Tensor out = hy ? torch::empty_like(dy) : dy;
+  Tensor ws;
+  float* wsp = nullptr;
+  if (has(dbias) && C % 8 == 0) {
+    ws = torch::empty({mpa::bn_ws_floats(M, C)}, dy.options().dtype(torch::kFloat32));
+    wsp = ws.data_ptr<float>();
+  }
   mpa::act_bwd(bp(dy), hy ? bopt(y) : nullptr, fopt_mut(dbias), M, C, hy ? bpm(out) : nullptr,
-               cur_stream());
+               wsp, cur_stream());
   return out;
 }
 
@@ -189,8 +199,9 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor st = stats;
   if (!has(st)) {
-    st = torch::zeros({2, C}, x.options().dtype(torch::kFloat32));
-    mpa::bn_stats(bp(x), M, C, st.data_ptr<float>(), cur_stream());
+    st = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
+    Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
+    mpa::bn_stats(bp(x), M, C, st.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
   }
   Tensor y = torch::empty_like(x);
   Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
@@ -225,7 +236,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
   Tensor gout = want_g ? torch::empty_like(x) : Tensor();
-  Tensor ws = torch::empty({2 * C}, x.options().dtype(torch::kFloat32));
+  Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
   mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
               fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr, want_g ? bpm(gout) : nullptr,
               ws.data_ptr<float>(), cur_stream());
@@ -345,7 +356,7 @@ Tensor linear_fwd(Tensor x, Tensor w, Tensor bias, bool relu) {
     ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
     wsp = ws.data_ptr<float>();
   }
-  mpa::igemm_rows(a, vec_width(Cin), wsp, cur_stream());
+  mpa::igemm_rows(a, vec_width(Cin), wsp, nullptr, cur_stream());
   return y;
 }
 

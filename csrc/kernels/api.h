@@ -53,13 +53,17 @@ struct WGradArgs {
 };
 
 // igemm.hip
-void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s);        // B K-contiguous
+int64_t igemm_slab_floats(int M, int N);
+void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s);  // B K-contig
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-contiguous
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
 bool igemm_wants_split(int M, int N, int Ktot);  // true => pass an M*N fp32 workspace
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
-void bn_stats(const bf16_raw* x, int M, int C, float* stats, hipStream_t s);
+// ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)
+int64_t bn_ws_floats(int M, int C);
+void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
+void bn_stats(const bf16_raw* x, int M, int C, float* stats, float* ws, hipStream_t s);
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s);
@@ -70,7 +74,7 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s);
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
-             hipStream_t s);
+             float* ws, hipStream_t s);
 void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s);
 
 // pool.hip  (NHWC)

@@ -60,7 +60,7 @@ __device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float*
 
 // ---------------------------------------------------------------------- statistics
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, int M,
-                                                        int C, float* __restrict__ stats) {
+                                                        int C, float* __restrict__ slab) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float s[8], q[8];
@@ -79,8 +79,8 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   if (cm.active && cm.r0 == 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      atomicAdd(stats + cm.cc * 8 + j, s[j]);
-      atomicAdd(stats + C + cm.cc * 8 + j, q[j]);
+      slab[(size_t)blockIdx.x * 2 * C + cm.cc * 8 + j] = s[j];
+      slab[(size_t)blockIdx.x * 2 * C + C + cm.cc * 8 + j] = q[j];
     }
   }
 }
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd, int M, int C,
-    float* __restrict__ ws) {
+    float* __restrict__ slab) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float sg[8], sgx[8];
@@ -205,8 +205,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   if (cm.active && cm.r0 == 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      atomicAdd(ws + cm.cc * 8 + j, sg[j]);
-      atomicAdd(ws + C + cm.cc * 8 + j, sgx[j]);
+      slab[(size_t)blockIdx.x * 2 * C + cm.cc * 8 + j] = sg[j];
+      slab[(size_t)blockIdx.x * 2 * C + C + cm.cc * 8 + j] = sgx[j];
     }
   }
 }
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 // g = dy * (y > 0) ; dbias += colsum(g)
 __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__ dy,
                                                        const bf16_t* __restrict__ y,
-                                                       float* __restrict__ dbias, int M, int C,
+                                                       float* __restrict__ slab, int M, int C,
                                                        bf16_t* __restrict__ g) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
@@ -288,11 +288,11 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__
       for (int j = 0; j < 8; ++j) s[j] += f[j];
     }
   }
-  if (!dbias) return;
+  if (!slab) return;
   block_reduce8(s, cm, red);
   if (cm.active && cm.r0 == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(dbias + cm.cc * 8 + j, s[j]);
+    for (int j = 0; j < 8; ++j) slab[(size_t)blockIdx.x * C + cm.cc * 8 + j] = s[j];
   }
 }
 
@@ -327,9 +327,43 @@ __global__ void relu_kernel(const bf16_t* __restrict__ x, int64_t n8, bf16_t* __
   }
 }
 
+// Cross-block reduction of per-block partial sums (replaces same-address fp32 atomics,
+// which serialise at the memory-side atomic unit when thousands of blocks target the
+// same 2*C words - MI355X_MICROARCH.md "Global float atomics", contention row).
+// out[w] += sum_s slab[s*W + w]; 64 columns x 4 slab groups per block, <= 32 adds/word.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int S,
+                                                           int W, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int w = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (w < W)
+    for (int s_ = blockIdx.y * 4 + g; s_ < S; s_ += gridDim.y * 4) acc += slab[(size_t)s_ * W + w];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (g == 0 && w < W) {
+    acc = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    if (gridDim.y == 1) out[w] += acc;
+    else atomicAdd(out + w, acc);
+  }
+}
+
+void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s) {
+  if (zero_out) (void)hipMemsetAsync(out, 0, sizeof(float) * W, s);
+  const int gy = std::max(1, std::min(32, (S + 63) / 64));
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 63) / 64, gy), dim3(256), 0, s, slab, S, W, out);
+}
+
+int64_t bn_ws_floats(int M, int C) {
+  const dim3 g = grid_for(M, C);
+  return (int64_t)g.x * 2 * C + 2 * C;
+}
+
 // ------------------------------------------------------------------------ launchers
-void bn_stats(const bf16_raw* x, int M, int C, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL(bn_stats_kernel, grid_for(M, C), dim3(256), 0, s, x, M, C, stats);
+void bn_stats(const bf16_raw* x, int M, int C, float* stats, float* ws, hipStream_t s) {
+  const dim3 g = grid_for(M, C);
+  hipLaunchKernelGGL(bn_stats_kernel, g, dim3(256), 0, s, x, M, C, ws);
+  slab_reduce(ws, g.x, 2 * C, stats, true, s);
 }
 
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
@@ -349,18 +383,23 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s) {
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C, s);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid_for(M, C), dim3(256), 0, s, dy, x, y, mean, rstd,
-                     M, C, ws);
+  // ws layout: [2C] final sums | [gx][2C] per-block partials
+  const dim3 gr = grid_for(M, C);
+  float* slab = ws + 2 * C;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, gr, dim3(256), 0, s, dy, x, y, mean, rstd, M, C, slab);
+  slab_reduce(slab, gr.x, 2 * C, ws, true, s);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, grid_for(M, C), dim3(256), 0, s, dy, x, y, mean, rstd,
                      gamma, ws, dgamma, dbeta, M, C, dx, g);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
-             hipStream_t s) {
-  if (C % 8 == 0)
-    hipLaunchKernelGGL(act_bwd_kernel, grid_for(M, C), dim3(256), 0, s, dy, y, dbias, M, C, g);
-  else
+             float* ws, hipStream_t s) {
+  if (C % 8 == 0) {
+    const dim3 gr = grid_for(M, C);
+    hipLaunchKernelGGL(act_bwd_kernel, gr, dim3(256), 0, s, dy, y, dbias ? ws : (float*)nullptr, M,
+                       C, g);
+    if (dbias) slab_reduce(ws, gr.x, C, dbias, false, s);
+  } else
     hipLaunchKernelGGL(act_bwd_generic_kernel, dim3((C + 255) / 256), dim3(256), 0, s, dy, y,
                        dbias, M, C, g);
 }

@@ -414,17 +414,31 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
           s[j][r] = a;
           q[j][r] = b;
         }
+      // cross-wave (WM waves share columns) reduction through the now idle LDS, then one
+      // plain store per column into this M-tile's row of the statistics slab - no
+      // contended same-address atomics; the slab is summed by slab_reduce afterwards.
+      float* red = (float*)smem;
       if ((lane & 15) == 0) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wcol0 + j * 16 + nl;
+          const int col = wcol0 + j * 16 + nl;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) {
-              atomicAdd(p.stats + n + r, s[j][r]);
-              atomicAdd(p.stats + p.N + n + r, q[j][r]);
-            }
+          for (int r = 0; r < 4; ++r) {
+            red[(wm * BN + col + r) * 2] = s[j][r];
+            red[(wm * BN + col + r) * 2 + 1] = q[j][r];
+          }
         }
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < p.N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          a += red[(w * BN + tid) * 2];
+          b += red[(w * BN + tid) * 2 + 1];
+        }
+        p.stats[(size_t)mt * 2 * p.N + n0 + tid] = a;
+        p.stats[(size_t)mt * 2 * p.N + p.N + n0 + tid] = b;
       }
     }
   }
@@ -607,8 +621,10 @@ __global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
 // ----------------------------------------------------------- split-K finalize (fp32->bf16)
 __global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
                                        int M, int N, const float* __restrict__ bias, int relu,
-                                       float* __restrict__ stats) {
-  // one block per 64 columns x (rows strided by gridDim.y)
+                                       float* __restrict__ slab) {
+  // one block per 64 columns x (rows strided by gridDim.y); statistics go to the
+  // per-block-row slab [gridDim.y][2N] (reduced by slab_reduce)
+  __shared__ float red[2][256];
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * 4 + (threadIdx.x >> 6);
   float s = 0.f, q = 0.f;
@@ -623,9 +639,15 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __r
       s += rv;
       q += rv * rv;
     }
-    if (stats) {
-      atomicAdd(stats + n, s);
-      atomicAdd(stats + N + n, q);
+  }
+  if (slab) {
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = q;
+    __syncthreads();
+    if (threadIdx.x < 64 && n < N) {
+      const int t = threadIdx.x;
+      slab[(size_t)blockIdx.y * 2 * N + n] = red[0][t] + red[0][t + 64] + red[0][t + 128] + red[0][t + 192];
+      slab[(size_t)blockIdx.y * 2 * N + N + n] = red[1][t] + red[1][t + 64] + red[1][t + 128] + red[1][t + 192];
     }
   }
 }
@@ -680,7 +702,16 @@ bool igemm_wants_split(int M, int N, int Ktot) {
   return choose_splits(tiles, (Ktot + BK - 1) / BK, Ktot) > 1;
 }
 
-void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s) {
+int64_t igemm_slab_floats(int M, int N) {
+  const int BN = choose_bn(N);
+  const int BM = (BN == 64) ? 256 : 128;
+  const int tiles_m = (M + BM - 1) / BM;
+  return (int64_t)std::max(tiles_m, 64) * 2 * N;
+}
+
+// `a.stats` (if set) receives the final [2][N] column sum / sum-of-squares; `slab` is a
+// workspace of igemm_slab_floats(M, N) floats for the per-tile partials.
+void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
   const int BN = choose_bn(a.N);
   const int BM = (BN == 64) ? 256 : 128;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -692,6 +723,7 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s) {
   splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
   void* final_out = a.C;
   float* stats = a.stats;
+  a.stats = stats ? slab : nullptr;
   if (splits > 1) {
     (void)hipMemsetAsync(ws, 0, (size_t)a.M * a.N * sizeof(float), s);
     a.C = ws;
@@ -700,11 +732,15 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, hipStream_t s) {
   if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
   else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);
   else dispatch_split<128, 32, 4, 1, true>(a, vw, splits, s);
+  int slab_rows = tiles_m;
   if (splits > 1) {
-    dim3 grid((a.N + 63) / 64, std::min(64, (a.M + 3) / 4));
+    const int gy = std::min(64, (a.M + 3) / 4);
+    dim3 grid((a.N + 63) / 64, gy);
     hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
-                       a.M, a.N, a.bias, a.relu, stats);
+                       a.M, a.N, a.bias, a.relu, stats ? slab : (float*)nullptr);
+    slab_rows = gy;
   }
+  if (stats) slab_reduce(slab, slab_rows, 2 * a.N, stats, true, s);
 }
 
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {

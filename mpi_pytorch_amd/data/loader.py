@@ -58,7 +58,7 @@ class DevicePrefetcher:
     def __init__(self, device: torch.device, batch: int, src_hw: Tuple[int, int],
                  out_hw: Tuple[int, int], num_classes: int, seed: int = 0, rank: int = 0,
                  world: int = 1, depth: int = 4, threads: int = 2, mode: int = 0,
-                 cpad: int = 3, ring=None):
+                 cpad: int = 8, ring=None):
         self.device = torch.device(device)
         self.batch = batch
         self.src_hw = src_hw

@@ -1,0 +1,81 @@
+"""Manifest (CSV) handling and per-row image sources.
+
+Reference: rank 0 reads ``test_sample.csv`` / ``train_sample.csv`` (``main.py:73-82``);
+in DEBUG it draws ``sample(1000, random_state=0)`` from the test manifest and splits it
+80/20 with ``train_test_split`` (800 training rows).  ``GetData`` (``data_loader.py:6-39``)
+opens ``TRAIN_DIR/file_name`` with PIL and returns ``(transform(img), label)``; labels
+are the raw ``category_id`` values used directly as class indices (``data_loader.py:37``).
+
+Image sources:
+* :class:`FolderImages` - real JPEGs decoded by PIL worker threads (PIL releases the
+  GIL while decoding), uint8 HWC arrays of varying size;
+* :class:`SyntheticImages` - no Herbarium images exist offline (BASELINE.json: synthetic
+  data), so each manifest row gets a deterministic pseudo-random uint8 image keyed by its
+  file name (same pixels on every rank/epoch) at a fixed "decoded" size.
+"""
+from __future__ import annotations
+
+import os
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+try:
+    import pandas as pd
+except Exception:  # pragma: no cover
+    pd = None
+
+
+def read_manifests(cfg):
+    """Rank-0 manifest read (main.py:73-82).  Returns (train_df, test_df)."""
+    if cfg.DEBUG:
+        from sklearn.model_selection import train_test_split
+        df_test = pd.read_csv(cfg.TEST_CSV)
+        sample = df_test.sample(min(cfg.DEBUG_SAMPLE, len(df_test)), random_state=0)
+        sample = sample.reset_index(drop=True).copy()
+        train_sample, test_sample = train_test_split(sample, test_size=0.2,
+                                                     random_state=cfg.seed)
+        return train_sample.copy(), test_sample.copy()
+    return pd.read_csv(cfg.TRAIN_CSV), pd.read_csv(cfg.TEST_CSV)
+
+
+def synthetic_manifest(n: int, num_classes: int, seed: int = 0):
+    rng = np.random.default_rng(seed)
+    return pd.DataFrame({
+        "file_name": ["synthetic/{:08d}.jpg".format(i) for i in range(n)],
+        "category_id": rng.integers(0, num_classes, size=n),
+    })
+
+
+class SyntheticImages:
+    def __init__(self, hw: Tuple[int, int]):
+        self.hw = hw
+
+    def load(self, names: Sequence[str]) -> np.ndarray:
+        out = np.empty((len(names), self.hw[0], self.hw[1], 3), dtype=np.uint8)
+        for i, n in enumerate(names):
+            rng = np.random.default_rng(zlib.crc32(str(n).encode()))
+            out[i] = rng.integers(0, 256, size=(self.hw[0], self.hw[1], 3), dtype=np.uint8)
+        return out
+
+
+class FolderImages:
+    """PIL decode of ``root/file_name`` in a thread pool; returns a list of HWC uint8."""
+
+    def __init__(self, root: str, workers: int = 4):
+        self.root = root
+        self.pool = ThreadPoolExecutor(max_workers=max(1, workers))
+
+    def _one(self, name: str) -> np.ndarray:
+        from PIL import Image
+        with Image.open(os.path.join(self.root, name)) as im:
+            return np.asarray(im.convert("RGB"))
+
+    def load(self, names: Sequence[str]) -> List[np.ndarray]:
+        return list(self.pool.map(self._one, names))
+
+
+def images_available(root: str, names: Sequence[str]) -> bool:
+    return bool(names) and os.path.exists(os.path.join(root, str(names[0])))

@@ -1,0 +1,225 @@
+"""Data-parallel training driver: the reference ``main.py::main()`` workflow
+(``/root/reference/main.py:49-185``) on the MI355X engine.
+
+Workflow parity (and the reference lines it mirrors):
+  * logger + ``Logger Initialized`` on rank 0 (main.py:22-46)
+  * rank 0 reads/samples/splits the manifest (main.py:73-82); shards with
+    ``np.array_split`` semantics and scatters them (main.py:84,91) -> ``_Files Received``
+  * train loader over the shard (bs=BATCH_SIZE, shuffle) and, on rank 0, a validation
+    loader over ``train_sample`` (main.py:99-112)
+  * ``initialize_model`` + Adam(lr=LR) (main.py:121-126); optional resume (main.py:127-130)
+  * broadcast of rank-0 parameters (main.py:131)
+  * epochs: train, per-rank ``_Epoch: e | Train Loss: l | Time: t`` (main.py:142-160);
+    rank-0 checkpoint every epoch (main.py:162-171) and validation accuracy
+    (main.py:173-185)
+
+Engine differences (MI355X-first): NHWC/bf16 fused MFMA kernels, flat-arena bucketed RCCL
+all-reduce overlapped with backward, fused optimizer, GPU preprocessing, a prefetch
+thread for the host image work, device-side loss accumulation (one host sync per epoch
+instead of one per step), equal step counts on every rank (the reference can deadlock
+when shard batch counts differ), resume honours the saved epoch.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..config import Config
+from ..checkpoint import save_checkpoint, load_checkpoint, build_state, checkpoint_path
+from ..data.manifest import (read_manifests, synthetic_manifest, SyntheticImages, FolderImages,
+                             images_available)
+from ..data.loader import IMAGENET_MEAN, IMAGENET_STD
+from ..ops import functional as Fn
+from ..parallel import (init_world, get_world, barrier, scatter_object, broadcast_object,
+                        shard_dataframe, array_split_sizes, replica_checksum)
+from ..parallel.sharding import equal_step_count
+from ..utils.logging import init_logger, MetricsWriter
+from .step import build_training
+
+
+class ManifestBatches:
+    """Batches of a manifest shard -> model-ready NHWC tensors on ``device``.
+
+    Host work (synthetic generation or PIL decode) for batch i+1 runs in a worker thread
+    while the GPU trains on batch i; images are copied pinned/non-blocking and
+    normalised by the GPU preprocess kernel (bilinear resize, no antialias - the
+    reference's ToTensor -> Resize -> Normalize on tensors, main.py:62-65)."""
+
+    def __init__(self, names: Sequence[str], labels: Sequence[int], batch: int, out_hw,
+                 device, source, shuffle: bool, seed: int = 0, mode: int = 0, cpad: int = 8):
+        self.names = list(names)
+        self.labels = np.asarray(labels, dtype=np.int64)
+        self.batch = batch
+        self.out_hw = out_hw
+        self.device = torch.device(device)
+        self.source = source
+        self.shuffle = shuffle
+        self.seed = seed
+        self.mode = mode
+        self.cpad = cpad
+        self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def __len__(self):
+        return (len(self.names) + self.batch - 1) // self.batch
+
+    def _host(self, idx):
+        names = [self.names[i] for i in idx]
+        return self.source.load(names), torch.from_numpy(self.labels[idx])
+
+    def _to_device(self, imgs, labels):
+        cuda = self.device.type == "cuda"
+        if isinstance(imgs, np.ndarray):
+            groups = [torch.from_numpy(imgs)]
+        else:
+            groups = [torch.from_numpy(np.ascontiguousarray(a))[None] for a in imgs]
+        outs = []
+        for g in groups:
+            if cuda:
+                g = g.pin_memory().to(self.device, non_blocking=True)
+            outs.append(Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
+                                      self.cpad, out_dtype=torch.float32))
+        x = outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+        y = labels.to(self.device, non_blocking=cuda)
+        return x, y
+
+    def epoch(self, e: int, steps: Optional[int] = None):
+        order = np.arange(len(self.names))
+        if self.shuffle:
+            np.random.default_rng(self.seed * 7919 + e).shuffle(order)
+        n = len(self)
+        if steps is not None:
+            n = min(n, steps)
+        chunks = [order[i * self.batch:(i + 1) * self.batch] for i in range(n)]
+        fut = self.pool.submit(self._host, chunks[0]) if chunks else None
+        for i in range(len(chunks)):
+            imgs, labels = fut.result()
+            if i + 1 < len(chunks):
+                fut = self.pool.submit(self._host, chunks[i + 1])
+            yield self._to_device(imgs, labels)
+
+
+def _image_source(cfg: Config, names: Sequence[str], src_hw):
+    if not cfg.synthetic and images_available(cfg.TRAIN_DIR, names):
+        return FolderImages(cfg.TRAIN_DIR, cfg.num_workers)
+    return SyntheticImages(src_hw)
+
+
+def run_training(cfg: Config) -> dict:
+    world = init_world(cfg.device, cfg.timeout_s)
+    rank, size = world.rank, world.world_size
+    log = init_logger(rank, cfg.log_file, cfg.log_per_rank_files)
+    metrics = MetricsWriter(cfg.metrics_jsonl, rank)
+    torch.manual_seed(cfg.seed)
+    if rank == 0:
+        log.info("Logger Initialized")
+
+    # ---------------------------------------------------------------- manifests
+    shards = None
+    train_sample = None
+    if rank == 0:
+        log.info("Reading Training & Testing samples")
+        if cfg.synthetic_images > 0 or not os.path.exists(cfg.TEST_CSV):
+            n = cfg.synthetic_images or 800
+            train_sample = synthetic_manifest(n, cfg.NUM_CLASSES, cfg.seed)
+        else:
+            train_sample, _test = read_manifests(cfg)
+        shards = shard_dataframe(train_sample, size)
+    my = scatter_object(shards, root=0)
+    log.info("_Files Received: {}".format(len(my)))
+    n_total = int(broadcast_object(len(train_sample) if rank == 0 else None))
+    steps_per_epoch = equal_step_count(array_split_sizes(n_total, size), cfg.BATCH_SIZE)
+    if cfg.max_steps:
+        steps_per_epoch = min(steps_per_epoch, cfg.max_steps)
+
+    out_hw = cfg.input_hw
+    if cfg.MODEL_NAME == "inception" and min(out_hw) < 299:
+        out_hw = (299, 299)  # aux head needs 17x17 Mixed_6e maps
+    src_hw = (max(out_hw[0], 2 * out_hw[0]), max(out_hw[1], 2 * out_hw[1]))
+    source = _image_source(cfg, list(my["file_name"].values), src_hw)
+    dev = world.device
+    train_loader = ManifestBatches(my["file_name"].values, my["category_id"].values,
+                                   cfg.BATCH_SIZE, out_hw, dev, source, True, cfg.seed + rank)
+    log.info("_Training Dataset Object Created")
+    log.info("_Training Loader Created")
+    val_loader = None
+    if rank == 0 and cfg.VALIDATE:
+        # reference validates on train_sample (main.py:108), not the test split
+        val_loader = ManifestBatches(train_sample["file_name"].values,
+                                     train_sample["category_id"].values, cfg.BATCH_SIZE,
+                                     out_hw, dev, source, False)
+        log.info("_Validation Dataset Object Created")
+        log.info("_Validation Loader Created")
+
+    # ------------------------------------------------------------------- model
+    model, opt, step, _input_size = build_training(
+        cfg.MODEL_NAME, cfg.NUM_CLASSES, dev, world, cfg.LR, cfg.optimizer, cfg.momentum,
+        cfg.weight_decay, cfg.FEATURE_EXTRACT, cfg.bucket_mb, cfg.overlap_comm,
+        cfg.grad_comm_dtype)
+    log.info("_Model Created: {}".format(cfg.MODEL_NAME))
+    log.info("_Optimizer Created")
+    start_epoch = 0
+    ckpt = os.path.join(cfg.CHECKPOINT_DIR, cfg.CHECKPOINT_NAME)
+    if cfg.FROM_CHECKPOINT:
+        log.info("_Loading Checkpoint")
+        _m, _o, saved_epoch = load_checkpoint(ckpt, model, opt, map_location="cpu")
+        start_epoch = saved_epoch + 1 if cfg.resume_epoch else 0
+        log.info("_Checkpoint loaded")
+    from ..parallel import sync_params
+    sync_params(model)
+    log.info("_Model loaded to {}".format("GPU" if dev.type == "cuda" else "CPU"))
+    log.info("_Entering training Loop")
+
+    history = []
+    for epoch in range(start_epoch, cfg.NUM_EPOCHS):
+        model.train()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        nimg = 0
+        for x, y in train_loader.epoch(epoch, steps_per_epoch):
+            step(x, y)
+            nimg += x.shape[0]
+        tr_loss = step.mean_loss()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        log.info("_Epoch: {} | Train Loss: {} | Time: {}".format(epoch, tr_loss, dt))
+        rec = {"epoch": epoch, "train_loss": tr_loss, "time_s": dt,
+               "img_per_s_rank": nimg / dt if dt > 0 else 0.0,
+               "img_per_s_global": nimg * size / dt if dt > 0 else 0.0}
+        if cfg.checksum_every and size > 1:
+            rec["replicas_consistent"] = replica_checksum(model)
+        if rank == 0:
+            log.info("_Creating a checkpoint at epoch {}".format(epoch))
+            save_checkpoint(build_state(epoch, model, opt, tr_loss), epoch, cfg.MODEL_NAME,
+                            cfg.CHECKPOINT_DIR, cfg.MODELS_DIR)
+            log.info("_Checkpoint saved")
+            if val_loader is not None:
+                log.info("_Evaluating model")
+                acc = evaluate(model, val_loader)
+                rec["acc"] = acc
+                log.info("_Epoch: {} | Acc: {}".format(epoch, acc))
+        metrics.write(**rec)
+        history.append(rec)
+    return {"history": history, "checkpoint": ckpt}
+
+
+@torch.no_grad()
+def evaluate(model, loader: ManifestBatches) -> float:
+    """Rank-0 accuracy over a loader (main.py:173-185)."""
+    model.eval()
+    dev = loader.device
+    count = torch.zeros(1, dtype=torch.int64, device=dev)
+    n = 0
+    for x, y in loader.epoch(0):
+        out = model(x)
+        Fn.count_correct(out, y, count)
+        n += x.shape[0]
+    model.train()
+    return float(count.item()) / max(n, 1)

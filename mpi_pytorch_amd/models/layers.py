@@ -36,12 +36,20 @@ def _oihw_to_krsc(t):
 
 
 class Conv2d(nn.Module):
-    """Conv2d with KRSC weight storage. ``state_dict`` exposes OIHW like ``nn.Conv2d``."""
+    """Conv2d with KRSC weight storage. ``state_dict`` exposes OIHW like ``nn.Conv2d``.
+
+    Image-input stems (``in_channels < 8``) store their weight with the channel dim
+    zero-padded to 8 (``cin_store``): the input images are produced with 8 channels by the
+    preprocess kernel, so the stem conv takes the 16-byte vector gather path; the zero
+    channels contribute exactly nothing and receive exactly zero gradient.  The padding is
+    invisible in state_dict / optimizer state (sliced off on export, re-added on import).
+    """
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size, stride=1, padding=0,
                  bias: bool = True):
         super().__init__()
         self.in_channels = in_channels
+        self.cin_store = 8 if in_channels < 8 else in_channels
         self.out_channels = out_channels
         self.kernel_size = _pair(kernel_size)
         self.stride = _pair(stride)
@@ -49,9 +57,9 @@ class Conv2d(nn.Module):
         kh, kw = self.kernel_size
         w = torch.empty(out_channels, in_channels, kh, kw)
         nn.init.kaiming_uniform_(w, a=math.sqrt(5))
-        self.weight = nn.Parameter(_oihw_to_krsc(w).contiguous())
-        self.weight._mpa_export = _krsc_to_oihw
-        self.weight._mpa_import = _oihw_to_krsc
+        self.weight = nn.Parameter(self._imp(w).contiguous())
+        self.weight._mpa_export = self._exp
+        self.weight._mpa_import = self._imp
         if bias:
             fan_in = in_channels * kh * kw
             bound = 1 / math.sqrt(fan_in)
@@ -59,12 +67,23 @@ class Conv2d(nn.Module):
         else:
             self.register_parameter("bias", None)
 
+    def _exp(self, t):  # internal KRSC (maybe channel padded) -> OIHW
+        if self.cin_store != self.in_channels:
+            t = t[..., :self.in_channels]
+        return _krsc_to_oihw(t)
+
+    def _imp(self, t):  # OIHW -> internal KRSC
+        t = _oihw_to_krsc(t)
+        if self.cin_store != self.in_channels:
+            t = F.pad(t, (0, self.cin_store - self.in_channels))
+        return t
+
     # init helpers operate in OIHW space so the distributions match torchvision
     def init_(self, fn) -> "Conv2d":
         with torch.no_grad():
             w = torch.empty(self.out_channels, self.in_channels, *self.kernel_size)
             fn(w)
-            self.weight.copy_(_oihw_to_krsc(w))
+            self.weight.copy_(self._imp(w))
         return self
 
     def _save_to_state_dict(self, destination, prefix, keep_vars):
@@ -72,7 +91,7 @@ class Conv2d(nn.Module):
         k = prefix + "weight"
         if k in destination:
             w = destination[k]
-            destination[k] = _krsc_to_oihw(w) if keep_vars else _krsc_to_oihw(w).contiguous()
+            destination[k] = self._exp(w) if keep_vars else self._exp(w).contiguous()
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
@@ -80,12 +99,19 @@ class Conv2d(nn.Module):
         if k in state_dict:
             w = state_dict[k]
             if tuple(w.shape) == (self.out_channels, self.in_channels, *self.kernel_size):
-                state_dict[k] = _oihw_to_krsc(w)
+                state_dict[k] = self._imp(w)
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
     def forward(self, x, relu: bool = False):
         return Fn.conv_act(x, self, relu=relu)
+
+    def fit_input(self, x):
+        """Zero-pad an image input's channel dim to the stored width (no-op normally)."""
+        c = x.shape[-1]
+        if c < self.cin_store:
+            x = F.pad(x, (0, self.cin_store - c))
+        return x
 
     def extra_repr(self):
         return "{}, {}, kernel_size={}, stride={}, padding={}, bias={}".format(

@@ -73,7 +73,7 @@ class _ConvBNAct(torch.autograd.Function):
         sh, sw = conv.stride
         ph, pw = conv.padding
         C = w.shape[0]
-        stats = torch.zeros(2, C, device=x.device, dtype=torch.float32)
+        stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
         z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats)
         y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
                                        bn.momentum_value(), bn.eps,
@@ -119,6 +119,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
     forward and running stats are exact; its gradient is exactly zero in exact arithmetic
     (BN removes any per-channel constant) and is left at zero instead of accumulating
     rounding noise."""
+    x = conv.fit_input(x)
     if bn.training:
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
                                 bn, relu)
@@ -167,6 +168,7 @@ class _ConvAct(torch.autograd.Function):
 
 
 def conv_act(x, conv, relu: bool = False):
+    x = conv.fit_input(x)
     if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
         return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu)
     k = K(x)

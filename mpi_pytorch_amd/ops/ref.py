@@ -55,10 +55,10 @@ def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats):
         y = torch.relu(y)
     y = y.to(x.dtype)
     st = _opt(stats)
-    if st is not None:
+    if st is not None:  # overwritten (not accumulated), like the native kernel
         yf = y.float().reshape(-1, y.shape[-1])
-        st[0].add_(yf.sum(0))
-        st[1].add_((yf * yf).sum(0))
+        st[0].copy_(yf.sum(0))
+        st[1].copy_((yf * yf).sum(0))
     return y
 
 
