@@ -45,6 +45,9 @@ def main(argv=None):
     p.add_argument("--bucket-mb", type=float, default=64.0)
     p.add_argument("--comm-dtype", default="fp32")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")
+    p.add_argument("--static-data", action="store_true",
+                   help="debug: reuse one device batch (no data pipeline in the loop)")
     args = p.parse_args(argv)
 
     from mpi_pytorch_amd.parallel import init_world, barrier, get_world
@@ -64,13 +67,30 @@ def main(argv=None):
     data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
                             world=world.world_size, depth=6, threads=4)
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and world.world_size == 1)
+    if args.static_data:
+        xs, ys = data.next()
+        data.next = lambda: (xs, ys)
+    # eager by default: the step is GPU-bound (host runs ahead), graph replay buys nothing
+    # measurable and needs a per-step sync for correctness (engine/step.py)
+    use_graph = args.graph == "on"
     if use_graph:
         x, y = data.next()
         use_graph = step.capture(x, y)
     for _ in range(args.warmup):
         x, y = data.next()
-        step(x, y)
+        loss = step(x, y)
+        if args.print_losses and world.rank == 0:
+            print("warmup loss %.4f" % float(loss), file=sys.stderr)
+    if args.print_losses:
+        for i in range(args.steps):
+            x, y = data.next()
+            print("step %d loss %.4f" % (i, float(step(x, y))), file=sys.stderr)
+        lazy = []
+        for i in range(args.steps):
+            x, y = data.next()
+            lazy.append(step(x, y).clone())
+        print("lazy losses:", " ".join("%.3f" % float(v) for v in lazy), file=sys.stderr)
+        print("loss_sum/steps: %.4f" % step.mean_loss(), file=sys.stderr)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -57,7 +57,7 @@ Tensor empty_like_shape(const Tensor& ref, at::IntArrayRef shape, torch::Dtype d
 
 // ------------------------------------------------------------------------------- conv
 Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                bool relu, Tensor stats) {
+                bool relu, Tensor stats, Tensor shift) {
   CHECK_ACT(x);
   CHECK_ACT(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: x NHWC, w KRSC");
@@ -87,6 +87,8 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
   a.dH = P; a.dW = Q; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   a.bias = fopt(bias);
   a.stats = fopt_mut(stats);
+  a.stats_shift = fopt(shift);
+  if (a.stats_shift) TORCH_CHECK(shift.numel() == K, "conv_fwd: shift size");
   a.relu = relu ? 1 : 0;
   Tensor ws;
   float* wsp = nullptr;
@@ -201,7 +203,8 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   if (!has(st)) {
     st = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
     Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
-    mpa::bn_stats(bp(x), M, C, st.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+    mpa::bn_stats(bp(x), M, C, fopt(rmean), st.data_ptr<float>(), ws.data_ptr<float>(),
+                  cur_stream());
   }
   Tensor y = torch::empty_like(x);
   Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));

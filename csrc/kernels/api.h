@@ -33,7 +33,8 @@ struct IGemmArgs {
   int ldc;
   int dH, dW, Uoh, Uow, Poh, Pow;
   const float* bias;
-  float* stats;
+  float* stats;              // [2][N]: finalized (mean, biased var) of the bf16 output
+  const float* stats_shift;  // per-column shift K for the sums (BN running mean) or null
   int relu;
   int ktiles_per_split;
   int tiles_n;
@@ -63,7 +64,11 @@ bool igemm_wants_split(int M, int N, int Ktot);  // true => pass an M*N fp32 wor
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)
 int64_t bn_ws_floats(int M, int C);
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
-void bn_stats(const bf16_raw* x, int M, int C, float* stats, float* ws, hipStream_t s);
+// sums [2][C] of (x - shift) and (x - shift)^2 over M rows -> out [mean(C), var(C)]
+void stats_finalize(const float* sums, const float* shift, int M, int C, float* out,
+                    hipStream_t s);
+void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,
+              hipStream_t s);
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s);

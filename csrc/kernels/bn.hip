@@ -60,18 +60,27 @@ __device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float*
 
 // ---------------------------------------------------------------------- statistics
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, int M,
-                                                        int C, float* __restrict__ slab) {
+                                                        int C, const float* __restrict__ shift,
+                                                        float* __restrict__ slab) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
-  float s[8], q[8];
+  float s[8], q[8], k[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; k[j] = 0.f; }
   if (cm.active) {
+    if (shift) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = shift[cm.cc * 8 + j];
+    }
     for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
       float f[8];
       unpack8(*(const uint4*)(x + (size_t)r * C + cm.cc * 8), f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+      for (int j = 0; j < 8; ++j) {
+        const float d = f[j] - k[j];
+        s[j] += d;
+        q[j] += d * d;
+      }
     }
   }
   block_reduce8(s, cm, red);
@@ -95,11 +104,10 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
   float sc[8], sh[8];
-  const float invM = 1.f / (float)M;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float mu = stats[c0 + j] * invM;
-    const float var = fmaxf(stats[C + c0 + j] * invM - mu * mu, 0.f);
+    const float mu = stats[c0 + j];       // finalized (mean, biased var)
+    const float var = stats[C + c0 + j];
     const float rs = rsqrtf(var + eps);
     sc[j] = gamma[c0 + j] * rs;
     sh[j] = beta[c0 + j] - mu * sc[j];
@@ -359,11 +367,31 @@ int64_t bn_ws_floats(int M, int C) {
   return (int64_t)g.x * 2 * C + 2 * C;
 }
 
+__global__ void stats_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ shift,
+                                      int M, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.f / (float)M;
+  const float d = sums[c] * inv;  // mean of (x - K)
+  const float k = shift ? shift[c] : 0.f;
+  out[c] = k + d;
+  out[C + c] = fmaxf(sums[C + c] * inv - d * d, 0.f);
+}
+
+void stats_finalize(const float* sums, const float* shift, int M, int C, float* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, shift,
+                     M, C, out);
+}
+
 // ------------------------------------------------------------------------ launchers
-void bn_stats(const bf16_raw* x, int M, int C, float* stats, float* ws, hipStream_t s) {
+void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,
+              hipStream_t s) {
   const dim3 g = grid_for(M, C);
-  hipLaunchKernelGGL(bn_stats_kernel, g, dim3(256), 0, s, x, M, C, ws);
-  slab_reduce(ws, g.x, 2 * C, stats, true, s);
+  hipLaunchKernelGGL(bn_stats_kernel, g, dim3(256), 0, s, x, M, C, shift, ws);
+  float* sums = ws + (int64_t)g.x * 2 * C;
+  slab_reduce(ws, g.x, 2 * C, sums, true, s);
+  stats_finalize(sums, shift, M, C, stats, s);
 }
 
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,

@@ -343,14 +343,19 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
-    f32x4 bias[TN];
+    f32x4 bias[TN], shift[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      shift[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int n = n0 + wcol0 + j * 16 + nl;
       if (p.bias) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? p.bias[n + r] : 0.f;
+      }
+      if (p.stats_shift) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? p.stats_shift[n + r] : 0.f;
       }
     }
 #pragma unroll
@@ -388,9 +393,10 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
             for (int r = 0; r < 4; ++r)
               if (n + r < p.N) out[orow + n + r] = e[r];
           }
-          // statistics on the bf16-rounded values BN will read
-          const float rv[4] = {bf2f(lo & 0xffff), bf2f(lo >> 16), bf2f(hi & 0xffff),
-                               bf2f(hi >> 16)};
+          // statistics on the bf16-rounded values BN will read, shifted by K ~ mean
+          // (BN running mean) so sum-of-squares does not cancel when |mean| >> std
+          const float rv[4] = {bf2f(lo & 0xffff) - shift[j][0], bf2f(lo >> 16) - shift[j][1],
+                               bf2f(hi & 0xffff) - shift[j][2], bf2f(hi >> 16) - shift[j][3]};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             s[j][r] += rv[r];
@@ -620,7 +626,8 @@ __global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
 // ----------------------------------------------------------- split-K finalize (fp32->bf16)
 __global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
                                        int M, int N, const float* __restrict__ bias, int relu,
-                                       float* __restrict__ slab) {
+                                       float* __restrict__ slab,
+                                       const float* __restrict__ shift) {
   // one block per 64 columns x (rows strided by gridDim.y); statistics go to the
   // per-block-row slab [gridDim.y][2N] (reduced by slab_reduce)
   __shared__ float red[2][256];
@@ -628,13 +635,14 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __r
   const int r0 = blockIdx.y * 4 + (threadIdx.x >> 6);
   float s = 0.f, q = 0.f;
   const float b = (bias && n < N) ? bias[n] : 0.f;
+  const float k = (shift && n < N) ? shift[n] : 0.f;
   if (n < N) {
     for (int m = r0; m < M; m += gridDim.y * 4) {
       float v = ws[(size_t)m * N + n] + b;
       if (relu) v = fmaxf(v, 0.f);
       const bf16_t o = f2bf(v);
       out[(size_t)m * N + n] = o;
-      const float rv = bf2f(o);
+      const float rv = bf2f(o) - k;
       s += rv;
       q += rv * rv;
     }
@@ -705,11 +713,12 @@ int64_t igemm_slab_floats(int M, int N) {
   const int BN = choose_bn(N);
   const int BM = (BN == 64) ? 256 : 128;
   const int tiles_m = (M + BM - 1) / BM;
-  return (int64_t)std::max(tiles_m, 64) * 2 * N;
+  return (int64_t)std::max(tiles_m, 64) * 2 * N + 2 * N;
 }
 
-// `a.stats` (if set) receives the final [2][N] column sum / sum-of-squares; `slab` is a
-// workspace of igemm_slab_floats(M, N) floats for the per-tile partials.
+// `a.stats` (if set) receives the finalized per-column statistics [mean(N), var(N)]
+// (biased variance, from sums shifted by a.stats_shift); `slab` is a workspace of
+// igemm_slab_floats(M, N) floats for the per-tile partials (+ 2N reduce scratch).
 void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
   const int BN = choose_bn(a.N);
   const int BM = (BN == 64) ? 256 : 128;
@@ -736,10 +745,15 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
     const int gy = std::min(64, (a.M + 3) / 4);
     dim3 grid((a.N + 63) / 64, gy);
     hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
-                       a.M, a.N, a.bias, a.relu, stats ? slab : (float*)nullptr);
+                       a.M, a.N, a.bias, a.relu, stats ? slab : (float*)nullptr,
+                       a.stats_shift);
     slab_rows = gy;
   }
-  if (stats) slab_reduce(slab, slab_rows, 2 * a.N, stats, true, s);
+  if (stats) {
+    float* sums = slab + (int64_t)std::max(tiles_m, 64) * 2 * a.N;
+    slab_reduce(slab, slab_rows, 2 * a.N, sums, true, s);
+    stats_finalize(sums, a.stats_shift, a.M, a.N, stats, s);
+  }
 }
 
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
@@ -764,7 +778,8 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
   if (splits > 1) {
     dim3 grid((a.N + 63) / 64, std::min(64, (a.M + 3) / 4));
     hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
-                       a.M, a.N, (const float*)nullptr, 0, (float*)nullptr);
+                       a.M, a.N, (const float*)nullptr, 0, (float*)nullptr,
+                       (const float*)nullptr);
   }
 }
 

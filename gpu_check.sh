@@ -11,11 +11,16 @@ for step in "$@"; do
     gputests) run gputests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider; rc=$? ;;
     smoke) run smoke 300 python __graft_entry__.py smoke; rc=$? ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5; rc=$? ;;
+    losses) run losses_g 300 python bench.py --steps 30 --warmup 2 --print-losses && MPA_NO_STATS_SHIFT=1 run losses_ns 300 python bench.py --steps 30 --warmup 2 --print-losses && run losses_e 300 python bench.py --steps 30 --warmup 2 --print-losses --graph off; rc=$? ;;
+    benchab) run benchab_g 300 python bench.py --steps 10 --warmup 3 --graph on && run benchab_e 300 python bench.py --steps 10 --warmup 3 --graph off && MPA_NO_STATS_SHIFT=1 run benchab_ns 300 python bench.py --steps 10 --warmup 3 --graph on; rc=$? ;;
     bench128) run bench128 600 python bench.py --steps 20 --warmup 5 --batch 128; rc=$? ;;
     benchnog) run benchnog 600 python bench.py --steps 20 --warmup 5 --graph off; rc=$? ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r18 --output-format csv -- python bench.py --steps 5 --warmup 2 --graph off; rc=$? ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
     diag2) run diag2 600 python tools/diag_grads.py twice; rc=$? ;;
+    traj) run traj 600 python tools/diag_traj.py 64 25 && MPA_NO_STATS_SHIFT=1 timeout -k 10 600 python tools/diag_traj.py 64 25 > gpurun_out/traj_noshift.log 2>&1; rc=$? ;;
+    train) run train 600 python main.py --synthetic_images 2048 --image_size 224 --NUM_EPOCHS 2 --BATCH_SIZE 256 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/training.log; rc=$? ;;
+    evalp) run evalp 600 python evaluation_pipeline.py --synthetic_images 1024 --image_size 224 --eval_lanes 3 --eval_batch 128 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/evaluation.log; rc=$? ;;
     *) echo "unknown step $step"; rc=0 ;;
   esac
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $step rc=$rc"; exit $rc; fi

@@ -46,7 +46,7 @@ def save_checkpoint(state: Dict[str, Any], epoch: int, model_name: str, checkpoi
     accepted and, as in the reference, unused)."""
     os.makedirs(checkpoint_dir or ".", exist_ok=True)
     path = checkpoint_path(checkpoint_dir, model_name)
-    fd, tmp = tempfile.mkstemp(prefix=".ckpt_", dir=checkpoint_dir or ".")
+    fd, tmp = tempfile.mkstemp(prefix="tmp_ckpt_", suffix=".pt", dir=checkpoint_dir or ".")
     os.close(fd)
     try:
         torch.save(_to_cpu(state), tmp)

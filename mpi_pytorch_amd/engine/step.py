@@ -18,6 +18,7 @@ RCCL collectives of the multi-GPU path run eagerly and overlap with backward).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -66,6 +67,12 @@ class TrainStep:
         self._static_x = None
         self._static_y = None
         self._static_loss = None
+        # Measured on ROCm 7.2 / MI355X: back-to-back replays of the full-step graph with
+        # no host sync in between intermittently corrupt training state (NaN / 1e30
+        # losses, docs/NOTES.md "HIP graph replay"), while synced replays and eager
+        # execution are exact and equally fast for GPU-bound steps.  Graph mode therefore
+        # syncs after each replay unless MPA_GRAPH_UNSAFE=1.
+        self._sync_replay = os.environ.get("MPA_GRAPH_UNSAFE", "0") != "1"
 
     def _eager(self, x, y):
         self.arena.zero_grad()
@@ -81,6 +88,8 @@ class TrainStep:
             self._static_x.copy_(x)
             self._static_y.copy_(y)
             self._graph.replay()
+            if self._sync_replay:
+                torch.cuda.current_stream().synchronize()
             loss = self._static_loss
         else:
             loss = self._eager(x, y)

@@ -21,6 +21,7 @@ tensor does not require grad.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -30,6 +31,7 @@ from . import _ext
 from ..parallel.arena import weight_of, grad_sink, grad_done
 
 _EMPTY = {}
+_NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
 
 
 def K(t: torch.Tensor):
@@ -74,7 +76,9 @@ class _ConvBNAct(torch.autograd.Function):
         ph, pw = conv.padding
         C = w.shape[0]
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
-        z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats)
+        # BN statistics come out of the conv epilogue, shifted by the running mean
+        z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
+                       _empty(x) if _NO_SHIFT else bn.running_mean)
         y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
                                        bn.momentum_value(), bn.eps,
                                        _or_empty(residual, x), relu)
@@ -127,7 +131,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
     sh, sw = conv.stride
     ph, pw = conv.padding
     z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,
-                   _empty(x))
+                   _empty(x), _empty(x))
     return k.bn_fwd_eval(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
                          _or_empty(residual, x), relu)
 
@@ -139,7 +143,8 @@ class _ConvAct(torch.autograd.Function):
         k = K(x)
         sh, sw = conv.stride
         ph, pw = conv.padding
-        y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu, _empty(x))
+        y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu, _empty(x),
+                       _empty(x))
         ctx.conv = conv
         ctx.relu = relu
         ctx.params = (w, b)
@@ -175,7 +180,7 @@ def conv_act(x, conv, relu: bool = False):
     sh, sw = conv.stride
     ph, pw = conv.padding
     return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,
-                      _empty(x))
+                      _empty(x), _empty(x))
 
 
 # =========================================================================== standalone BN

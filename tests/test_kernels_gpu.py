@@ -38,6 +38,7 @@ CONV_CASES = [
     (2, 8, 8, 256, 512, 3, 3, 1, 1),       # deep K (split-K candidate)
     (1, 13, 13, 12, 20, 5, 5, 1, 2),       # C%8 != 0 (VW=4)
     (2, 20, 20, 16, 64, 11, 11, 4, 2),     # AlexNet-style 11x11 s4
+    (2, 7, 7, 512, 512, 3, 3, 1, 1),       # small M, deep K: split-K + stats + shift path
 ]
 
 
@@ -55,8 +56,9 @@ def test_conv_fwd(gpu, case):
     b = torch.randn(K, device=gpu)
     st_c = torch.zeros(2, K, device=gpu)
     st_r = torch.zeros(2, K, device=gpu)
-    y = C().conv_fwd(x, w, b, st, st, ph, pw, True, st_c)
-    yr = ref.conv_fwd(x, w, b, st, st, ph, pw, True, st_r)
+    shift = torch.randn(K, device=gpu) * 0.1
+    y = C().conv_fwd(x, w, b, st, st, ph, pw, True, st_c, shift)
+    yr = ref.conv_fwd(x, w, b, st, st, ph, pw, True, st_r, shift)
     torch.cuda.synchronize()
     assert y.shape == yr.shape
     assert rel(y, yr) < 2e-2
@@ -149,7 +151,8 @@ def test_bn_stats_from_conv(gpu):
     x = bf(4, 16, 16, 64, dev=gpu)
     w = bf(128, 3, 3, 64, dev=gpu, scale=0.05)
     st = torch.zeros(2, 128, device=gpu)
-    z = C().conv_fwd(x, w, torch.empty(0, device=gpu), 1, 1, 1, 1, False, st)
+    z = C().conv_fwd(x, w, torch.empty(0, device=gpu), 1, 1, 1, 1, False, st,
+                     torch.full((128,), 0.3, device=gpu))
     g, b = torch.ones(128, device=gpu), torch.zeros(128, device=gpu)
     e = torch.empty(0, device=gpu)
     y1 = C().bn_fwd_train(z, st, g, b, torch.zeros(128, device=gpu), torch.ones(128, device=gpu),

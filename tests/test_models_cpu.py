@@ -1,0 +1,140 @@
+"""Model zoo on the CPU path: torchvision parameter names/shapes/counts, head replacement,
+feature-extract freezing, and exact fp32 parity of forward+backward against an
+independent NCHW implementation built from plain torch.nn.functional calls."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mpi_pytorch_amd.models import initialize_model, ARCH
+from mpi_pytorch_amd.engine import build_model, loss_fn
+from mpi_pytorch_amd.parallel import World
+
+# torchvision totals at 1000 classes
+TV_PARAMS_1000 = {"resnet18": 11689512, "resnet34": 21797672, "alexnet": 61100840,
+                  "vgg": 132868840, "squeezenet": 1248424, "densenet": 7978856,
+                  "inception": 27161264, "vgg16": 138357544}
+# at 64,500 classes
+TV_PARAMS_64500 = {"resnet18": 44265012, "resnet34": 54373172, "alexnet": 321260340,
+                   "vgg": 393028340, "squeezenet": 33823924, "densenet": 73066356,
+                   "inception": 206104264, "vgg16": 398517044}
+N_PARAM_TENSORS = {"resnet18": 62, "resnet34": 110, "alexnet": 16, "vgg": 38, "squeezenet": 52,
+                   "densenet": 364, "inception": 292, "vgg16": 32}
+
+
+def _sd_params(model):
+    sd = model.state_dict()
+    names = {n for n, _ in model.named_parameters()}
+    return {k: v for k, v in sd.items() if k in names}
+
+
+@pytest.mark.parametrize("name", list(ARCH))
+def test_param_counts_match_torchvision(name):
+    m, _ = initialize_model(name, 1000, False)
+    ps = _sd_params(m)
+    assert sum(v.numel() for v in ps.values()) == TV_PARAMS_1000[name]
+    assert len(ps) == N_PARAM_TENSORS[name]
+
+
+@pytest.mark.parametrize("name", ["resnet18", "squeezenet", "densenet", "alexnet"])
+def test_head_replacement_64500(name):
+    m, isz = initialize_model(name, 64500, False)
+    assert sum(v.numel() for v in _sd_params(m).values()) == TV_PARAMS_64500[name]
+    assert isz == ARCH[name][2]
+
+
+def test_input_sizes():
+    assert initialize_model("resnet34", 10, False)[1] == 128
+    assert initialize_model("inception", 10, False)[1] == 299
+    with pytest.raises(ValueError):
+        initialize_model("lenet", 10, False)
+
+
+def test_state_dict_layout_resnet18():
+    m, _ = initialize_model("resnet18", 64500, False)
+    sd = m.state_dict()
+    assert len(sd) == 122
+    assert sd["conv1.weight"].shape == (64, 3, 7, 7)
+    assert sd["layer2.0.downsample.0.weight"].shape == (128, 64, 1, 1)
+    assert sd["fc.weight"].shape == (64500, 512)
+    assert sd["bn1.num_batches_tracked"].dtype == torch.long
+    # round trip
+    m2, _ = initialize_model("resnet18", 64500, False)
+    m2.load_state_dict(sd)
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+
+
+def test_vgg_flatten_layout_roundtrip():
+    m, _ = initialize_model("vgg", 10, False)
+    sd = m.state_dict()
+    assert sd["classifier.0.weight"].shape == (4096, 25088)
+    m2, _ = initialize_model("vgg", 10, False)
+    m2.load_state_dict(sd)
+    assert torch.equal(m2.state_dict()["classifier.0.weight"], sd["classifier.0.weight"])
+
+
+def test_feature_extract_freezes_all_but_head():
+    m, _ = initialize_model("resnet18", 100, True)
+    trainable = [n for n, p in m.named_parameters() if p.requires_grad]
+    assert trainable == ["fc.weight", "fc.bias"]
+
+
+# ------------------------------------------------------------- independent NCHW oracle
+def _ref_resnet18(sd, x_nchw):
+    def bn(x, p):
+        return F.batch_norm(x, None, None, sd[p + ".weight"], sd[p + ".bias"], True, 0.1, 1e-5)
+
+    x = F.relu(bn(F.conv2d(x_nchw, sd["conv1.weight"], stride=2, padding=3), "bn1"))
+    x = F.max_pool2d(x, 3, 2, 1)
+    for li, stride in zip(range(1, 5), (1, 2, 2, 2)):
+        for b in range(2):
+            pre = "layer%d.%d." % (li, b)
+            s = stride if b == 0 else 1
+            out = F.relu(bn(F.conv2d(x, sd[pre + "conv1.weight"], stride=s, padding=1), pre + "bn1"))
+            out = bn(F.conv2d(out, sd[pre + "conv2.weight"], padding=1), pre + "bn2")
+            if pre + "downsample.0.weight" in sd:
+                x = bn(F.conv2d(x, sd[pre + "downsample.0.weight"], stride=s), pre + "downsample.1")
+            x = F.relu(out + x)
+    x = F.adaptive_avg_pool2d(x, 1).flatten(1)
+    return F.linear(x, sd["fc.weight"], sd["fc.bias"])
+
+
+def test_resnet18_cpu_matches_functional_oracle():
+    torch.manual_seed(0)
+    m, _ = build_model("resnet18", 10, False, torch.device("cpu"), World())
+    sd = {k: v.clone().requires_grad_(v.dtype.is_floating_point and "running" not in k)
+          for k, v in m.state_dict().items()}
+    x = torch.randn(4, 64, 64, 3)
+    y = torch.randint(0, 10, (4,))
+    loss = loss_fn(m(x), y)
+    loss.backward()
+    lr = F.cross_entropy(_ref_resnet18(sd, x.permute(0, 3, 1, 2)), y)
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-4
+    ours = {n: p.grad for n, p in m.named_parameters()}
+    exp = m.conv1._exp  # internal KRSC -> OIHW
+    assert torch.allclose(exp(ours["conv1.weight"]), sd["conv1.weight"].grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(m.layer3[0].conv1._exp(ours["layer3.0.conv1.weight"]),
+                          sd["layer3.0.conv1.weight"].grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(ours["fc.weight"], sd["fc.weight"].grad, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(ours["layer2.0.bn1.weight"], sd["layer2.0.bn1.weight"].grad, atol=1e-4,
+                          rtol=1e-3)
+
+
+@pytest.mark.parametrize("name,hw", [("alexnet", 95), ("squeezenet", 64), ("vgg16", 32),
+                                     ("densenet", 32), ("inception", 299)])
+def test_models_train_step_cpu(name, hw):
+    torch.manual_seed(0)
+    m, _ = build_model(name, 20, False, torch.device("cpu"), World())
+    x = torch.randn(2, hw, hw, 3)
+    y = torch.randint(0, 20, (2,))
+    out = m(x)
+    if name == "inception":
+        assert isinstance(out, tuple) and out[1].shape == (2, 20)
+    loss = loss_fn(out, y)
+    loss.backward()
+    g = m._mpa_arena.grad
+    assert torch.isfinite(g).all() and float(g.abs().sum()) > 0
+    m.eval()
+    with torch.no_grad():
+        assert m(x).shape == (2, 20)
