@@ -51,6 +51,12 @@ inline const mpa::bf16_raw* bopt(const Tensor& t) {
 
 inline int vec_width(int64_t c) { return (c % 8 == 0) ? 8 : ((c % 4 == 0) ? 4 : 1); }
 
+float* alloc_ws(Tensor& holder, const Tensor& like, int64_t n) {
+  if (n <= 0) return nullptr;
+  holder = torch::empty({n}, like.options().dtype(torch::kFloat32));
+  return holder.data_ptr<float>();
+}
+
 Tensor empty_like_shape(const Tensor& ref, at::IntArrayRef shape, torch::Dtype dt) {
   return torch::empty(shape, ref.options().dtype(dt));
 }
@@ -91,11 +97,7 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
   if (a.stats_shift) TORCH_CHECK(shift.numel() == K, "conv_fwd: shift size");
   a.relu = relu ? 1 : 0;
   Tensor ws;
-  float* wsp = nullptr;
-  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
-    ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
-    wsp = ws.data_ptr<float>();
-  }
+  float* wsp = alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
   Tensor slab;
   if (a.stats)
     slab = torch::empty({mpa::igemm_slab_floats(a.M, a.N)}, x.options().dtype(torch::kFloat32));
@@ -141,11 +143,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
       a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw; a.Poh = a_; a.Pow = b_;
       a.bias = nullptr; a.stats = nullptr; a.relu = 0;
       Tensor ws;
-      float* wsp = nullptr;
-      if (sh == 1 && sw == 1 && mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
-        ws = torch::empty({(int64_t)a.M * a.N}, dy.options().dtype(torch::kFloat32));
-        wsp = ws.data_ptr<float>();
-      }
+      float* wsp = alloc_ws(ws, dy, (sh == 1 && sw == 1) ? mpa::igemm_ws_floats(a.M, a.N, a.Ktot) : 0);
       mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream());
     }
   return dx;
@@ -169,6 +167,8 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t 
   a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
   a.Mpix = N * P * Q;
   a.Ncols = R * S * C;
+  Tensor slab;
+  a.slab = alloc_ws(slab, dy, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   mpa::igemm_wgrad(a, vec_width(K), (C % 8 == 0) ? 8 : 1, cur_stream());
 }
 
@@ -354,11 +354,7 @@ Tensor linear_fwd(Tensor x, Tensor w, Tensor bias, bool relu) {
   a.dH = 1; a.dW = 1; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   a.bias = fopt(bias); a.stats = nullptr; a.relu = relu ? 1 : 0;
   Tensor ws;
-  float* wsp = nullptr;
-  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
-    ws = torch::empty({(int64_t)a.M * a.N}, x.options().dtype(torch::kFloat32));
-    wsp = ws.data_ptr<float>();
-  }
+  float* wsp = alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
   mpa::igemm_rows(a, vec_width(Cin), wsp, nullptr, cur_stream());
   return y;
 }
@@ -380,11 +376,7 @@ Tensor linear_dgrad(Tensor dy, Tensor w) {
   a.C = dx.data_ptr(); a.ldc = Cin;
   a.dH = 1; a.dW = 1; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   Tensor ws;
-  float* wsp = nullptr;
-  if (mpa::igemm_wants_split(a.M, a.N, a.Ktot)) {
-    ws = torch::empty({(int64_t)a.M * a.N}, dy.options().dtype(torch::kFloat32));
-    wsp = ws.data_ptr<float>();
-  }
+  float* wsp = alloc_ws(ws, dy, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
   mpa::igemm_rows_dgrad(a, std::min(vec_width(Cout), vec_width(Cin)), wsp, cur_stream());
   return dx;
 }
@@ -402,6 +394,8 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
   a.Kout = Cout; a.C = Cin; a.H = 1; a.W = 1; a.P = 1; a.Q = 1; a.R = 1; a.S = 1;
   a.sh = 1; a.sw = 1; a.ph = 0; a.pw = 0;
   a.Mpix = B; a.Ncols = Cin;
+  Tensor slab;
+  a.slab = alloc_ws(slab, dy, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   mpa::igemm_wgrad(a, vec_width(Cout), (Cin % 8 == 0) ? 8 : 1, cur_stream());
 }
 

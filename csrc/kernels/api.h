@@ -46,6 +46,7 @@ struct WGradArgs {
   const bf16_raw* dy;
   const bf16_raw* x;
   float* dw;
+  float* slab;  // split partials [splits][Kout][Ncols] (igemm_wgrad_ws_floats), or null
   int Kout, C, H, W, P, Q, R, S, sh, sw, ph, pw;
   int Mpix;
   int Ncols;
@@ -58,7 +59,8 @@ int64_t igemm_slab_floats(int M, int N);
 void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s);  // B K-contig
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-contiguous
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
-bool igemm_wants_split(int M, int N, int Ktot);  // true => pass an M*N fp32 workspace
+int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
+int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

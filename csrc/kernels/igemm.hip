@@ -27,6 +27,7 @@
 // flight while tile k's MFMAs run, one barrier per K-step.  Blocks are remapped so tiles
 // sharing an operand panel land on the same XCD (private L2).
 #include <algorithm>
+#include <cstdlib>
 #include "common.h"
 #include "api.h"
 
@@ -117,8 +118,8 @@ __device__ __forceinline__ int nvalid(int idx, int lim) {
 // ======================================================================================
 //  fwd / dgrad kernel
 // ======================================================================================
-template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
-__global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
+template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT, int OCC>
+__global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
   constexpr int NA = BM / 64;                 // A chunks / thread
   constexpr int A_BYTES = BM * 64;
   constexpr int B_BYTES = BN * 64;
@@ -322,7 +323,10 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
   // ---- epilogue: lane owns D[n = nb + r][m = lane&15], r = 0..3
   const int nl = (lane >> 4) * 4;
   if constexpr (SPLIT) {
-    float* out = (float*)p.C;
+    // split-K partial: plain 16-B stores into this split's slab [z][M][N] (summed by
+    // splitk_finalize) - no fp32 atomics (a lane's 4 channels are contiguous, but its
+    // rows are 64 different rows per instruction: the slowest atomic access shape)
+    float* out = (float*)p.C + (size_t)blockIdx.z * p.M * p.N;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wrow0 + i * 16 + (lane & 15);
@@ -330,9 +334,13 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wcol0 + j * 16 + nl;
+        if (n + 3 < p.N && (p.N & 3) == 0) {
+          *(f32x4*)(out + (size_t)m * p.N + n) = acc[i][j];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) atomicAdd(out + (size_t)m * p.ldc + n + r, acc[i][j][r]);
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) out[(size_t)m * p.N + n + r] = acc[i][j][r];
+        }
       }
     }
     return;
@@ -452,8 +460,8 @@ __global__ __launch_bounds__(256) void igemm_rows_kernel(IGemmArgs p) {
 // ======================================================================================
 //  wgrad kernel: dW[m = kout][n = (r,s,c)] += sum_pix dy[pix][m] * im2col(x)[pix][n]
 // ======================================================================================
-template <int BM, int BN, int WM, int WN, int VWA, int VWB>
-__global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
+template <int BM, int BN, int WM, int WN, int VWA, int VWB, int OCC>
+__global__ __launch_bounds__(256, OCC) void igemm_wgrad_kernel(WGradArgs p) {
   constexpr int A_BYTES = BK * BM * 2;
   constexpr int B_BYTES = BK * BN * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -606,8 +614,12 @@ __global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
     cur ^= 1;
   }
 
-  // lane owns D[m = mb + r][n = lane&15]
+  // lane owns D[m = mb + r][n = lane&15].  One split: exclusive read-modify-write into
+  // the gradient arena.  Several splits: plain stores of this split's partial into the
+  // slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
   const int ml = (lane >> 4) * 4;
+  const bool direct = gridDim.z == 1;
+  float* dst = direct ? p.dw : p.slab + (size_t)blockIdx.z * p.Kout * p.Ncols;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -617,28 +629,62 @@ __global__ __launch_bounds__(256) void igemm_wgrad_kernel(WGradArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wrow0 + i * 16 + ml + r;
-        if (m < p.Kout) atomicAdd(p.dw + (size_t)m * p.Ncols + n, acc[i][j][r]);
+        if (m < p.Kout) {
+          float* q = dst + (size_t)m * p.Ncols + n;
+          *q = direct ? *q + acc[i][j][r] : acc[i][j][r];
+        }
       }
     }
   }
 }
 
+// dw[i] += sum_z slab[z][i]  (float4-vectorised; n % 4 == 0 asserted by the launcher)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int S,
+                                                            int64_t n, float* __restrict__ dw) {
+  const int64_t n4 = n / 4;
+  const bool vec = (n & 3) == 0;  // rows of the slab stay 16-B aligned only then
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (vec) {
+      f32x4 acc = ((const f32x4*)dw)[i];
+      for (int z = 0; z < S; ++z) acc += ((const f32x4*)(slab + (size_t)z * n))[i];
+      ((f32x4*)dw)[i] = acc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float acc = dw[4 * i + e];
+        for (int z = 0; z < S; ++z) acc += slab[(size_t)z * n + 4 * i + e];
+        dw[4 * i + e] = acc;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    float acc = dw[i];
+    for (int z = 0; z < S; ++z) acc += slab[(size_t)z * n + i];
+    dw[i] = acc;
+  }
+}
+
 // ----------------------------------------------------------- split-K finalize (fp32->bf16)
-__global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
-                                       int M, int N, const float* __restrict__ bias, int relu,
+__global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
+                                       bf16_t* __restrict__ out, int M, int N,
+                                       const float* __restrict__ bias, int relu,
                                        float* __restrict__ slab,
                                        const float* __restrict__ shift) {
-  // one block per 64 columns x (rows strided by gridDim.y); statistics go to the
-  // per-block-row slab [gridDim.y][2N] (reduced by slab_reduce)
+  // sums the S split partials [S][M][N]; one block per 64 columns x (rows strided by
+  // gridDim.y); statistics go to the per-block-row slab [gridDim.y][2N]
   __shared__ float red[2][256];
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const size_t MN = (size_t)M * N;
   float s = 0.f, q = 0.f;
   const float b = (bias && n < N) ? bias[n] : 0.f;
   const float k = (shift && n < N) ? shift[n] : 0.f;
   if (n < N) {
     for (int m = r0; m < M; m += gridDim.y * 4) {
-      float v = ws[(size_t)m * N + n] + b;
+      float v = b;
+      for (int z = 0; z < S; ++z) v += ws[z * MN + (size_t)m * N + n];
       if (relu) v = fmaxf(v, 0.f);
       const bf16_t o = f2bf(v);
       out[(size_t)m * N + n] = o;
@@ -662,11 +708,31 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, bf16_t* __r
 // ======================================================================================
 //  host-side launch logic
 // ======================================================================================
+// Occupancy target (waves per SIMD) for the MFMA kernels: 3 fits every tile in <= 168
+// VGPRs with no spills (accumulators move from AGPRs to VGPRs); 4 (<= 128 VGPRs) spills a
+// few registers on the large tiles.  MPA_IGEMM_OCC selects it (tuning).
+static int occ_target() {
+  static int v = [] {
+    const char* e = getenv("MPA_IGEMM_OCC");
+    const int o = e ? atoi(e) : 3;
+    return (o == 2 || o == 4) ? o : 3;
+  }();
+  return v;
+}
+
 template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
 static void launch_rows(const IGemmArgs& a, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
-  hipLaunchKernelGGL((igemm_rows_kernel<BM, BN, WM, WN, VW, BKC, SPLIT>), grid, dim3(256), 0, s,
-                     a);
+  const int o = occ_target();
+  if (o == 4)
+    hipLaunchKernelGGL((igemm_rows_kernel<BM, BN, WM, WN, VW, BKC, SPLIT, 4>), grid, dim3(256), 0,
+                       s, a);
+  else if (o == 2)
+    hipLaunchKernelGGL((igemm_rows_kernel<BM, BN, WM, WN, VW, BKC, SPLIT, 2>), grid, dim3(256), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((igemm_rows_kernel<BM, BN, WM, WN, VW, BKC, SPLIT, 3>), grid, dim3(256), 0,
+                       s, a);
 }
 
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT>
@@ -688,25 +754,36 @@ static int choose_bn(int N) {
   return 128;
 }
 
-// rows engine: fills tiling fields, picks split-K, launches.  `ws` is an fp32 workspace
-// of M*N floats (zeroed here) used when split-K is chosen; when ws == nullptr split-K is
-// disabled (strided output mappings).
-// Split-K only while the fp32-atomic reduction bytes stay well below the MFMA work:
-// FLOP per atomic byte = Ktot / (2*splits) must exceed ~2.5 PF / 1.3 TB/s (atomic rate,
-// MI355X_MICROARCH.md "Global float atomics") => splits <= Ktot / 2048.
-static int choose_splits(int tiles, int ktiles, int Ktot) {
-  if (tiles >= 512 || ktiles < 16) return 1;
-  int s = (1024 + tiles - 1) / tiles;
+// Split-K for grids smaller than the chip (< 256 tiles): each split stores its partial
+// tile with plain 16-B stores into a [splits][M][N] fp32 slab and splitk_finalize sums
+// them (+bias, ReLU, bf16, BN statistics) - no atomics.  Slab traffic is
+// 2 * splits * M * N * 4 bytes, small next to the GEMM for these deep-K shapes.
+static int choose_splits(int tiles, int ktiles) {
+  if (tiles >= 256 || ktiles < 16) return 1;
+  int s = (512 + tiles - 1) / tiles;
   s = std::min(s, ktiles / 8);
-  s = std::min(s, std::max(1, Ktot / 2048));
+  s = std::min(s, 64);
   return std::max(s, 1);
 }
 
-bool igemm_wants_split(int M, int N, int Ktot) {
-  const int BN = choose_bn(N);
-  const int BM = (BN == 64) ? 256 : 128;
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  return choose_splits(tiles, (Ktot + BK - 1) / BK, Ktot) > 1;
+static void rows_plan(IGemmArgs& a, int& BM, int& BN, int& splits, bool allow_split) {
+  BN = choose_bn(a.N);
+  BM = (BN == 64) ? 256 : 128;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  a.tiles_total = tiles_m * a.tiles_n;
+  const int ktiles = (a.Ktot + BK - 1) / BK;
+  splits = allow_split ? choose_splits(a.tiles_total, ktiles) : 1;
+  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
+  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
+}
+
+int64_t igemm_ws_floats(int M, int N, int Ktot) {
+  IGemmArgs a{};
+  a.M = M; a.N = N; a.Ktot = Ktot;
+  int BM, BN, splits;
+  rows_plan(a, BM, BN, splits, true);
+  return splits > 1 ? (int64_t)splits * M * N : 0;
 }
 
 int64_t igemm_slab_floats(int M, int N) {
@@ -716,37 +793,33 @@ int64_t igemm_slab_floats(int M, int N) {
   return (int64_t)std::max(tiles_m, 64) * 2 * N + 2 * N;
 }
 
-// `a.stats` (if set) receives the finalized per-column statistics [mean(N), var(N)]
-// (biased variance, from sums shifted by a.stats_shift); `slab` is a workspace of
-// igemm_slab_floats(M, N) floats for the per-tile partials (+ 2N reduce scratch).
-void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
-  const int BN = choose_bn(a.N);
-  const int BM = (BN == 64) ? 256 : 128;
-  a.tiles_n = (a.N + BN - 1) / BN;
+static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
+  int BM, BN, splits;
+  rows_plan(a, BM, BN, splits, ws != nullptr);
   const int tiles_m = (a.M + BM - 1) / BM;
-  a.tiles_total = tiles_m * a.tiles_n;
-  const int ktiles = (a.Ktot + BK - 1) / BK;
-  int splits = ws != nullptr ? choose_splits(a.tiles_total, ktiles, a.Ktot) : 1;
-  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
-  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
   void* final_out = a.C;
   float* stats = a.stats;
   a.stats = stats ? slab : nullptr;
   if (splits > 1) {
-    (void)hipMemsetAsync(ws, 0, (size_t)a.M * a.N * sizeof(float), s);
     a.C = ws;
     a.ldc = a.N;
   }
-  if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
-  else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);
-  else dispatch_split<128, 32, 4, 1, true>(a, vw, splits, s);
+  if (bkc) {
+    if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
+    else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);
+    else dispatch_split<128, 32, 4, 1, true>(a, vw, splits, s);
+  } else {
+    if (BN == 128) dispatch_split<128, 128, 2, 2, false>(a, vw, splits, s);
+    else if (BN == 64) dispatch_split<256, 64, 4, 1, false>(a, vw, splits, s);
+    else dispatch_split<128, 32, 4, 1, false>(a, vw, splits, s);
+  }
   int slab_rows = tiles_m;
   if (splits > 1) {
     const int gy = std::min(64, (a.M + 3) / 4);
     dim3 grid((a.N + 63) / 64, gy);
-    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
-                       a.M, a.N, a.bias, a.relu, stats ? slab : (float*)nullptr,
-                       a.stats_shift);
+    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, splits,
+                       (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
+                       stats ? slab : (float*)nullptr, a.stats_shift);
     slab_rows = gy;
   }
   if (stats) {
@@ -756,37 +829,29 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
   }
 }
 
+// `a.stats` (if set) receives the finalized per-column statistics [mean(N), var(N)]
+// (biased variance, from sums shifted by a.stats_shift); `slab` is a workspace of
+// igemm_slab_floats(M, N) floats; `ws` holds igemm_ws_floats(M, N, Ktot) floats for the
+// split-K partials (nullptr disables split-K, e.g. for strided output mappings).
+void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
+  run_rows(a, true, vw, ws, slab, s);
+}
+
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
-  const int BN = choose_bn(a.N);
-  const int BM = (BN == 64) ? 256 : 128;
-  a.tiles_n = (a.N + BN - 1) / BN;
-  const int tiles_m = (a.M + BM - 1) / BM;
-  a.tiles_total = tiles_m * a.tiles_n;
-  const int ktiles = (a.Ktot + BK - 1) / BK;
-  int splits = ws != nullptr ? choose_splits(a.tiles_total, ktiles, a.Ktot) : 1;
-  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
-  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
-  void* final_out = a.C;
-  if (splits > 1) {
-    (void)hipMemsetAsync(ws, 0, (size_t)a.M * a.N * sizeof(float), s);
-    a.C = ws;
-    a.ldc = a.N;
-  }
-  if (BN == 128) dispatch_split<128, 128, 2, 2, false>(a, vw, splits, s);
-  else if (BN == 64) dispatch_split<256, 64, 4, 1, false>(a, vw, splits, s);
-  else dispatch_split<128, 32, 4, 1, false>(a, vw, splits, s);
-  if (splits > 1) {
-    dim3 grid((a.N + 63) / 64, std::min(64, (a.M + 3) / 4));
-    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, (bf16_t*)final_out,
-                       a.M, a.N, (const float*)nullptr, 0, (float*)nullptr,
-                       (const float*)nullptr);
-  }
+  a.stats = nullptr;
+  run_rows(a, false, vw, ws, nullptr, s);
 }
 
 template <int BM, int BN, int WM, int WN, int VWA, int VWB>
 static void launch_wgrad(const WGradArgs& a, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
-  hipLaunchKernelGGL((igemm_wgrad_kernel<BM, BN, WM, WN, VWA, VWB>), grid, dim3(256), 0, s, a);
+  const int o = occ_target();
+  if (o == 4)
+    hipLaunchKernelGGL((igemm_wgrad_kernel<BM, BN, WM, WN, VWA, VWB, 4>), grid, dim3(256), 0, s, a);
+  else if (o == 2)
+    hipLaunchKernelGGL((igemm_wgrad_kernel<BM, BN, WM, WN, VWA, VWB, 2>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_wgrad_kernel<BM, BN, WM, WN, VWA, VWB, 3>), grid, dim3(256), 0, s, a);
 }
 
 template <int BM, int BN>
@@ -802,22 +867,42 @@ static void wgrad_vw(const WGradArgs& a, int vwa, int vwb, int splits, hipStream
   }
 }
 
-void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
-  const int BM = (a.Kout <= 64) ? 64 : 128;
+// split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB
+static void wgrad_plan(WGradArgs& a, int& BM, int& splits) {
+  BM = (a.Kout <= 64) ? 64 : 128;
   const int BN = 128;
   a.tiles_n = (a.Ncols + BN - 1) / BN;
   const int tiles_m = (a.Kout + BM - 1) / BM;
   a.tiles_total = tiles_m * a.tiles_n;
   const int ktiles = (a.Mpix + BK - 1) / BK;
-  // enough blocks to fill 256 CUs several times over; >= 16 K-steps per block so the
-  // fp32 atomic epilogue stays well under the chip-wide atomic rate
-  int splits = std::max(1, (2048 + a.tiles_total - 1) / a.tiles_total);
+  splits = std::max(1, (512 + a.tiles_total - 1) / a.tiles_total);
   splits = std::min(splits, std::max(1, ktiles / 16));
-  splits = std::min(splits, std::max(1, a.Mpix / 2048));
+  const int64_t out = (int64_t)a.Kout * a.Ncols;
+  splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, (16ll << 20) / out));
   a.ktiles_per_split = (ktiles + splits - 1) / splits;
   splits = (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split;
+}
+
+int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
+  WGradArgs a{};
+  a.Kout = Kout; a.Ncols = Ncols; a.Mpix = Mpix;
+  int BM, splits;
+  wgrad_plan(a, BM, splits);
+  return splits > 1 ? (int64_t)splits * Kout * Ncols : 0;
+}
+
+void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
+  int BM, splits;
+  wgrad_plan(a, BM, splits);
   if (BM == 64) wgrad_vw<64, 128>(a, vwa, vwb, splits, s);
   else wgrad_vw<128, 128>(a, vwa, vwb, splits, s);
+  if (splits > 1) {
+    const int64_t n = (int64_t)a.Kout * a.Ncols;
+    const int64_t n4 = n / 4;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 4096));
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, splits, n,
+                       a.dw);
+  }
 }
 
 }  // namespace mpa

@@ -39,6 +39,7 @@ CONV_CASES = [
     (1, 13, 13, 12, 20, 5, 5, 1, 2),       # C%8 != 0 (VW=4)
     (2, 20, 20, 16, 64, 11, 11, 4, 2),     # AlexNet-style 11x11 s4
     (2, 7, 7, 512, 512, 3, 3, 1, 1),       # small M, deep K: split-K + stats + shift path
+    (8, 56, 56, 64, 64, 3, 3, 1, 1),       # large pixel count: wgrad split slab path
 ]
 
 
