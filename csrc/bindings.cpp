@@ -499,6 +499,8 @@ Tensor dropout_bwd(Tensor dy, Tensor mask, double p) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mpi_pytorch_amd native gfx950 kernels + runtime";
+  m.def("igemm_engine", &mpa::igemm_engine, "GEMM staging engine: 1 LDS-DMA, 0 register");
+  m.def("igemm_set_engine", &mpa::igemm_set_engine);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

@@ -61,6 +61,8 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-co
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
+int igemm_engine();              // 1: LDS-DMA staging (default), 0: register staging
+void igemm_set_engine(int dma);
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

@@ -28,92 +28,9 @@
 // sharing an operand panel land on the same XCD (private L2).
 #include <algorithm>
 #include <cstdlib>
-#include "common.h"
-#include "api.h"
+#include "igemm_common.h"
 
 namespace mpa {
-
-__device__ __forceinline__ u32x4 u32x4_make(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  return u32x4{a, b, c, d};
-}
-
-constexpr int BK = 32;
-
-// ---------------------------------------------------------------------- LDS swizzles
-// K-contiguous image: [rows][32] bf16, 64-B rows, 4 x 16-B chunks per row.
-__device__ __forceinline__ int kc_off(int row, int chunk) {
-  return row * 64 + ((chunk ^ ((4 - ((row >> 2) & 3)) & 3)) << 4);
-}
-
-// N-contiguous image: [32 k-rows][COLS] bf16.  Chunk XOR keeps 8-B granules intact for
-// the transposed read and spreads the 8 rows read by one 32-lane half over all banks.
-template <int COLS>
-__device__ __forceinline__ int mn_swz(int k) {
-  if constexpr (COLS >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
-  else if constexpr (COLS == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
-  else return 2 * ((k >> 3) & 1);
-}
-template <int COLS>
-__device__ __forceinline__ int mn_off(int k, int col) {
-  const int chunk = col >> 3;
-  return k * (COLS * 2) + (((chunk ^ mn_swz<COLS>(k))) << 4) + ((col & 7) << 1);
-}
-
-// fragment (8 consecutive k of one row) from a K-contiguous image
-__device__ __forceinline__ bf16x8 frag_kc(const char* img, int row, int lane) {
-  const u32x4 v = *LDS_PTR(const u32x4, img + kc_off(row, lane >> 4));
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// fragment (8 consecutive k of one column) from an N-contiguous image, two tr reads
-template <int COLS>
-__device__ __forceinline__ bf16x8 frag_mn(const char* img, int col0, int lane) {
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  const int col = col0 + 4 * pp;
-  const int k0 = 8 * g + q;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0, col)));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0 + 4, col)));
-  s16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// ------------------------------------------------------------------- vector loaders
-// Load 8 consecutive bf16 (one 16-B chunk) with VW-wide accesses.  `nv` = number of
-// valid leading elements (0..8); VW=8 callers guarantee nv is 0 or 8 (alignment).
-template <int VW>
-__device__ __forceinline__ u32x4 ld_chunk(const bf16_t* p, int nv) {
-  u32x4 r = u32x4{0, 0, 0, 0};
-  if constexpr (VW == 8) {
-    if (nv >= 8) r = *(const u32x4*)p;
-  } else if constexpr (VW == 4) {
-    if (nv >= 4) {
-      const u32x2 a = *(const u32x2*)p;
-      r.x = a.x; r.y = a.y;
-    }
-    if (nv >= 8) {
-      const u32x2 b = *(const u32x2*)(p + 4);
-      r.z = b.x; r.w = b.y;
-    }
-  } else {
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (i < nv) w[i >> 1] |= (uint32_t)p[i] << (16 * (i & 1));
-    r = u32x4{w[0], w[1], w[2], w[3]};
-  }
-  return r;
-}
-
-__device__ __forceinline__ int nvalid(int idx, int lim) {
-  const int d = lim - idx;
-  return d <= 0 ? 0 : (d >= 8 ? 8 : d);
-}
 
 // ======================================================================================
 //  fwd / dgrad kernel
@@ -319,142 +236,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
       cur ^= 1;
     }
   }
-
-  // ---- epilogue: lane owns D[n = nb + r][m = lane&15], r = 0..3
-  const int nl = (lane >> 4) * 4;
-  if constexpr (SPLIT) {
-    // split-K partial: plain 16-B stores into this split's slab [z][M][N] (summed by
-    // splitk_finalize) - no fp32 atomics (a lane's 4 channels are contiguous, but its
-    // rows are 64 different rows per instruction: the slowest atomic access shape)
-    float* out = (float*)p.C + (size_t)blockIdx.z * p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wrow0 + i * 16 + (lane & 15);
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wcol0 + j * 16 + nl;
-        if (n + 3 < p.N && (p.N & 3) == 0) {
-          *(f32x4*)(out + (size_t)m * p.N + n) = acc[i][j];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) out[(size_t)m * p.N + n + r] = acc[i][j][r];
-        }
-      }
-    }
-    return;
-  } else {
-    bf16_t* out = (bf16_t*)p.C;
-    float s[TN][4], q[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
-    f32x4 bias[TN], shift[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      shift[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int n = n0 + wcol0 + j * 16 + nl;
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? p.bias[n + r] : 0.f;
-      }
-      if (p.stats_shift) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? p.stats_shift[n + r] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wrow0 + i * 16 + (lane & 15);
-      const bool mok = m < p.M;
-      size_t orow = 0;
-      if (mok) {
-        const int hw = p.oH * p.oW;
-        const int img = m / hw;
-        const int rr = m - img * hw;
-        const int oh = rr / p.oW;
-        const int ow = rr - oh * p.oW;
-        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + p.Poh) * p.dW +
-                (ow * p.Uow + p.Pow)) * p.ldc;
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wcol0 + j * 16 + nl;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = acc[i][j][r] + bias[j][r];
-          if (p.relu) t = fmaxf(t, 0.f);
-          v[r] = t;
-        }
-        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-        if (mok) {
-          if (n + 3 < p.N) {
-            *(uint2*)(out + orow + n) = make_uint2(lo, hi);
-          } else {
-            const uint16_t e[4] = {(uint16_t)(lo & 0xffff), (uint16_t)(lo >> 16),
-                                   (uint16_t)(hi & 0xffff), (uint16_t)(hi >> 16)};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) out[orow + n + r] = e[r];
-          }
-          // statistics on the bf16-rounded values BN will read, shifted by K ~ mean
-          // (BN running mean) so sum-of-squares does not cancel when |mean| >> std
-          const float rv[4] = {bf2f(lo & 0xffff) - shift[j][0], bf2f(lo >> 16) - shift[j][1],
-                               bf2f(hi & 0xffff) - shift[j][2], bf2f(hi >> 16) - shift[j][3]};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[j][r] += rv[r];
-            q[j][r] += rv[r] * rv[r];
-          }
-        }
-      }
-    }
-    if (p.stats) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float a = s[j][r], b = q[j][r];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            a += __shfl_xor(a, o, 64);
-            b += __shfl_xor(b, o, 64);
-          }
-          s[j][r] = a;
-          q[j][r] = b;
-        }
-      // cross-wave (WM waves share columns) reduction through the now idle LDS, then one
-      // plain store per column into this M-tile's row of the statistics slab - no
-      // contended same-address atomics; the slab is summed by slab_reduce afterwards.
-      float* red = (float*)smem;
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wcol0 + j * 16 + nl;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            red[(wm * BN + col + r) * 2] = s[j][r];
-            red[(wm * BN + col + r) * 2 + 1] = q[j][r];
-          }
-        }
-      }
-      __syncthreads();
-      if (tid < BN && n0 + tid < p.N) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) {
-          a += red[(w * BN + tid) * 2];
-          b += red[(w * BN + tid) * 2 + 1];
-        }
-        p.stats[(size_t)mt * 2 * p.N + n0 + tid] = a;
-        p.stats[(size_t)mt * 2 * p.N + p.N + n0 + tid] = b;
-      }
-    }
-  }
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid);
 }
 
 // ======================================================================================
@@ -613,29 +395,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_wgrad_kernel(WGradArgs p) {
     __syncthreads();
     cur ^= 1;
   }
+  wgrad_epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wrow0, wcol0, lane);
 
-  // lane owns D[m = mb + r][n = lane&15].  One split: exclusive read-modify-write into
-  // the gradient arena.  Several splits: plain stores of this split's partial into the
-  // slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
-  const int ml = (lane >> 4) * 4;
-  const bool direct = gridDim.z == 1;
-  float* dst = direct ? p.dw : p.slab + (size_t)blockIdx.z * p.Kout * p.Ncols;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wcol0 + j * 16 + (lane & 15);
-      if (n >= p.Ncols) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wrow0 + i * 16 + ml + r;
-        if (m < p.Kout) {
-          float* q = dst + (size_t)m * p.Ncols + n;
-          *q = direct ? *q + acc[i][j][r] : acc[i][j][r];
-        }
-      }
-    }
-  }
 }
 
 // dw[i] += sum_z slab[z][i]  (float4-vectorised; n % 4 == 0 asserted by the launcher)
@@ -716,6 +477,28 @@ static int occ_target() {
     const char* e = getenv("MPA_IGEMM_OCC");
     const int o = e ? atoi(e) : 3;
     return (o == 2 || o == 4) ? o : 3;
+  }();
+  return v;
+}
+
+// Staging engine for 16-B-granular operands: 1 = LDS-DMA (igemm_dma.hip, default),
+// 0 = register-staged (this file).  MPA_IGEMM_ENGINE=reg|dma sets the start value;
+// igemm_set_engine switches at run time (A/B benchmarks, cross-checking tests).
+static int g_engine = -1;
+int igemm_engine() {
+  if (g_engine < 0) {
+    const char* e = getenv("MPA_IGEMM_ENGINE");
+    g_engine = (e && (e[0] == 'r' || e[0] == '0')) ? 0 : 1;
+  }
+  return g_engine;
+}
+void igemm_set_engine(int dma) { g_engine = dma ? 1 : 0; }
+// The 4-wave wgrad tiles measure ~10 % slower on LDS-DMA than register-staged (the
+// register path keeps two pixel rows per chunk in flight); opt in with MPA_WGRAD_DMA=1.
+static bool wgrad_dma_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("MPA_WGRAD_DMA");
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -804,7 +587,9 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     a.C = ws;
     a.ldc = a.N;
   }
-  if (bkc) {
+  if (vw == 8 && igemm_engine() == 1 && igemm_rows_dma(a, BM, BN, bkc, splits, s)) {
+    // LDS-DMA engine (igemm_dma.hip)
+  } else if (bkc) {
     if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
     else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);
     else dispatch_split<128, 32, 4, 1, true>(a, vw, splits, s);
@@ -894,8 +679,14 @@ int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   int BM, splits;
   wgrad_plan(a, BM, splits);
-  if (BM == 64) wgrad_vw<64, 128>(a, vwa, vwb, splits, s);
-  else wgrad_vw<128, 128>(a, vwa, vwb, splits, s);
+  if (vwa == 8 && vwb == 8 && igemm_engine() == 1 && wgrad_dma_enabled() &&
+      igemm_wgrad_dma(a, BM, 128, splits, s)) {
+    // LDS-DMA engine (igemm_dma.hip)
+  } else if (BM == 64) {
+    wgrad_vw<64, 128>(a, vwa, vwb, splits, s);
+  } else {
+    wgrad_vw<128, 128>(a, vwa, vwb, splits, s);
+  }
   if (splits > 1) {
     const int64_t n = (int64_t)a.Kout * a.Ncols;
     const int64_t n4 = n / 4;

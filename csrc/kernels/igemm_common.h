@@ -1,0 +1,275 @@
+// Device-side building blocks shared by the implicit-GEMM kernels (igemm.hip: register-
+// staged engine; igemm_dma.hip: LDS-DMA engine): LDS image swizzles, MFMA fragment reads,
+// vector loaders and the two epilogues.  Layout derivations: docs/KERNELS.md.
+#pragma once
+#include "common.h"
+#include "api.h"
+
+namespace mpa {
+
+__device__ __forceinline__ u32x4 u32x4_make(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return u32x4{a, b, c, d};
+}
+
+constexpr int BK = 32;
+
+// ---------------------------------------------------------------------- LDS swizzles
+// K-contiguous image: [rows][32] bf16, 64-B rows, 4 x 16-B chunks per row.
+__device__ __forceinline__ int kc_off(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((4 - ((row >> 2) & 3)) & 3)) << 4);
+}
+
+// N-contiguous image: [32 k-rows][COLS] bf16.  Chunk XOR keeps 8-B granules intact for
+// the transposed read and spreads the 8 rows read by one 32-lane half over all banks.
+template <int COLS>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (COLS >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else if constexpr (COLS == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  else return 2 * ((k >> 3) & 1);
+}
+template <int COLS>
+__device__ __forceinline__ int mn_off(int k, int col) {
+  const int chunk = col >> 3;
+  return k * (COLS * 2) + (((chunk ^ mn_swz<COLS>(k))) << 4) + ((col & 7) << 1);
+}
+
+// fragment (8 consecutive k of one row) from a K-contiguous image
+__device__ __forceinline__ bf16x8 frag_kc(const char* img, int row, int lane) {
+  const u32x4 v = *LDS_PTR(const u32x4, img + kc_off(row, lane >> 4));
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// fragment (8 consecutive k of one column) from an N-contiguous image, two tr reads
+template <int COLS>
+__device__ __forceinline__ bf16x8 frag_mn(const char* img, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int col = col0 + 4 * pp;
+  const int k0 = 8 * g + q;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, img + mn_off<COLS>(k0 + 4, col)));
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------- vector loaders
+// Load 8 consecutive bf16 (one 16-B chunk) with VW-wide accesses.  `nv` = number of
+// valid leading elements (0..8); VW=8 callers guarantee nv is 0 or 8 (alignment).
+template <int VW>
+__device__ __forceinline__ u32x4 ld_chunk(const bf16_t* p, int nv) {
+  u32x4 r = u32x4{0, 0, 0, 0};
+  if constexpr (VW == 8) {
+    if (nv >= 8) r = *(const u32x4*)p;
+  } else if constexpr (VW == 4) {
+    if (nv >= 4) {
+      const u32x2 a = *(const u32x2*)p;
+      r.x = a.x; r.y = a.y;
+    }
+    if (nv >= 8) {
+      const u32x2 b = *(const u32x2*)(p + 4);
+      r.z = b.x; r.w = b.y;
+    }
+  } else {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < nv) w[i >> 1] |= (uint32_t)p[i] << (16 * (i & 1));
+    r = u32x4{w[0], w[1], w[2], w[3]};
+  }
+  return r;
+}
+
+__device__ __forceinline__ int nvalid(int idx, int lim) {
+  const int d = lim - idx;
+  return d <= 0 ? 0 : (d >= 8 ? 8 : d);
+}
+
+// -------------------------------------------------------------------------- epilogues
+// Rows engine (fwd / dgrad / linear).  The MFMA is issued channel-operand first, so lane
+// owns D[n = nb + r][m = lane&15], r = 0..3: four consecutive output channels of one row.
+//   SPLIT: plain 16-B fp32 stores of this split's partial into [z][M][N] (summed by
+//          splitk_finalize) - no atomics.
+//   else : +bias, ReLU, bf16 store (8 B per lane), and per-column shifted BN statistics of
+//          the bf16-rounded outputs, reduced in-wave, across the WM waves through LDS
+//          (`smem` must be free: the caller has passed a barrier after its last LDS read),
+//          and written as this M-tile's row of the statistics slab p.stats [tiles_m][2N].
+template <int BM, int BN, int WM, int WN, bool SPLIT>
+__device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
+                                              f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                              char* smem, int mt, int m0, int n0, int wm,
+                                              int wrow0, int wcol0, int tid) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  const int lane = tid & 63;
+  const int nl = (lane >> 4) * 4;
+  if constexpr (SPLIT) {
+    float* out = (float*)p.C + (size_t)blockIdx.z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wrow0 + i * 16 + (lane & 15);
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wcol0 + j * 16 + nl;
+        if (n + 3 < p.N && (p.N & 3) == 0) {
+          *(f32x4*)(out + (size_t)m * p.N + n) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) out[(size_t)m * p.N + n + r] = acc[i][j][r];
+        }
+      }
+    }
+  } else {
+    bf16_t* out = (bf16_t*)p.C;
+    float s[TN][4], q[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
+    f32x4 bias[TN], shift[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      shift[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int n = n0 + wcol0 + j * 16 + nl;
+      if (p.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? p.bias[n + r] : 0.f;
+      }
+      if (p.stats_shift) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? p.stats_shift[n + r] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wrow0 + i * 16 + (lane & 15);
+      const bool mok = m < p.M;
+      size_t orow = 0;
+      if (mok) {
+        const int hw = p.oH * p.oW;
+        const int img = m / hw;
+        const int rr = m - img * hw;
+        const int oh = rr / p.oW;
+        const int ow = rr - oh * p.oW;
+        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + p.Poh) * p.dW +
+                (ow * p.Uow + p.Pow)) * p.ldc;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wcol0 + j * 16 + nl;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[i][j][r] + bias[j][r];
+          if (p.relu) t = fmaxf(t, 0.f);
+          v[r] = t;
+        }
+        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+        if (mok) {
+          if (n + 3 < p.N) {
+            *(uint2*)(out + orow + n) = make_uint2(lo, hi);
+          } else {
+            const uint16_t e[4] = {(uint16_t)(lo & 0xffff), (uint16_t)(lo >> 16),
+                                   (uint16_t)(hi & 0xffff), (uint16_t)(hi >> 16)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) out[orow + n + r] = e[r];
+          }
+          // statistics on the bf16-rounded values BN will read, shifted by K ~ mean
+          // (BN running mean) so the sum of squares does not cancel when |mean| >> std
+          const float rv[4] = {bf2f(lo & 0xffff) - shift[j][0], bf2f(lo >> 16) - shift[j][1],
+                               bf2f(hi & 0xffff) - shift[j][2], bf2f(hi >> 16) - shift[j][3]};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[j][r] += rv[r];
+            q[j][r] += rv[r] * rv[r];
+          }
+        }
+      }
+    }
+    if (p.stats) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = s[j][r], b = q[j][r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+          }
+          s[j][r] = a;
+          q[j][r] = b;
+        }
+      float* red = (float*)smem;
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wcol0 + j * 16 + nl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            red[(wm * BN + col + r) * 2] = s[j][r];
+            red[(wm * BN + col + r) * 2 + 1] = q[j][r];
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < p.N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          a += red[(w * BN + tid) * 2];
+          b += red[(w * BN + tid) * 2 + 1];
+        }
+        p.stats[(size_t)mt * 2 * p.N + n0 + tid] = a;
+        p.stats[(size_t)mt * 2 * p.N + p.N + n0 + tid] = b;
+      }
+    }
+  }
+}
+
+// Wgrad engine: lane owns D[m = mb + r][n = lane&15].  One split: exclusive read-modify-
+// write into the fp32 gradient arena.  Several splits: plain stores of this split's partial
+// into the slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
+                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                               int m0, int n0, int wrow0, int wcol0,
+                                               int lane) {
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  const int ml = (lane >> 4) * 4;
+  const bool direct = gridDim.z == 1;
+  float* dst = direct ? p.dw : p.slab + (size_t)blockIdx.z * p.Kout * p.Ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wcol0 + j * 16 + (lane & 15);
+      if (n >= p.Ncols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wrow0 + i * 16 + ml + r;
+        if (m < p.Kout) {
+          float* q = dst + (size_t)m * p.Ncols + n;
+          *q = direct ? *q + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------- LDS-DMA engine (igemm_dma.hip)
+// Launch the LDS-DMA variant of a planned rows / wgrad GEMM (16-B operand granularity
+// required).  Return false when no instantiation covers the tile shape.
+bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hipStream_t s);
+bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s);
+
+}  // namespace mpa

@@ -1,0 +1,390 @@
+// LDS-DMA implicit-GEMM engine for gfx950 (MI355X / CDNA4).
+//
+// Same GEMM decomposition, tap tables, LDS images, fragment reads and epilogues as the
+// register-staged engine in igemm.hip (conv fwd / dgrad / linear "rows" kernel and the
+// wgrad kernel), but both operands are staged with
+// global_load_lds_dwordx4: each lane DMA's one 16-B chunk straight from HBM/L2 into LDS,
+// no VGPR round trip and no ds_write pass.  Why: per 32-deep K-step a 128x128 block reads
+// 32 KiB of fragments (~128 LDS clk at 256 B/clk) but the register path also writes 16 KiB
+// with ds_write_b128 (~79 B/clk/CU, ~207 clk) - against 256 clk of MFMA per SIMD the
+// register-staged kernel is LDS-write bound (MI355X_MICROARCH.md §LDS).
+//
+//  * An LDS-DMA instruction writes wave-uniform base + 16*lane, so the images stay in the
+//    engine's XOR-swizzled layouts by permuting the SOURCE: the lane that lands on chunk
+//    position p of a row fetches logical chunk p ^ swz(row) (the same involution the
+//    fragment reads apply).  Lanes whose element is padding / out of range fetch a 16-B
+//    zero page instead, so halo and tail handling cost nothing in the loop.
+//  * 3-stage ring, one raw s_barrier per K-step, counted `s_waitcnt vmcnt(N)`: tile kt+1's
+//    DMAs stay in flight across the barrier while tile kt is multiplied, and the DMA for
+//    tile kt+2 is issued right after the barrier into the stage tile kt-1 just vacated.
+//  * No ordinary VGPR-destination global load inside the loop (hipcc would drain the DMA
+//    queue with vmcnt(0) at its first use): the per-launch tap table is copied to LDS at
+//    kernel start and read with ds_read; every other loop operand is a kernel argument.
+//  * All LDS lives in one __shared__ array (a second LDS object makes hipcc insert a
+//    vmcnt(0) before the first ds_read of every K-step).
+// Requires 16-B granularity on both operands (the VW = 8 case of igemm.hip); the host
+// falls back to the register-staged engine otherwise.
+#include "igemm_common.h"
+
+namespace mpa {
+
+// 16-B zero page: the DMA source of every padded / out-of-range lane
+static __device__ __attribute__((aligned(16))) uint32_t g_zero16[4];
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16,
+                                   0, 0);
+}
+
+// wait until at most N of this wave's vector-memory ops are outstanding and all its LDS
+// reads have returned, then barrier; the memory clobber pins LDS reads/DMAs on their side
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// logical 16-B chunk fetched by `lane` for K-contiguous images (kc_off layout): the lane
+// lands on row 16j + lane/4, position lane&3; kc_off's XOR depends on (row>>2)&3 only
+__device__ __forceinline__ int kc_lane_chunk(int lane) {
+  const int sub = lane >> 2;
+  return (lane & 3) ^ ((4 - ((sub >> 2) & 3)) & 3);
+}
+
+// blocks per CU allowed by the 3-stage ring's LDS (160 KiB per CU), capped at 3 (<= 168
+// VGPRs per lane); used as the occupancy target of __launch_bounds__
+constexpr int dma_occ(int lds_bytes) {
+  return (160 * 1024) / lds_bytes >= 3 ? 3 : ((160 * 1024) / lds_bytes >= 2 ? 2 : 1);
+}
+
+// ======================================================================================
+//  rows kernel (fwd / dgrad / linear): C[m][n] = sum_k im2col(A)[m][k] * B(k, n)
+// ======================================================================================
+template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT>
+__global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void igemm_rows_dma_kernel(IGemmArgs p) {
+  constexpr int NS = 3;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
+  constexpr int IA = BM / 16, IB = BN / 16;  // 1-KiB DMA instructions per tile
+  constexpr int IAW = IA / 4;                // A instructions per wave (BM % 64 == 0)
+  constexpr int IBW = (IB + 3) / 4;          // B instructions per wave (max)
+  constexpr int WAITN = IAW + IB / 4;        // DMAs per wave per tile (min over waves)
+  constexpr int CPR = BN / 8, RPI = 64 / CPR;  // N-contig B image: chunks / row, rows / instr
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  static_assert(BM % 64 == 0 && WM * WN == 4, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + MAXT * 8];
+  int* tap_hw = (int*)(smem + NS * STAGE);  // (dh << 16) | (dw & 0xffff)
+  int* tap_b = tap_hw + MAXT;               // weight tap of the N-contig operand
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (p.Ktot + BK - 1) / BK;
+  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+
+  for (int t = tid; t < p.T; t += 256) {
+    tap_hw[t] = ((int)p.taps.dh[t] << 16) | ((int)p.taps.dw[t] & 0xffff);
+    tap_b[t] = p.taps.bt[t];
+  }
+  __syncthreads();
+  const int tlast = max(p.T - 1, 0);
+  const bf16_t* const zp = (const bf16_t*)g_zero16;
+
+  // ---- A: this lane's rows (one per DMA instruction) and its k-chunk state
+  const int kch = kc_lane_chunk(lane);
+  int a_img[IAW], a_bh[IAW], a_bw[IAW];
+#pragma unroll
+  for (int i = 0; i < IAW; ++i) {
+    const int m = m0 + 16 * (wave * IAW + i) + (lane >> 2);
+    if (m < p.M) {
+      const int hw = p.oH * p.oW;
+      const int img = m / hw;
+      const int r = m - img * hw;
+      const int oh = r / p.oW;
+      a_img[i] = img * p.aH * p.aW;
+      a_bh[i] = oh * p.Uh + p.Oh;
+      a_bw[i] = (r - oh * p.oW) * p.Uw + p.Ow;
+    } else {
+      a_img[i] = -1;
+      a_bh[i] = 0;
+      a_bw[i] = 0;
+    }
+  }
+  // tap / channel of k = kt*BK + 8*kch, advanced incrementally by BK per issued tile
+  int a_t, a_c;
+  {
+    const int kk = kbeg * BK + kch * 8;
+    a_t = kk / p.aC;
+    a_c = kk - a_t * p.aC;
+  }
+  // ---- B (N-contig, dgrad): per instruction k-row state
+  int b_t[IBW], b_k[IBW], b_col[IBW];
+  if constexpr (!BKC) {
+#pragma unroll
+    for (int i = 0; i < IBW; ++i) {
+      const int jb = wave + 4 * i;
+      const int krow = RPI * jb + lane / CPR;
+      b_col[i] = n0 + (((lane % CPR) ^ mn_swz<BN>(krow)) << 3);
+      const int kk = kbeg * BK + krow;
+      b_t[i] = kk / p.aC;
+      b_k[i] = kk - b_t[i] * p.aC;
+    }
+  }
+
+  auto issue = [&](int kt, int stage) {
+    char* st = smem + stage * STAGE;
+    const int kk = kt * BK + kch * 8;
+    const bool kok = kk < p.Ktot;
+    const int hwv = tap_hw[min(a_t, tlast)];
+    const int dh = hwv >> 16, dw = (short)(hwv & 0xffff);
+#pragma unroll
+    for (int i = 0; i < IAW; ++i) {
+      const int ih = a_bh[i] + dh, iw = a_bw[i] + dw;
+      const bool ok = kok & (a_img[i] >= 0) & ((unsigned)ih < (unsigned)p.aH) &
+                      ((unsigned)iw < (unsigned)p.aW);
+      const bf16_t* src = ok ? p.A + (size_t)(a_img[i] + ih * p.aW + iw) * p.aC + a_c
+                             : zp;
+      glds16(src, st + (wave * IAW + i) * 1024);
+    }
+    char* bimg = st + A_BYTES;
+    if constexpr (BKC) {
+#pragma unroll
+      for (int i = 0; i < IBW; ++i) {
+        const int jb = wave + 4 * i;
+        if (jb < IB) {
+          const int n = n0 + 16 * jb + (lane >> 2);
+          const bool ok = kok & (n < p.N);
+          const bf16_t* src = ok ? p.B + (size_t)n * p.ldb + kk : zp;
+          glds16(src, bimg + jb * 1024);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IBW; ++i) {
+        const int jb = wave + 4 * i;
+        if (jb < IB) {
+          const int kr = kt * BK + RPI * jb + lane / CPR;
+          const bool ok = (kr < p.Ktot) & (b_col[i] < p.N);
+          const bf16_t* src =
+              ok ? p.B + ((size_t)b_k[i] * p.RS + tap_b[min(b_t[i], tlast)]) * p.ldb + b_col[i]
+                 : zp;
+          glds16(src, bimg + jb * 1024);
+          b_k[i] += BK;
+          while (b_k[i] >= p.aC) { b_k[i] -= p.aC; ++b_t[i]; }
+        }
+      }
+    }
+    a_c += BK;
+    while (a_c >= p.aC) { a_c -= p.aC; ++a_t; }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wrow0 = wm * (BM / WM);
+  const int wcol0 = wn * (BN / WN);
+
+  if (kbeg < kend) {
+    issue(kbeg, 0);
+    if (kbeg + 1 < kend) issue(kbeg + 1, 1);
+    int s = 0;
+    for (int kt = kbeg; kt < kend; ++kt) {
+      if (kt + 1 < kend) wait_barrier<WAITN>();
+      else wait_barrier<0>();
+      if (kt + 2 < kend) issue(kt + 2, s == 0 ? 2 : s - 1);
+      const char* st = smem + s * STAGE;
+      const char* bimg = st + A_BYTES;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_kc(st, wrow0 + i * 16 + (lane & 15), lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (BKC) bfr[j] = frag_kc(bimg, wcol0 + j * 16 + (lane & 15), lane);
+        else bfr[j] = frag_mn<BN>(bimg, wcol0 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      s = (s == 2) ? 0 : s + 1;
+    }
+  }
+  __syncthreads();  // every DMA waited (vmcnt(0) on the last step); LDS free for the epilogue
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid);
+}
+
+// ======================================================================================
+//  wgrad kernel: dW[m = kout][n = (r,s,c)] += sum_pix dy[pix][m] * im2col(x)[pix][n]
+// ======================================================================================
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_dma_kernel(WGradArgs p) {
+  constexpr int NS = 3;
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int CPRA = BM / 8, RPIA = 64 / CPRA;
+  constexpr int CPRB = BN / 8, RPIB = 64 / CPRB;
+  constexpr int IA = BM / 16, IB = BN / 16;
+  constexpr int IAW = (IA + 3) / 4, IBW = (IB + 3) / 4;
+  constexpr int WAITN = IA / 4 + IB / 4;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  static_assert(WM * WN == 4, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (p.Mpix + BK - 1) / BK;
+  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+  if (kbeg >= kend) return;
+  const bf16_t* const zp = (const bf16_t*)g_zero16;
+
+  // ---- A (dy, [pix][Kout]): per instruction pixel row and output-channel chunk
+  int a_row[IAW], a_m[IAW];
+#pragma unroll
+  for (int i = 0; i < IAW; ++i) {
+    const int ja = wave + 4 * i;
+    a_row[i] = RPIA * ja + lane / CPRA;
+    a_m[i] = m0 + (((lane % CPRA) ^ mn_swz<BM>(a_row[i])) << 3);
+  }
+  // ---- B (im2col(x)): per instruction column decode n -> (dh, dw, c) and pixel iterator
+  const int PQ = p.P * p.Q;
+  int b_dh[IBW], b_dw[IBW], b_c[IBW], b_img[IBW], b_oh[IBW], b_ow[IBW];
+  bool b_ok[IBW];
+#pragma unroll
+  for (int i = 0; i < IBW; ++i) {
+    const int jb = wave + 4 * i;
+    const int krow = RPIB * jb + lane / CPRB;
+    const int n = n0 + (((lane % CPRB) ^ mn_swz<BN>(krow)) << 3);
+    const int tap = n / p.C;
+    const int r = tap / p.S;
+    b_dh[i] = r - p.ph;
+    b_dw[i] = tap - r * p.S - p.pw;
+    b_c[i] = n - tap * p.C;
+    b_ok[i] = n < p.Ncols;
+    const int pix = kbeg * BK + krow;
+    const int img = pix / PQ;
+    const int rr = pix - img * PQ;
+    b_img[i] = img;
+    b_oh[i] = rr / p.Q;
+    b_ow[i] = rr - b_oh[i] * p.Q;
+  }
+
+  auto issue = [&](int kt, int stage) {
+    char* st = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < IAW; ++i) {
+      const int ja = wave + 4 * i;
+      if (ja < IA) {
+        const int pix = kt * BK + a_row[i];
+        const bool ok = (pix < p.Mpix) & (a_m[i] < p.Kout);
+        const bf16_t* src = ok ? p.dy + (size_t)pix * p.Kout + a_m[i] : zp;
+        glds16(src, st + ja * 1024);
+      }
+    }
+    char* bimg = st + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < IBW; ++i) {
+      const int jb = wave + 4 * i;
+      if (jb < IB) {
+        const int pix = kt * BK + RPIB * jb + lane / CPRB;
+        const int ih = b_oh[i] * p.sh + b_dh[i], iw = b_ow[i] * p.sw + b_dw[i];
+        const bool ok = b_ok[i] & (pix < p.Mpix) & ((unsigned)ih < (unsigned)p.H) &
+                        ((unsigned)iw < (unsigned)p.W);
+        const bf16_t* src =
+            ok ? p.x + (((size_t)b_img[i] * p.H + ih) * p.W + iw) * p.C + b_c[i]
+               : zp;
+        glds16(src, bimg + jb * 1024);
+        int ow = b_ow[i] + BK, oh = b_oh[i], img = b_img[i];
+        while (ow >= p.Q) { ow -= p.Q; ++oh; }
+        while (oh >= p.P) { oh -= p.P; ++img; }
+        b_ow[i] = ow; b_oh[i] = oh; b_img[i] = img;
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wrow0 = wm * (BM / WM);
+  const int wcol0 = wn * (BN / WN);
+
+  issue(kbeg, 0);
+  if (kbeg + 1 < kend) issue(kbeg + 1, 1);
+  int s = 0;
+  for (int kt = kbeg; kt < kend; ++kt) {
+    if (kt + 1 < kend) wait_barrier<WAITN>();
+    else wait_barrier<0>();
+    if (kt + 2 < kend) issue(kt + 2, s == 0 ? 2 : s - 1);
+    const char* st = smem + s * STAGE;
+    const char* bimg = st + A_BYTES;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag_mn<BM>(st, wrow0 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag_mn<BN>(bimg, wcol0 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    s = (s == 2) ? 0 : s + 1;
+  }
+  wgrad_epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wrow0, wcol0, lane);
+}
+
+// ======================================================================================
+//  host launchers (plans are made by igemm.hip)
+// ======================================================================================
+template <int BM, int BN, int WM, int WN, bool BKC>
+static void launch_rows_dma(const IGemmArgs& a, int splits, hipStream_t s) {
+  dim3 grid(a.tiles_total, 1, splits);
+  if (splits > 1)
+    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, true>), grid, dim3(256), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, false>), grid, dim3(256), 0,
+                       s, a);
+}
+
+bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hipStream_t s) {
+  if (bkc) {
+    if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, true>(a, splits, s);
+    else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, true>(a, splits, s);
+    else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, true>(a, splits, s);
+    else return false;
+  } else {
+    if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, false>(a, splits, s);
+    else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, false>(a, splits, s);
+    else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, false>(a, splits, s);
+    else return false;
+  }
+  return true;
+}
+
+bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s) {
+  dim3 grid(a.tiles_total, 1, splits);
+  if (BM == 128 && BN == 128)
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  else if (BM == 64 && BN == 128)
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  else
+    return false;
+  return true;
+}
+
+}  // namespace mpa

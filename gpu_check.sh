@@ -16,6 +16,7 @@ for step in "$@"; do
     bench128) run bench128 600 python bench.py --steps 20 --warmup 5 --batch 128; rc=$? ;;
     benchnog) run benchnog 600 python bench.py --steps 20 --warmup 5 --graph off; rc=$? ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r18 --output-format csv -- python bench.py --steps 5 --warmup 2 --graph off; rc=$? ;;
+    benchk) run benchk 600 python tools/bench_kernels.py 256 10; rc=$? ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
     diag2) run diag2 600 python tools/diag_grads.py twice; rc=$? ;;
     traj) run traj 600 python tools/diag_traj.py 64 25 && MPA_NO_STATS_SHIFT=1 timeout -k 10 600 python tools/diag_traj.py 64 25 > gpurun_out/traj_noshift.log 2>&1; rc=$? ;;

@@ -40,6 +40,8 @@ CONV_CASES = [
     (2, 20, 20, 16, 64, 11, 11, 4, 2),     # AlexNet-style 11x11 s4
     (2, 7, 7, 512, 512, 3, 3, 1, 1),       # small M, deep K: split-K + stats + shift path
     (8, 56, 56, 64, 64, 3, 3, 1, 1),       # large pixel count: wgrad split slab path
+    (2, 32, 32, 8, 64, 7, 7, 2, 3),        # padded stem (C=8: 16-B granular, DMA path)
+    (4, 28, 28, 128, 128, 3, 3, 1, 1),     # 128x128 tile, several K-tiles
 ]
 
 
@@ -47,8 +49,17 @@ def _pair(v):
     return v if isinstance(v, tuple) else (v, v)
 
 
+@pytest.fixture(params=[1, 0], ids=["dma", "reg"])
+def engine(request, gpu):
+    """Run a GEMM test on the LDS-DMA engine and on the register-staged engine."""
+    prev = C().igemm_engine()
+    C().igemm_set_engine(request.param)
+    yield request.param
+    C().igemm_set_engine(prev)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd(gpu, case):
+def test_conv_fwd(gpu, engine, case):
     torch.manual_seed(0)
     N, H, W, Cc, K, R, S, st, pd = case
     ph, pw = _pair(pd)
@@ -67,7 +78,7 @@ def test_conv_fwd(gpu, case):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_dgrad(gpu, case):
+def test_conv_dgrad(gpu, engine, case):
     torch.manual_seed(1)
     N, H, W, Cc, K, R, S, st, pd = case
     ph, pw = _pair(pd)
@@ -82,7 +93,7 @@ def test_conv_dgrad(gpu, case):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wgrad(gpu, case):
+def test_conv_wgrad(gpu, engine, case):
     torch.manual_seed(2)
     N, H, W, Cc, K, R, S, st, pd = case
     ph, pw = _pair(pd)
@@ -98,9 +109,43 @@ def test_conv_wgrad(gpu, case):
     assert rel(dw, dwr) < 1e-2
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (1, 2, 4, 6, 7, 11, 12, 13, 14)])
+def test_engines_bitwise_equal(gpu, case):
+    """Both staging engines run the same MFMA sequence over the same LDS images, so every
+    output must match bit for bit; repeated launches screen the DMA ring for races."""
+    torch.manual_seed(5)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * Cc))
+    dy = bf(N, P, Q, K, dev=gpu)
+    e = torch.empty(0, device=gpu)
+    prev = C().igemm_engine()
+    outs = {}
+    try:
+        for eng in (0, 1):
+            C().igemm_set_engine(eng)
+            for rep in range(3 if eng else 1):
+                stt = torch.zeros(2, K, device=gpu)
+                y = C().conv_fwd(x, w, e, st, st, ph, pw, False, stt, e)
+                dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
+                dw = torch.zeros(K, R, S, Cc, device=gpu)
+                C().conv_wgrad(dy, x, dw, st, st, ph, pw)
+                outs[(eng, rep)] = (y, stt, dx, dw)
+    finally:
+        C().igemm_set_engine(prev)
+    torch.cuda.synchronize()
+    base = outs[(0, 0)]
+    for key, o in outs.items():
+        for a, b, nm in zip(o, base, ("y", "stats", "dx", "dw")):
+            assert torch.equal(a, b), (key, nm, rel(a, b))
+
+
 @pytest.mark.parametrize("B,Cin,Cout", [(8, 512, 1000), (128, 512, 64500), (16, 72, 36),
                                         (32, 4096, 4096)])
-def test_linear(gpu, B, Cin, Cout):
+def test_linear(gpu, engine, B, Cin, Cout):
     torch.manual_seed(3)
     x = bf(B, Cin, dev=gpu)
     w = bf(Cout, Cin, dev=gpu, scale=1.0 / math.sqrt(Cin))
