@@ -117,15 +117,21 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
   const c10::OptionalDeviceGuard g(device_of(dy));
   Tensor dx = empty_like_shape(dy, {N, (int64_t)H, (int64_t)W, C}, torch::kBFloat16);
   const int vw = std::min(vec_width(K), vec_width(C));
+  // sub-pixel decomposition: output phase (a_, b_) of dx is a stride-1 conv of dy with the
+  // taps (r, s) congruent to it; stride 1 has one phase
+  mpa::IGemmArgs a{};
+  a.A = bp(dy); a.aH = P; a.aW = Q; a.aC = K;
+  a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+  a.B = bp(w); a.N = C; a.RS = R * S; a.ldb = C;
+  a.C = dx.data_ptr(); a.ldc = C;
+  a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw;
+  a.bias = nullptr; a.stats = nullptr; a.relu = 0;
+  int T = 0, nph = 0;
   for (int a_ = 0; a_ < sh; ++a_)
     for (int b_ = 0; b_ < sw; ++b_) {
       const int Hp = (H - a_ + sh - 1) / sh, Wp = (W - b_ + sw - 1) / sw;
       if (Hp <= 0 || Wp <= 0) continue;
-      mpa::IGemmArgs a{};
-      a.A = bp(dy); a.aH = P; a.aW = Q; a.aC = K;
-      a.oH = Hp; a.oW = Wp; a.M = N * Hp * Wp;
-      a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
-      int T = 0;
+      const int t0 = T;
       for (int r = 0; r < R; ++r) {
         if (((a_ + ph - r) % sh) != 0) continue;
         for (int s = 0; s < S; ++s) {
@@ -136,16 +142,26 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
           ++T;
         }
       }
-      a.T = T;
-      a.Ktot = T * K;
-      a.B = bp(w); a.N = C; a.RS = R * S; a.ldb = C;
-      a.C = dx.data_ptr(); a.ldc = C;
-      a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw; a.Poh = a_; a.Pow = b_;
-      a.bias = nullptr; a.stats = nullptr; a.relu = 0;
-      Tensor ws;
-      float* wsp = alloc_ws(ws, dy, (sh == 1 && sw == 1) ? mpa::igemm_ws_floats(a.M, a.N, a.Ktot) : 0);
-      mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream());
+      TORCH_CHECK(nph < mpa::MAXPH, "conv_dgrad: too many stride phases");
+      a.ph[nph++] = mpa::PhaseDesc{N * Hp * Wp, Hp, Wp, (T - t0) * K, t0, T - t0, a_, b_, 0};
     }
+  if (sh == 1 && sw == 1) {
+    const mpa::PhaseDesc& d = a.ph[0];
+    a.M = d.M; a.oH = d.oH; a.oW = d.oW; a.T = d.T; a.Ktot = d.Ktot; a.Poh = 0; a.Pow = 0;
+    Tensor ws;
+    float* wsp = alloc_ws(ws, dy, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
+    mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream());
+  } else {
+    // phases with no taps (stride > kernel) leave their dx pixels zero
+    bool empty = false;
+    for (int i = 0; i < nph; ++i) empty |= a.ph[i].T == 0;
+    if (empty) dx.zero_();
+    int k = 0;
+    for (int i = 0; i < nph; ++i)
+      if (a.ph[i].T > 0) a.ph[k++] = a.ph[i];
+    a.nphase = k;
+    mpa::igemm_rows_dgrad_phases(a, vw, cur_stream());
+  }
   return dx;
 }
 
@@ -501,6 +517,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mpi_pytorch_amd native gfx950 kernels + runtime";
   m.def("igemm_engine", &mpa::igemm_engine, "GEMM staging engine: 1 LDS-DMA, 0 register");
   m.def("igemm_set_engine", &mpa::igemm_set_engine);
+  m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

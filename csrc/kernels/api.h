@@ -16,6 +16,16 @@ struct Taps {
   short bt[MAXT];
 };
 
+// One stride phase of a merged dgrad launch: its output sub-grid (oH x oW pixels at
+// rows/cols Poh + Uoh*i, Pow + Uow*j of dx), its taps [tap0, tap0 + T) of the shared table,
+// and its tile count.  Tile g of the launch belongs to phase g % nphase (phases interleaved
+// so every XCD's contiguous share of the tile list holds an equal mix of long and short
+// phases), local tile g / nphase; phases are padded to the longest tile count.
+constexpr int MAXPH = 16;
+struct PhaseDesc {
+  int M, oH, oW, Ktot, tap0, T, Poh, Pow, tiles;
+};
+
 // implicit GEMM whose rows are pixels of a gathered NHWC tensor (conv fwd / dgrad / linear)
 struct IGemmArgs {
   const bf16_raw* A;
@@ -40,6 +50,8 @@ struct IGemmArgs {
   int tiles_n;
   int tiles_total;
   Taps taps;
+  int nphase;             // > 0: merged stride-phase dgrad launch (igemm_rows_dgrad_phases)
+  PhaseDesc ph[MAXPH];
 };
 
 struct WGradArgs {
@@ -58,11 +70,15 @@ struct WGradArgs {
 int64_t igemm_slab_floats(int M, int N);
 void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s);  // B K-contig
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-contiguous
+// all stride phases of a strided-conv dgrad (a.nphase, a.ph[], shared a.taps) in one launch
+// on the LDS-DMA engine when eligible, else one igemm_rows_dgrad per phase
+void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s);
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
-int igemm_engine();              // 1: LDS-DMA staging (default), 0: register staging
-void igemm_set_engine(int dma);
+int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LDS-DMA all
+void igemm_set_engine(int engine);
+void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

@@ -236,7 +236,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
       cur ^= 1;
     }
   }
-  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid);
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid,
+                                       RowsGeom{p.M, p.oH, p.oW, p.Poh, p.Pow});
 }
 
 // ======================================================================================
@@ -481,26 +482,28 @@ static int occ_target() {
   return v;
 }
 
-// Staging engine for 16-B-granular operands: 1 = LDS-DMA (igemm_dma.hip, default),
-// 0 = register-staged (this file).  MPA_IGEMM_ENGINE=reg|dma sets the start value;
+// Staging engine for 16-B-granular operands: 0 = register-staged (this file),
+// 1 = tuned default: LDS-DMA (igemm_dma.hip) for the rows GEMMs (fwd / dgrad / linear)
+//     and for the wgrad shapes its 8-wave tile wins (wgrad_big), register-staged wgrad
+//     elsewhere (the 4-wave wgrad tiles measure ~10 % faster register-staged),
+// 2 = LDS-DMA for every GEMM.  MPA_IGEMM_ENGINE=0|1|2 sets the start value;
 // igemm_set_engine switches at run time (A/B benchmarks, cross-checking tests).
 static int g_engine = -1;
 int igemm_engine() {
   if (g_engine < 0) {
     const char* e = getenv("MPA_IGEMM_ENGINE");
-    g_engine = (e && (e[0] == 'r' || e[0] == '0')) ? 0 : 1;
+    g_engine = e ? std::min(2, std::max(0, atoi(e))) : 1;
   }
   return g_engine;
 }
-void igemm_set_engine(int dma) { g_engine = dma ? 1 : 0; }
-// The 4-wave wgrad tiles measure ~10 % slower on LDS-DMA than register-staged (the
-// register path keeps two pixel rows per chunk in flight); opt in with MPA_WGRAD_DMA=1.
-static bool wgrad_dma_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("MPA_WGRAD_DMA");
-    return e && e[0] == '1';
-  }();
-  return v;
+void igemm_set_engine(int e) { g_engine = std::min(2, std::max(0, e)); }
+
+// Tile override for measurement (tools/bench_kernels.py): igemm_force_tile(BM, BN, splits);
+// zeros restore the heuristics.  Applies to both plans (rows and wgrad, BM x BN of the
+// respective GEMM) when the requested tile exists for the engine in use.
+static int g_force_bm = 0, g_force_bn = 0, g_force_splits = 0;
+void igemm_force_tile(int bm, int bn, int splits) {
+  g_force_bm = bm; g_force_bn = bn; g_force_splits = splits;
 }
 
 template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
@@ -549,36 +552,58 @@ static int choose_splits(int tiles, int ktiles) {
   return std::max(s, 1);
 }
 
-static void rows_plan(IGemmArgs& a, int& BM, int& BN, int& splits, bool allow_split) {
+static void finish_split_plan(int ktiles, int& splits, int& per_split) {
+  per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
+  splits = ktiles > 0 ? (ktiles + per_split - 1) / per_split : 1;
+}
+
+// dma: the LDS-DMA engine will run it (adds the 8-wave 256x128 / 256x256 tiles, reachable
+// through igemm_force_tile; tools/bench_kernels.py sweep measures them slower than 128x128
+// on every ResNet layer: they leave the grid under one block per CU or force split-K,
+// whose fp32 partial slab costs more than the tile saves).
+static void rows_plan(IGemmArgs& a, int& BM, int& BN, int& splits, bool allow_split, bool dma) {
   BN = choose_bn(a.N);
   BM = (BN == 64) ? 256 : 128;
+  const int ktiles = (a.Ktot + BK - 1) / BK;
+  if (g_force_bm && g_force_bn) {
+    const bool ok_reg = (g_force_bm == 128 && g_force_bn == 128) ||
+                        (g_force_bm == 256 && g_force_bn == 64) ||
+                        (g_force_bm == 128 && g_force_bn == 32);
+    const bool ok_dma = ok_reg || (g_force_bm == 256 && (g_force_bn == 256 || g_force_bn == 128));
+    if (dma ? ok_dma : ok_reg) { BM = g_force_bm; BN = g_force_bn; }
+  }
   a.tiles_n = (a.N + BN - 1) / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
   a.tiles_total = tiles_m * a.tiles_n;
-  const int ktiles = (a.Ktot + BK - 1) / BK;
   splits = allow_split ? choose_splits(a.tiles_total, ktiles) : 1;
-  a.ktiles_per_split = ktiles > 0 ? (ktiles + splits - 1) / splits : 1;
-  splits = ktiles > 0 ? (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split : 1;
+  if (allow_split && g_force_splits > 0) splits = std::min(g_force_splits, std::max(ktiles, 1));
+  finish_split_plan(ktiles, splits, a.ktiles_per_split);
 }
+
+static bool use_dma(int vw) { return vw == 8 && igemm_engine() >= 1; }
 
 int64_t igemm_ws_floats(int M, int N, int Ktot) {
-  IGemmArgs a{};
-  a.M = M; a.N = N; a.Ktot = Ktot;
-  int BM, BN, splits;
-  rows_plan(a, BM, BN, splits, true);
-  return splits > 1 ? (int64_t)splits * M * N : 0;
+  int64_t best = 0;
+  for (int dma = 0; dma < 2; ++dma) {  // sized for whichever engine ends up running it
+    IGemmArgs a{};
+    a.M = M; a.N = N; a.Ktot = Ktot;
+    int BM, BN, splits;
+    rows_plan(a, BM, BN, splits, true, dma == 1);
+    if (splits > 1) best = std::max(best, (int64_t)splits * M * N);
+  }
+  return best;
 }
 
-int64_t igemm_slab_floats(int M, int N) {
-  const int BN = choose_bn(N);
-  const int BM = (BN == 64) ? 256 : 128;
-  const int tiles_m = (M + BM - 1) / BM;
-  return (int64_t)std::max(tiles_m, 64) * 2 * N + 2 * N;
-}
+// statistics slab rows: one per 128-row M-tile (the smallest BM of any plan) or per
+// splitk_finalize block row (<= 64), then the [2][N] sums
+static int64_t slab_rows_max(int M) { return std::max((M + 127) / 128, 64); }
+
+int64_t igemm_slab_floats(int M, int N) { return slab_rows_max(M) * 2 * N + 2 * N; }
 
 static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
   int BM, BN, splits;
-  rows_plan(a, BM, BN, splits, ws != nullptr);
+  const bool dma = use_dma(vw);
+  rows_plan(a, BM, BN, splits, ws != nullptr, dma);
   const int tiles_m = (a.M + BM - 1) / BM;
   void* final_out = a.C;
   float* stats = a.stats;
@@ -587,7 +612,7 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     a.C = ws;
     a.ldc = a.N;
   }
-  if (vw == 8 && igemm_engine() == 1 && igemm_rows_dma(a, BM, BN, bkc, splits, s)) {
+  if (dma && igemm_rows_dma(a, BM, BN, bkc, splits, s)) {
     // LDS-DMA engine (igemm_dma.hip)
   } else if (bkc) {
     if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
@@ -608,7 +633,7 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     slab_rows = gy;
   }
   if (stats) {
-    float* sums = slab + (int64_t)std::max(tiles_m, 64) * 2 * a.N;
+    float* sums = slab + slab_rows_max(a.M) * 2 * a.N;
     slab_reduce(slab, slab_rows, 2 * a.N, sums, true, s);
     stats_finalize(sums, a.stats_shift, a.M, a.N, stats, s);
   }
@@ -624,7 +649,51 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
 
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
   a.stats = nullptr;
+  a.nphase = 0;
   run_rows(a, false, vw, ws, nullptr, s);
+}
+
+// All stride phases in ONE launch on the LDS-DMA engine: a stride-2 conv's dgrad is 4
+// GEMMs of a quarter of the pixels each; launched separately each fills a fraction of the
+// 256 CUs (ResNet-18 layer4 at batch 256: 196 tiles per phase), merged they fill it.
+void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s) {
+  a.stats = nullptr;
+  a.bias = nullptr;
+  if (a.nphase <= 0) return;
+  if (use_dma(vw) && a.nphase <= MAXPH) {
+    IGemmArgs probe = a;
+    probe.M = 0;
+    probe.Ktot = 0;
+    for (int i = 0; i < a.nphase; ++i) {
+      probe.M = std::max(probe.M, a.ph[i].M);
+      probe.Ktot = std::max(probe.Ktot, a.ph[i].Ktot);
+    }
+    int BM, BN, splits;
+    rows_plan(probe, BM, BN, splits, false, true);
+    a.tiles_n = (a.N + BN - 1) / BN;
+    int most = 0;
+    for (int i = 0; i < a.nphase; ++i) {
+      a.ph[i].tiles = ((a.ph[i].M + BM - 1) / BM) * a.tiles_n;
+      most = std::max(most, a.ph[i].tiles);
+    }
+    const int tot = most * a.nphase;
+    a.tiles_total = tot;
+    a.ktiles_per_split = 1 << 30;
+    if (tot > 0 && igemm_rows_dma(a, BM, BN, false, 1, s)) return;
+  }
+  for (int i = 0; i < a.nphase; ++i) {  // one launch per phase
+    const PhaseDesc& d = a.ph[i];
+    IGemmArgs b = a;
+    b.nphase = 0;
+    b.M = d.M; b.oH = d.oH; b.oW = d.oW; b.Ktot = d.Ktot; b.T = d.T;
+    b.Poh = d.Poh; b.Pow = d.Pow;
+    for (int t = 0; t < d.T; ++t) {
+      b.taps.dh[t] = a.taps.dh[d.tap0 + t];
+      b.taps.dw[t] = a.taps.dw[d.tap0 + t];
+      b.taps.bt[t] = a.taps.bt[d.tap0 + t];
+    }
+    run_rows(b, false, vw, nullptr, nullptr, s);
+  }
 }
 
 template <int BM, int BN, int WM, int WN, int VWA, int VWB>
@@ -653,34 +722,53 @@ static void wgrad_vw(const WGradArgs& a, int vwa, int vwb, int splits, hipStream
 }
 
 // split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB
-static void wgrad_plan(WGradArgs& a, int& BM, int& splits) {
+// split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB
+// big: the 8-wave 128x256 LDS-DMA tile (measured +20..40 % over the 4-wave tiles for
+// Kout >= 256 and for the stem's tiny-output / huge-pixel-count reduction)
+static bool wgrad_big(const WGradArgs& a, bool dma_ok) {
+  return dma_ok && (a.Kout >= 256 || ((int64_t)a.Kout * a.Ncols <= 32768 && a.Mpix >= (1 << 20)));
+}
+
+static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bool big) {
   BM = (a.Kout <= 64) ? 64 : 128;
-  const int BN = 128;
+  BN = 128;
+  if (big) BN = 256, BM = 128;
+  if (g_force_bm && g_force_bn) {
+    const bool ok_reg = (g_force_bm == 64 || g_force_bm == 128) && g_force_bn == 128;
+    const bool ok_dma = ok_reg || (g_force_bn == 256 && (g_force_bm == 128 || g_force_bm == 256));
+    if (dma ? ok_dma : ok_reg) { BM = g_force_bm; BN = g_force_bn; }
+  }
   a.tiles_n = (a.Ncols + BN - 1) / BN;
   const int tiles_m = (a.Kout + BM - 1) / BM;
   a.tiles_total = tiles_m * a.tiles_n;
   const int ktiles = (a.Mpix + BK - 1) / BK;
   splits = std::max(1, (512 + a.tiles_total - 1) / a.tiles_total);
   splits = std::min(splits, std::max(1, ktiles / 16));
+  if (g_force_splits > 0) splits = std::min(g_force_splits, std::max(ktiles, 1));
   const int64_t out = (int64_t)a.Kout * a.Ncols;
   splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, (16ll << 20) / out));
-  a.ktiles_per_split = (ktiles + splits - 1) / splits;
-  splits = (ktiles + a.ktiles_per_split - 1) / a.ktiles_per_split;
+  finish_split_plan(ktiles, splits, a.ktiles_per_split);
 }
 
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
-  WGradArgs a{};
-  a.Kout = Kout; a.Ncols = Ncols; a.Mpix = Mpix;
-  int BM, splits;
-  wgrad_plan(a, BM, splits);
-  return splits > 1 ? (int64_t)splits * Kout * Ncols : 0;
+  int64_t best = 0;
+  for (int dma = 0; dma < 3; ++dma) {  // register, DMA, DMA big tile
+    WGradArgs a{};
+    a.Kout = Kout; a.Ncols = Ncols; a.Mpix = Mpix;
+    int BM, BN, splits;
+    wgrad_plan(a, BM, BN, splits, dma >= 1, dma == 2);
+    if (splits > 1) best = std::max(best, (int64_t)splits * Kout * Ncols);
+  }
+  return best;
 }
 
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
-  int BM, splits;
-  wgrad_plan(a, BM, splits);
-  if (vwa == 8 && vwb == 8 && igemm_engine() == 1 && wgrad_dma_enabled() &&
-      igemm_wgrad_dma(a, BM, 128, splits, s)) {
+  int BM, BN, splits;
+  const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
+  const bool big = wgrad_big(a, dma_ok);
+  const bool dma = big || (dma_ok && igemm_engine() == 2);
+  wgrad_plan(a, BM, BN, splits, dma, big);
+  if (dma && igemm_wgrad_dma(a, BM, BN, splits, s)) {
     // LDS-DMA engine (igemm_dma.hip)
   } else if (BM == 64) {
     wgrad_vw<64, 128>(a, vwa, vwb, splits, s);

@@ -98,21 +98,26 @@ __device__ __forceinline__ int nvalid(int idx, int lim) {
 //          the bf16-rounded outputs, reduced in-wave, across the WM waves through LDS
 //          (`smem` must be free: the caller has passed a barrier after its last LDS read),
 //          and written as this M-tile's row of the statistics slab p.stats [tiles_m][2N].
+// output-row geometry of the rows engine (per stride phase in a merged dgrad launch)
+struct RowsGeom {
+  int M, oH, oW, Poh, Pow;
+};
+
 template <int BM, int BN, int WM, int WN, bool SPLIT>
 __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                               char* smem, int mt, int m0, int n0, int wm,
-                                              int wrow0, int wcol0, int tid) {
+                                              int wrow0, int wcol0, int tid, const RowsGeom& g) {
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
   const int lane = tid & 63;
   const int nl = (lane >> 4) * 4;
   if constexpr (SPLIT) {
-    float* out = (float*)p.C + (size_t)blockIdx.z * p.M * p.N;
+    float* out = (float*)p.C + (size_t)blockIdx.z * g.M * p.N;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wrow0 + i * 16 + (lane & 15);
-      if (m >= p.M) continue;
+      if (m >= g.M) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wcol0 + j * 16 + nl;
@@ -150,16 +155,16 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wrow0 + i * 16 + (lane & 15);
-      const bool mok = m < p.M;
+      const bool mok = m < g.M;
       size_t orow = 0;
       if (mok) {
-        const int hw = p.oH * p.oW;
+        const int hw = g.oH * g.oW;
         const int img = m / hw;
         const int rr = m - img * hw;
-        const int oh = rr / p.oW;
-        const int ow = rr - oh * p.oW;
-        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + p.Poh) * p.dW +
-                (ow * p.Uow + p.Pow)) * p.ldc;
+        const int oh = rr / g.oW;
+        const int ow = rr - oh * g.oW;
+        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + g.Poh) * p.dW +
+                (ow * p.Uow + g.Pow)) * p.ldc;
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {

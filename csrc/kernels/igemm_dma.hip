@@ -51,27 +51,30 @@ __device__ __forceinline__ int kc_lane_chunk(int lane) {
   return (lane & 3) ^ ((4 - ((sub >> 2) & 3)) & 3);
 }
 
-// blocks per CU allowed by the 3-stage ring's LDS (160 KiB per CU), capped at 3 (<= 168
-// VGPRs per lane); used as the occupancy target of __launch_bounds__
-constexpr int dma_occ(int lds_bytes) {
-  return (160 * 1024) / lds_bytes >= 3 ? 3 : ((160 * 1024) / lds_bytes >= 2 ? 2 : 1);
+// waves per SIMD allowed by the 3-stage ring's LDS (160 KiB per CU) for a block of `nw`
+// waves, capped at 3 (<= 168 VGPRs per lane): the occupancy target of __launch_bounds__
+constexpr int dma_occ(int lds_bytes, int nw) {
+  return ((160 * 1024) / lds_bytes) * nw / 4 >= 3 ? 3
+         : (((160 * 1024) / lds_bytes) * nw / 4 >= 2 ? 2 : 1);
 }
 
 // ======================================================================================
 //  rows kernel (fwd / dgrad / linear): C[m][n] = sum_k im2col(A)[m][k] * B(k, n)
 // ======================================================================================
-template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT>
-__global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void igemm_rows_dma_kernel(IGemmArgs p) {
+template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
+__global__ __launch_bounds__(WM * WN * 64, dma_occ(3 * (BM + BN) * 64 + MAXT * 8, WM * WN))
+void igemm_rows_dma_kernel(IGemmArgs p) {
+  constexpr int NW = WM * WN, NT = NW * 64;  // waves / threads per block
   constexpr int NS = 3;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
   constexpr int IA = BM / 16, IB = BN / 16;  // 1-KiB DMA instructions per tile
-  constexpr int IAW = IA / 4;                // A instructions per wave (BM % 64 == 0)
-  constexpr int IBW = (IB + 3) / 4;          // B instructions per wave (max)
-  constexpr int WAITN = IAW + IB / 4;        // DMAs per wave per tile (min over waves)
+  constexpr int IAW = IA / NW;               // A instructions per wave
+  constexpr int IBW = (IB + NW - 1) / NW;    // B instructions per wave (max)
+  constexpr int WAITN = IAW + IB / NW;       // DMAs per wave per tile (min over waves)
   constexpr int CPR = BN / 8, RPI = 64 / CPR;  // N-contig B image: chunks / row, rows / instr
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
-  static_assert(BM % 64 == 0 && WM * WN == 4, "tile");
+  static_assert(IA % NW == 0 && (NW == 4 || NW == 8), "tile");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + MAXT * 8];
   int* tap_hw = (int*)(smem + NS * STAGE);  // (dh << 16) | (dw & 0xffff)
   int* tap_b = tap_hw + MAXT;               // weight tap of the N-contig operand
@@ -81,19 +84,33 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  // merged stride-phase launch: the block's phase sets output geometry, K and taps
+  RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow};
+  int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
+  if constexpr (PH) {
+    const int ph = tile % p.nphase;
+    tile /= p.nphase;
+    const PhaseDesc& d = p.ph[ph];
+    if (tile >= d.tiles) return;  // padding tile of a shorter phase (whole block)
+    g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow};
+    Ktot = d.Ktot;
+    T = d.T;
+    tap0 = d.tap0;
+    kps = (Ktot + BK - 1) / BK;
+  }
   const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int ktiles = (p.Ktot + BK - 1) / BK;
-  const int kbeg = blockIdx.z * p.ktiles_per_split;
-  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+  const int ktiles = (Ktot + BK - 1) / BK;
+  const int kbeg = blockIdx.z * kps;
+  const int kend = min(ktiles, kbeg + kps);
 
-  for (int t = tid; t < p.T; t += 256) {
-    tap_hw[t] = ((int)p.taps.dh[t] << 16) | ((int)p.taps.dw[t] & 0xffff);
-    tap_b[t] = p.taps.bt[t];
+  for (int t = tid; t < T; t += NT) {
+    tap_hw[t] = ((int)p.taps.dh[tap0 + t] << 16) | ((int)p.taps.dw[tap0 + t] & 0xffff);
+    tap_b[t] = p.taps.bt[tap0 + t];
   }
   __syncthreads();
-  const int tlast = max(p.T - 1, 0);
+  const int tlast = max(T - 1, 0);
   const bf16_t* const zp = (const bf16_t*)g_zero16;
 
   // ---- A: this lane's rows (one per DMA instruction) and its k-chunk state
@@ -102,14 +119,14 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
 #pragma unroll
   for (int i = 0; i < IAW; ++i) {
     const int m = m0 + 16 * (wave * IAW + i) + (lane >> 2);
-    if (m < p.M) {
-      const int hw = p.oH * p.oW;
+    if (m < g.M) {
+      const int hw = g.oH * g.oW;
       const int img = m / hw;
       const int r = m - img * hw;
-      const int oh = r / p.oW;
+      const int oh = r / g.oW;
       a_img[i] = img * p.aH * p.aW;
       a_bh[i] = oh * p.Uh + p.Oh;
-      a_bw[i] = (r - oh * p.oW) * p.Uw + p.Ow;
+      a_bw[i] = (r - oh * g.oW) * p.Uw + p.Ow;
     } else {
       a_img[i] = -1;
       a_bh[i] = 0;
@@ -128,7 +145,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
   if constexpr (!BKC) {
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
-      const int jb = wave + 4 * i;
+      const int jb = wave + NW * i;
       const int krow = RPI * jb + lane / CPR;
       b_col[i] = n0 + (((lane % CPR) ^ mn_swz<BN>(krow)) << 3);
       const int kk = kbeg * BK + krow;
@@ -140,7 +157,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
   auto issue = [&](int kt, int stage) {
     char* st = smem + stage * STAGE;
     const int kk = kt * BK + kch * 8;
-    const bool kok = kk < p.Ktot;
+    const bool kok = kk < Ktot;
     const int hwv = tap_hw[min(a_t, tlast)];
     const int dh = hwv >> 16, dw = (short)(hwv & 0xffff);
 #pragma unroll
@@ -156,7 +173,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
     if constexpr (BKC) {
 #pragma unroll
       for (int i = 0; i < IBW; ++i) {
-        const int jb = wave + 4 * i;
+        const int jb = wave + NW * i;
         if (jb < IB) {
           const int n = n0 + 16 * jb + (lane >> 2);
           const bool ok = kok & (n < p.N);
@@ -167,10 +184,10 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
     } else {
 #pragma unroll
       for (int i = 0; i < IBW; ++i) {
-        const int jb = wave + 4 * i;
+        const int jb = wave + NW * i;
         if (jb < IB) {
           const int kr = kt * BK + RPI * jb + lane / CPR;
-          const bool ok = (kr < p.Ktot) & (b_col[i] < p.N);
+          const bool ok = (kr < Ktot) & (b_col[i] < p.N);
           const bf16_t* src =
               ok ? p.B + ((size_t)b_k[i] * p.RS + tap_b[min(b_t[i], tlast)]) * p.ldb + b_col[i]
                  : zp;
@@ -218,24 +235,26 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64 + MAXT * 8)) void i
     }
   }
   __syncthreads();  // every DMA waited (vmcnt(0) on the last step); LDS free for the epilogue
-  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid);
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid, g);
 }
 
 // ======================================================================================
 //  wgrad kernel: dW[m = kout][n = (r,s,c)] += sum_pix dy[pix][m] * im2col(x)[pix][n]
 // ======================================================================================
 template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_dma_kernel(WGradArgs p) {
+__global__ __launch_bounds__(WM * WN * 64, dma_occ(3 * (BM + BN) * 64, WM * WN))
+void igemm_wgrad_dma_kernel(WGradArgs p) {
+  constexpr int NW = WM * WN;
   constexpr int NS = 3;
   constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int CPRA = BM / 8, RPIA = 64 / CPRA;
   constexpr int CPRB = BN / 8, RPIB = 64 / CPRB;
   constexpr int IA = BM / 16, IB = BN / 16;
-  constexpr int IAW = (IA + 3) / 4, IBW = (IB + 3) / 4;
-  constexpr int WAITN = IA / 4 + IB / 4;
+  constexpr int IAW = (IA + NW - 1) / NW, IBW = (IB + NW - 1) / NW;
+  constexpr int WAITN = IA / NW + IB / NW;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
-  static_assert(WM * WN == 4, "tile");
+  static_assert(NW == 4 || NW == 8, "tile");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
   const int tid = threadIdx.x;
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_
   int a_row[IAW], a_m[IAW];
 #pragma unroll
   for (int i = 0; i < IAW; ++i) {
-    const int ja = wave + 4 * i;
+    const int ja = wave + NW * i;
     a_row[i] = RPIA * ja + lane / CPRA;
     a_m[i] = m0 + (((lane % CPRA) ^ mn_swz<BM>(a_row[i])) << 3);
   }
@@ -266,7 +285,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_
   bool b_ok[IBW];
 #pragma unroll
   for (int i = 0; i < IBW; ++i) {
-    const int jb = wave + 4 * i;
+    const int jb = wave + NW * i;
     const int krow = RPIB * jb + lane / CPRB;
     const int n = n0 + (((lane % CPRB) ^ mn_swz<BN>(krow)) << 3);
     const int tap = n / p.C;
@@ -287,7 +306,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_
     char* st = smem + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < IAW; ++i) {
-      const int ja = wave + 4 * i;
+      const int ja = wave + NW * i;
       if (ja < IA) {
         const int pix = kt * BK + a_row[i];
         const bool ok = (pix < p.Mpix) & (a_m[i] < p.Kout);
@@ -298,7 +317,7 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_
     char* bimg = st + A_BYTES;
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
-      const int jb = wave + 4 * i;
+      const int jb = wave + NW * i;
       if (jb < IB) {
         const int pix = kt * BK + RPIB * jb + lane / CPRB;
         const int ih = b_oh[i] * p.sh + b_dh[i], iw = b_ow[i] * p.sw + b_dw[i];
@@ -353,32 +372,43 @@ __global__ __launch_bounds__(256, dma_occ(3 * (BM + BN) * 64)) void igemm_wgrad_
 template <int BM, int BN, int WM, int WN, bool BKC>
 static void launch_rows_dma(const IGemmArgs& a, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
+  if constexpr (!BKC) {
+    if (a.nphase > 0) {  // merged stride phases (dgrad): never split
+      hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, false, true>), grid,
+                         dim3(WM * WN * 64), 0, s, a);
+      return;
+    }
+  }
   if (splits > 1)
-    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, true>), grid, dim3(256), 0,
-                       s, a);
+    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, true, false>), grid,
+                       dim3(WM * WN * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, false>), grid, dim3(256), 0,
-                       s, a);
+    hipLaunchKernelGGL((igemm_rows_dma_kernel<BM, BN, WM, WN, BKC, false, false>), grid,
+                       dim3(WM * WN * 64), 0, s, a);
+}
+
+template <bool BKC>
+static bool rows_dma_tile(const IGemmArgs& a, int BM, int BN, int splits, hipStream_t s) {
+  if (BM == 256 && BN == 256) launch_rows_dma<256, 256, 2, 4, BKC>(a, splits, s);
+  else if (BM == 256 && BN == 128) launch_rows_dma<256, 128, 4, 2, BKC>(a, splits, s);
+  else if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, BKC>(a, splits, s);
+  else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, BKC>(a, splits, s);
+  else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, BKC>(a, splits, s);
+  else return false;
+  return true;
 }
 
 bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hipStream_t s) {
-  if (bkc) {
-    if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, true>(a, splits, s);
-    else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, true>(a, splits, s);
-    else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, true>(a, splits, s);
-    else return false;
-  } else {
-    if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, false>(a, splits, s);
-    else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, false>(a, splits, s);
-    else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, false>(a, splits, s);
-    else return false;
-  }
-  return true;
+  return bkc ? rows_dma_tile<true>(a, BM, BN, splits, s) : rows_dma_tile<false>(a, BM, BN, splits, s);
 }
 
 bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
-  if (BM == 128 && BN == 128)
+  if (BM == 256 && BN == 256)
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
+  else if (BM == 128 && BN == 256)
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<128, 256, 2, 4>), grid, dim3(512), 0, s, a);
+  else if (BM == 128 && BN == 128)
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
   else if (BM == 64 && BN == 128)
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<64, 128, 2, 2>), grid, dim3(256), 0, s, a);

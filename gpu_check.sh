@@ -17,6 +17,8 @@ for step in "$@"; do
     benchnog) run benchnog 600 python bench.py --steps 20 --warmup 5 --graph off; rc=$? ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r18 --output-format csv -- python bench.py --steps 5 --warmup 2 --graph off; rc=$? ;;
     benchk) run benchk 600 python tools/bench_kernels.py 256 10; rc=$? ;;
+    benchk1) MPA_BENCH_ENGINES=1 run benchk1 600 python tools/bench_kernels.py 256 10; rc=$? ;;
+    sweep) run sweep 900 python tools/bench_kernels.py 256 5 sweep; rc=$? ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
     diag2) run diag2 600 python tools/diag_grads.py twice; rc=$? ;;
     traj) run traj 600 python tools/diag_traj.py 64 25 && MPA_NO_STATS_SHIFT=1 timeout -k 10 600 python tools/diag_traj.py 64 25 > gpurun_out/traj_noshift.log 2>&1; rc=$? ;;

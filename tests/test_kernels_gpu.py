@@ -49,7 +49,7 @@ def _pair(v):
     return v if isinstance(v, tuple) else (v, v)
 
 
-@pytest.fixture(params=[1, 0], ids=["dma", "reg"])
+@pytest.fixture(params=[2, 0], ids=["dma", "reg"])
 def engine(request, gpu):
     """Run a GEMM test on the LDS-DMA engine and on the register-staged engine."""
     prev = C().igemm_engine()
@@ -125,7 +125,7 @@ def test_engines_bitwise_equal(gpu, case):
     prev = C().igemm_engine()
     outs = {}
     try:
-        for eng in (0, 1):
+        for eng in (0, 2):
             C().igemm_set_engine(eng)
             for rep in range(3 if eng else 1):
                 stt = torch.zeros(2, K, device=gpu)
@@ -141,6 +141,58 @@ def test_engines_bitwise_equal(gpu, case):
     for key, o in outs.items():
         for a, b, nm in zip(o, base, ("y", "stats", "dx", "dw")):
             assert torch.equal(a, b), (key, nm, rel(a, b))
+
+
+TILES = [(256, 256), (256, 128), (128, 128), (256, 64), (128, 32), (128, 256), (64, 128)]
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 256, 256, 3, 3, 1, 1), (3, 15, 13, 136, 264, 3, 3, 2, 1),
+                                  (2, 20, 20, 64, 128, 1, 1, 1, 0)])
+def test_forced_tiles_bitwise(gpu, case):
+    """Every tile shape of both engines, with split-K pinned to 1, accumulates each output
+    over K in the same order: all must agree bit for bit with the register engine's
+    default tile, and that one with the fp32 oracle."""
+    torch.manual_seed(6)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * Cc))
+    dy = bf(N, P, Q, K, dev=gpu)
+    e = torch.empty(0, device=gpu)
+
+    def run():
+        stt = torch.zeros(2, K, device=gpu)
+        y = C().conv_fwd(x, w, e, st, st, ph, pw, False, stt, e)
+        dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
+        dw = torch.zeros(K, R, S, Cc, device=gpu)
+        C().conv_wgrad(dy, x, dw, st, st, ph, pw)
+        return y, stt, dx, dw
+
+    prev = C().igemm_engine()
+    try:
+        C().igemm_set_engine(0)
+        C().igemm_force_tile(0, 0, 1)
+        base = run()
+        for eng in (0, 2):
+            C().igemm_set_engine(eng)
+            for bm, bn in TILES:
+                C().igemm_force_tile(bm, bn, 1)
+                out = run()
+                for a, b, nm in zip(out, base, ("y", "stats", "dx", "dw")):
+                    if nm == "stats":  # per-tile partial sums: order depends on BM
+                        assert rel(a, b) < 1e-5, (eng, bm, bn, rel(a, b))
+                    else:
+                        assert torch.equal(a, b), (eng, bm, bn, nm, rel(a, b))
+    finally:
+        C().igemm_force_tile(0, 0, 0)
+        C().igemm_set_engine(prev)
+    dwr = torch.zeros(K, R, S, Cc, device=gpu)
+    ref.conv_wgrad(dy, x, dwr, st, st, ph, pw)
+    assert rel(base[0], ref.conv_fwd(x, w, e, st, st, ph, pw, False, None, None)) < 2e-2
+    assert rel(base[2], ref.conv_dgrad(dy, w, H, W, st, st, ph, pw)) < 2e-2
+    assert rel(base[3], dwr) < 1e-2
 
 
 @pytest.mark.parametrize("B,Cin,Cout", [(8, 512, 1000), (128, 512, 64500), (16, 72, 36),

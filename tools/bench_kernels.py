@@ -1,8 +1,12 @@
 """Per-shape timing of the native conv kernels (fwd / dgrad / wgrad) on the ResNet-18 layer
-shapes at a given batch, reported as TFLOP/s.  Usage:
-    python tools/bench_kernels.py [batch] [iters]
-Runs each shape on both staging engines (register-staged, LDS-DMA) in one process.
-Set MPA_IGEMM_OCC=2|3|4 to compare occupancy targets of the register engine."""
+shapes at a given batch, reported as TFLOP/s.
+
+    python tools/bench_kernels.py [batch] [iters]          engines 0 (register) and 1/2 (DMA)
+    python tools/bench_kernels.py [batch] [iters] sweep    every tile on the DMA engine
+
+MPA_BENCH_ENGINES=0,1,2 selects engines; MPA_IGEMM_OCC=2|3|4 the register engine's
+occupancy target.  Sweep rows print each tile's time (us) with its split count forced to
+auto; the `auto` column is what the planner picks."""
 import os
 import sys
 
@@ -13,6 +17,7 @@ from mpi_pytorch_amd.ops import _ext
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 IT = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+SWEEP = len(sys.argv) > 3 and sys.argv[3] == "sweep"
 C = _ext.ext()
 dev = torch.device("cuda", 0)
 SHAPES = [  # name, H, Cin, Cout, R, stride, pad
@@ -26,6 +31,8 @@ SHAPES = [  # name, H, Cin, Cout, R, stride, pad
     ("l4.3x3s2", 14, 256, 512, 3, 2, 1),
     ("l4.3x3", 7, 512, 512, 3, 1, 1),
 ]
+ROWS_TILES = [(0, 0), (256, 256), (256, 128), (128, 128), (256, 64)]
+WGRAD_TILES = [(0, 0), (256, 256), (128, 256), (128, 128), (64, 128)]
 
 
 def timeit(fn):
@@ -41,28 +48,51 @@ def timeit(fn):
     return s.elapsed_time(e) / IT * 1e-3
 
 
-ENGINES = [int(e) for e in os.environ.get("MPA_BENCH_ENGINES", "0,1").split(",")]
+def tensors(H, Ci, Co, R, st, pd):
+    x = torch.randn(B, H, H, Ci, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, R, R, Ci, device=dev) * 0.05).to(torch.bfloat16)
+    P = (H + 2 * pd - R) // st + 1
+    dy = torch.randn(B, P, P, Co, device=dev).to(torch.bfloat16)
+    dw = torch.zeros(Co, R, R, Ci, device=dev)
+    e = torch.empty(0, device=dev)
+    stats = torch.empty(2, Co, device=dev)
+    flop = 2.0 * B * P * P * Co * R * R * Ci
+    fns = (lambda: C.conv_fwd(x, w, e, st, st, pd, pd, False, stats, e),
+           lambda: C.conv_dgrad(dy, w, H, H, st, st, pd, pd),
+           lambda: C.conv_wgrad(dy, x, dw, st, st, pd, pd))
+    return flop, fns
+
+
+if SWEEP:
+    C.igemm_set_engine(2)
+    print("tile sweep, DMA engine, batch %d (us; TF in brackets)" % B)
+    for name, H, Ci, Co, R, st, pd in SHAPES:
+        flop, (f, d, w) = tensors(H, Ci, Co, R, st, pd)
+        for label, fn, tiles in (("fwd", f, ROWS_TILES), ("dgrad", d, ROWS_TILES),
+                                 ("wgrad", w, WGRAD_TILES)):
+            cells = []
+            for bm, bn in tiles:
+                C.igemm_force_tile(bm, bn, 0)
+                t = timeit(fn)
+                cells.append("%s %6.1f(%4.0f)" % ("auto" if bm == 0 else "%dx%d" % (bm, bn),
+                                                 t * 1e6, flop / t / 1e12))
+            print("%-9s %-5s " % (name, label) + " | ".join(cells))
+        C.igemm_force_tile(0, 0, 0)
+    sys.exit(0)
+
+ENGINES = [int(e) for e in os.environ.get("MPA_BENCH_ENGINES", "0,1,2").split(",")]
 for eng in ENGINES:
     C.igemm_set_engine(eng)
-    print("== engine %s" % ("dma" if eng else "reg"))
+    print("== engine %d (%s)" % (eng, ["register", "dma rows", "dma all"][eng]))
     print("occ=%s batch=%d" % (os.environ.get("MPA_IGEMM_OCC", "3"), B))
-    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    tot = [0.0, 0.0, 0.0]
     for name, H, Ci, Co, R, st, pd in SHAPES:
-        x = torch.randn(B, H, H, Ci, device=dev).to(torch.bfloat16)
-        w = (torch.randn(Co, R, R, Ci, device=dev) * 0.05).to(torch.bfloat16)
-        P = (H + 2 * pd - R) // st + 1
-        dy = torch.randn(B, P, P, Co, device=dev).to(torch.bfloat16)
-        dw = torch.zeros(Co, R, R, Ci, device=dev)
-        e = torch.empty(0, device=dev)
-        stats = torch.empty(2, Co, device=dev)
-        flop = 2.0 * B * P * P * Co * R * R * Ci
-        tf = timeit(lambda: C.conv_fwd(x, w, e, st, st, pd, pd, False, stats, e))
-        td = timeit(lambda: C.conv_dgrad(dy, w, H, H, st, st, pd, pd))
-        tw = timeit(lambda: C.conv_wgrad(dy, x, dw, st, st, pd, pd))
-        tot["fwd"] += tf
-        tot["dgrad"] += td
-        tot["wgrad"] += tw
+        flop, fns = tensors(H, Ci, Co, R, st, pd)
+        ts = [timeit(fn) for fn in fns]
+        for i in range(3):
+            tot[i] += ts[i]
         print("%-10s fwd %7.1f us %6.0f TF | dgrad %7.1f us %6.0f TF | wgrad %7.1f us %6.0f TF" % (
-            name, tf * 1e6, flop / tf / 1e12, td * 1e6, flop / td / 1e12, tw * 1e6, flop / tw / 1e12))
+            name, ts[0] * 1e6, flop / ts[0] / 1e12, ts[1] * 1e6, flop / ts[1] / 1e12,
+            ts[2] * 1e6, flop / ts[2] / 1e12))
     print("sum (one instance each): fwd %.0f us  dgrad %.0f us  wgrad %.0f us" % (
-        tot["fwd"] * 1e6, tot["dgrad"] * 1e6, tot["wgrad"] * 1e6))
+        tot[0] * 1e6, tot[1] * 1e6, tot[2] * 1e6))
