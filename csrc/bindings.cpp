@@ -209,7 +209,8 @@ Tensor act_bwd(Tensor dy, Tensor y, Tensor dbias) {
 
 // -------------------------------------------------------------------------------- BN
 std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
-                                 Tensor rvar, double momentum, double eps, Tensor res, bool relu) {
+                                 Tensor rvar, double momentum, double eps, Tensor res, bool relu,
+                                 c10::optional<Tensor> counter) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
@@ -227,7 +228,10 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
   mpa::bn_fwd_train(bp(x), fopt(st), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
                     (float)momentum, (float)eps, bopt(res), relu ? 1 : 0, M, C, bpm(y),
-                    mean.data_ptr<float>(), rstd.data_ptr<float>(), cur_stream());
+                    mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                    (counter && counter->defined() && counter->numel() == 1)
+                        ? counter->data_ptr<int64_t>() : nullptr,
+                    cur_stream());
   return {y, mean, rstd};
 }
 
@@ -522,7 +526,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_bwd", &act_bwd);
-  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
+        py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
+        py::arg("res"), py::arg("relu"), py::arg("counter") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd);
   m.def("relu_fwd", &relu_fwd);

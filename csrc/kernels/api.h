@@ -45,6 +45,7 @@ struct IGemmArgs {
   const float* bias;
   float* stats;              // [2][N]: finalized (mean, biased var) of the bf16 output
   const float* stats_shift;  // per-column shift K for the sums (BN running mean) or null
+  float* stats_sums;         // [2][N] final sums: zeroed by the epilogue's mt == 0 blocks
   int relu;
   int ktiles_per_split;
   int tiles_n;
@@ -91,7 +92,8 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
               hipStream_t s);
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
-                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s);
+                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
+                  int64_t* counter, hipStream_t s);  // counter (num_batches_tracked) += 1
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s);

@@ -14,6 +14,7 @@
 #include "common.h"
 #include "api.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace mpa {
 
@@ -33,7 +34,38 @@ __device__ __forceinline__ ColMap colmap(int cpr) {
   return m;
 }
 
-static dim3 grid_for(int M, int C, int target = 2048) {
+// Tuning knobs (tools/bench_bn.py): MPA_BN_GRID = target block count, MPA_BN_UNR = rows in
+// flight per thread (1, 2 or 4).
+static int bn_grid_target() {  // 0: size-based default
+  static const int v = [] {
+    const char* e = getenv("MPA_BN_GRID");
+    return e ? std::max(64, atoi(e)) : 0;
+  }();
+  return v;
+}
+static int bn_unr() {
+  static const int v = [] {
+    const char* e = getenv("MPA_BN_UNR");
+    const int u = e ? atoi(e) : 1;
+    return (u == 2 || u == 4) ? u : 1;
+  }();
+  return v;
+}
+#define BN_LAUNCH(kern, grid, ...)                                                        \
+  do {                                                                                    \
+    const int u_ = bn_unr();                                                              \
+    if (u_ == 4) hipLaunchKernelGGL(kern<4>, grid, dim3(256), 0, __VA_ARGS__);            \
+    else if (u_ == 2) hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, __VA_ARGS__);       \
+    else hipLaunchKernelGGL(kern<1>, grid, dim3(256), 0, __VA_ARGS__);                    \
+  } while (0)
+
+// Default block count, measured on the ResNet-18 batch-256 shapes (tools/bench_bn.py,
+// profiles/bn_grid_sweep.txt): 512 blocks stream 5.5 TB/s on the 411 MB stem activations
+// (1024: 5.2, 2048: 4.7 - more blocks only add slab rows and tail waves); tensors under
+// 2M 16-B chunks (layer3/4) are tail-bound and fastest at 256.
+static dim3 grid_for(int M, int C, int target = 0) {
+  if (target <= 0) target = bn_grid_target();
+  if (target <= 0) target = ((int64_t)M * (C / 8) >= (2 << 20)) ? 512 : 256;
   const int cpr = C / 8;
   const int gy = (cpr + 255) / 256;
   const int cw = std::min(256, cpr);
@@ -41,6 +73,17 @@ static dim3 grid_for(int M, int C, int target = 2048) {
   int gx = (M + rpi - 1) / rpi;
   gx = std::max(1, std::min(gx, std::max(1, target / gy)));
   return dim3(gx, gy);
+}
+
+// Row sweep with UNR rows in flight per thread: every row's loads are issued before any
+// row is consumed, so a thread keeps UNR x (tensors) 16-B loads outstanding (one load per
+// thread leaves ~8 MB in flight chip-wide, half of HBM bandwidth x latency).
+template <int UNR, typename F>
+__device__ __forceinline__ void sweep_rows(const ColMap& cm, int M, F&& body) {
+  const int stride = gridDim.x * cm.rpi;
+  int r = blockIdx.x * cm.rpi + cm.r0;
+  for (; r + (UNR - 1) * stride < M; r += UNR * stride) body(r, stride, UNR);
+  for (; r < M; r += stride) body(r, stride, 1);
 }
 
 // block-reduce 8-channel partials held per thread; returns sums in threads with r0 == 0
@@ -59,29 +102,43 @@ __device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float*
 }
 
 // ---------------------------------------------------------------------- statistics
+template <int UNR>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, int M,
                                                         int C, const float* __restrict__ shift,
-                                                        float* __restrict__ slab) {
+                                                        float* __restrict__ slab,
+                                                        float* __restrict__ sums) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float s[8], q[8], k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; k[j] = 0.f; }
   if (cm.active) {
+    if (blockIdx.x == 0 && cm.r0 == 0) {  // slab_reduce accumulates into these afterwards
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sums[cm.cc * 8 + j] = 0.f; sums[C + cm.cc * 8 + j] = 0.f; }
+    }
     if (shift) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) k[j] = shift[cm.cc * 8 + j];
     }
-    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-      float f[8];
-      unpack8(*(const uint4*)(x + (size_t)r * C + cm.cc * 8), f);
+    sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+      uint4 v[UNR];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = f[j] - k[j];
-        s[j] += d;
-        q[j] += d * d;
+      for (int u = 0; u < UNR; ++u)
+        if (u < n) v[u] = *(const uint4*)(x + (size_t)(r + u * st) * C + cm.cc * 8);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (u >= n) break;
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = f[j] - k[j];
+          s[j] += d;
+          q[j] += d * d;
+        }
       }
-    }
+    });
   }
   block_reduce8(s, cm, red);
   block_reduce8(q, cm, red);
@@ -94,12 +151,54 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   }
 }
 
+// y = relu?(x * sc + sh (+ res)) over this thread's rows
+template <int UNR>
+__device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, int c0,
+                                              const float* sc, const float* sh,
+                                              const bf16_t* __restrict__ x,
+                                              const bf16_t* __restrict__ res, int relu,
+                                              bf16_t* __restrict__ y) {
+  sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+    uint4 xv[UNR], rv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (u < n) {
+        const size_t off = (size_t)(r + u * st) * C + c0;
+        xv[u] = *(const uint4*)(x + off);
+        if (res) rv[u] = *(const uint4*)(res + off);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (u >= n) break;
+      float f[8];
+      unpack8(xv[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+      if (res) {
+        float g[8];
+        unpack8(rv[u], g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += g[j];
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      }
+      *(uint4*)(y + (size_t)(r + u * st) * C + c0) = pack8(f);
+    }
+  });
+}
+
 // ------------------------------------------------------------------- forward (train)
+template <int UNR>
 __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
-    bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+    bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    unsigned long long* __restrict__ counter) {
+  if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -119,27 +218,11 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
       rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
     }
   }
-  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-    const size_t off = (size_t)r * C + c0;
-    float f[8];
-    unpack8(*(const uint4*)(x + off), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
-    if (res) {
-      float g[8];
-      unpack8(*(const uint4*)(res + off), g);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += g[j];
-    }
-    if (relu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    }
-    *(uint4*)(y + off) = pack8(f);
-  }
+  bn_apply_rows<UNR>(cm, M, C, c0, sc, sh, x, res, relu, y);
 }
 
 // -------------------------------------------------------------------- forward (eval)
+template <int UNR>
 __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
@@ -154,32 +237,16 @@ __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
     sc[j] = gamma[c0 + j] * rs;
     sh[j] = beta[c0 + j] - rmean[c0 + j] * sc[j];
   }
-  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-    const size_t off = (size_t)r * C + c0;
-    float f[8];
-    unpack8(*(const uint4*)(x + off), f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
-    if (res) {
-      float g[8];
-      unpack8(*(const uint4*)(res + off), g);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += g[j];
-    }
-    if (relu) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    }
-    *(uint4*)(y + off) = pack8(f);
-  }
+  bn_apply_rows<UNR>(cm, M, C, c0, sc, sh, x, res, relu, y);
 }
 
 // ---------------------------------------------------------------------- backward
 // pass 1: ws[0:C] += sum(g), ws[C:2C] += sum(g * xhat), g = dy * (y > 0 if relu)
+template <int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd, int M, int C,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, float* __restrict__ sums) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float sg[8], sgx[8];
@@ -187,26 +254,43 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
   if (cm.active) {
     const int c0 = cm.cc * 8;
+    if (blockIdx.x == 0 && cm.r0 == 0) {  // slab_reduce accumulates into these afterwards
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sums[c0 + j] = 0.f; sums[C + c0 + j] = 0.f; }
+    }
     float mu[8], rs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
-    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-      const size_t off = (size_t)r * C + c0;
-      float g[8], xv[8];
-      unpack8(*(const uint4*)(dy + off), g);
-      unpack8(*(const uint4*)(x + off), xv);
-      if (y) {
-        float yv[8];
-        unpack8(*(const uint4*)(y + off), yv);
+    sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+      uint4 dv[UNR], xr[UNR], yr[UNR];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      for (int u = 0; u < UNR; ++u) {
+        if (u < n) {
+          const size_t off = (size_t)(r + u * st) * C + c0;
+          dv[u] = *(const uint4*)(dy + off);
+          xr[u] = *(const uint4*)(x + off);
+          if (y) yr[u] = *(const uint4*)(y + off);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sg[j] += g[j];
-        sgx[j] += g[j] * (xv[j] - mu[j]) * rs[j];
+      for (int u = 0; u < UNR; ++u) {
+        if (u >= n) break;
+        float g[8], xv[8];
+        unpack8(dv[u], g);
+        unpack8(xr[u], xv);
+        if (y) {
+          float yv[8];
+          unpack8(yr[u], yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sg[j] += g[j];
+          sgx[j] += g[j] * (xv[j] - mu[j]) * rs[j];
+        }
       }
-    }
+    });
   }
   block_reduce8(sg, cm, red);
   block_reduce8(sgx, cm, red);
@@ -221,6 +305,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // pass 2: dx = a*g + b + c*x ; optionally write g (residual-branch gradient); block 0
 // folds the sums into dgamma/dbeta.
+template <int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -245,31 +330,45 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
   }
   if (!dx && !gout) return;
-  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-    const size_t off = (size_t)r * C + c0;
-    float g[8];
-    const uint4 graw = *(const uint4*)(dy + off);
-    unpack8(graw, g);
-    if (y) {
-      float yv[8];
-      unpack8(*(const uint4*)(y + off), yv);
+  sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+    uint4 dv[UNR], xr[UNR], yr[UNR];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-      if (gout) *(uint4*)(gout + off) = pack8(g);
-    } else if (gout) {
-      *(uint4*)(gout + off) = graw;
+    for (int u = 0; u < UNR; ++u) {
+      if (u < n) {
+        const size_t off = (size_t)(r + u * st) * C + c0;
+        dv[u] = *(const uint4*)(dy + off);
+        if (y) yr[u] = *(const uint4*)(y + off);
+        if (dx) xr[u] = *(const uint4*)(x + off);
+      }
     }
-    if (dx) {
-      float xv[8];
-      unpack8(*(const uint4*)(x + off), xv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
-      *(uint4*)(dx + off) = pack8(xv);
+    for (int u = 0; u < UNR; ++u) {
+      if (u >= n) break;
+      const size_t off = (size_t)(r + u * st) * C + c0;
+      float g[8];
+      unpack8(dv[u], g);
+      if (y) {
+        float yv[8];
+        unpack8(yr[u], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+        if (gout) *(uint4*)(gout + off) = pack8(g);
+      } else if (gout) {
+        *(uint4*)(gout + off) = dv[u];
+      }
+      if (dx) {
+        float xv[8];
+        unpack8(xr[u], xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
+        *(uint4*)(dx + off) = pack8(xv);
+      }
     }
-  }
+  });
 }
 
 // g = dy * (y > 0) ; dbias += colsum(g)
+template <int UNR>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__ dy,
                                                        const bf16_t* __restrict__ y,
                                                        float* __restrict__ slab, int M, int C,
@@ -281,20 +380,32 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
   if (cm.active) {
     const int c0 = cm.cc * 8;
-    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-      const size_t off = (size_t)r * C + c0;
-      float f[8];
-      unpack8(*(const uint4*)(dy + off), f);
-      if (y) {
-        float yv[8];
-        unpack8(*(const uint4*)(y + off), yv);
+    sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+      uint4 dv[UNR], yr[UNR];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = yv[j] > 0.f ? f[j] : 0.f;
-        *(uint4*)(g + off) = pack8(f);
+      for (int u = 0; u < UNR; ++u) {
+        if (u < n) {
+          const size_t off = (size_t)(r + u * st) * C + c0;
+          dv[u] = *(const uint4*)(dy + off);
+          if (y) yr[u] = *(const uint4*)(y + off);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += f[j];
-    }
+      for (int u = 0; u < UNR; ++u) {
+        if (u >= n) break;
+        float f[8];
+        unpack8(dv[u], f);
+        if (y) {
+          float yv[8];
+          unpack8(yr[u], yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = yv[j] > 0.f ? f[j] : 0.f;
+          *(uint4*)(g + (size_t)(r + u * st) * C + c0) = pack8(f);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    });
   }
   if (!slab) return;
   block_reduce8(s, cm, red);
@@ -356,6 +467,8 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// out must hold its starting value (the producer kernels zero it in their first block
+// when the reduction should start from 0; zero_out=true is only a fallback memset)
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s) {
   if (zero_out) (void)hipMemsetAsync(out, 0, sizeof(float) * W, s);
   const int gy = std::max(1, std::min(32, (S + 63) / 64));
@@ -388,23 +501,25 @@ void stats_finalize(const float* sums, const float* shift, int M, int C, float* 
 void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,
               hipStream_t s) {
   const dim3 g = grid_for(M, C);
-  hipLaunchKernelGGL(bn_stats_kernel, g, dim3(256), 0, s, x, M, C, shift, ws);
   float* sums = ws + (int64_t)g.x * 2 * C;
-  slab_reduce(ws, g.x, 2 * C, sums, true, s);
+  BN_LAUNCH(bn_stats_kernel, g, s, x, M, C, shift, ws, sums);
+  slab_reduce(ws, g.x, 2 * C, sums, false, s);
   stats_finalize(sums, shift, M, C, stats, s);
 }
 
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
-                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd, hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_train_kernel, grid_for(M, C), dim3(256), 0, s, x, stats, gamma,
-                     beta, rmean, rvar, momentum, eps, res, relu, M, C, y, mean, rstd);
+                  int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
+                  int64_t* counter, hipStream_t s) {
+  BN_LAUNCH(bn_fwd_train_kernel, grid_for(M, C), s, x, stats, gamma,
+                     beta, rmean, rvar, momentum, eps, res, relu, M, C, y, mean, rstd,
+                     (unsigned long long*)counter);
 }
 
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_eval_kernel, grid_for(M, C), dim3(256), 0, s, x, gamma, beta, rmean,
+  BN_LAUNCH(bn_fwd_eval_kernel, grid_for(M, C), s, x, gamma, beta, rmean,
                      rvar, eps, res, relu, M, C, y);
 }
 
@@ -414,9 +529,10 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
   // ws layout: [2C] final sums | [gx][2C] per-block partials
   const dim3 gr = grid_for(M, C);
   float* slab = ws + 2 * C;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, gr, dim3(256), 0, s, dy, x, y, mean, rstd, M, C, slab);
-  slab_reduce(slab, gr.x, 2 * C, ws, true, s);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid_for(M, C), dim3(256), 0, s, dy, x, y, mean, rstd,
+  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, M, C, slab,
+                     ws);
+  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd,
                      gamma, ws, dgamma, dbeta, M, C, dx, g);
 }
 
@@ -424,7 +540,7 @@ void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, 
              float* ws, hipStream_t s) {
   if (C % 8 == 0) {
     const dim3 gr = grid_for(M, C);
-    hipLaunchKernelGGL(act_bwd_kernel, gr, dim3(256), 0, s, dy, y, dbias ? ws : (float*)nullptr, M,
+    BN_LAUNCH(act_bwd_kernel, gr, s, dy, y, dbias ? ws : (float*)nullptr, M,
                        C, g);
     if (dbias) slab_reduce(ws, gr.x, C, dbias, false, s);
   } else

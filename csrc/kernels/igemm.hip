@@ -433,7 +433,8 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
                                        bf16_t* __restrict__ out, int M, int N,
                                        const float* __restrict__ bias, int relu,
                                        float* __restrict__ slab,
-                                       const float* __restrict__ shift) {
+                                       const float* __restrict__ shift,
+                                       float* __restrict__ sums) {
   // sums the S split partials [S][M][N]; one block per 64 columns x (rows strided by
   // gridDim.y); statistics go to the per-block-row slab [gridDim.y][2N]
   __shared__ float red[2][256];
@@ -456,6 +457,10 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
     }
   }
   if (slab) {
+    if (blockIdx.y == 0 && threadIdx.x < 64 && n < N) {  // start value of the slab reduction
+      sums[n] = 0.f;
+      sums[N + n] = 0.f;
+    }
     red[0][threadIdx.x] = s;
     red[1][threadIdx.x] = q;
     __syncthreads();
@@ -607,7 +612,9 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
   const int tiles_m = (a.M + BM - 1) / BM;
   void* final_out = a.C;
   float* stats = a.stats;
+  float* sums = stats ? slab + slab_rows_max(a.M) * 2 * a.N : nullptr;
   a.stats = stats ? slab : nullptr;
+  a.stats_sums = sums;
   if (splits > 1) {
     a.C = ws;
     a.ldc = a.N;
@@ -629,12 +636,11 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     dim3 grid((a.N + 63) / 64, gy);
     hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, splits,
                        (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
-                       stats ? slab : (float*)nullptr, a.stats_shift);
+                       stats ? slab : (float*)nullptr, a.stats_shift, sums);
     slab_rows = gy;
   }
   if (stats) {
-    float* sums = slab + slab_rows_max(a.M) * 2 * a.N;
-    slab_reduce(slab, slab_rows, 2 * a.N, sums, true, s);
+    slab_reduce(slab, slab_rows, 2 * a.N, sums, false, s);
     stats_finalize(sums, a.stats_shift, a.M, a.N, stats, s);
   }
 }

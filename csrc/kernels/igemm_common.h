@@ -226,6 +226,11 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
         }
       }
       __syncthreads();
+      if (mt == 0 && blockIdx.z == 0 && tid < BN && n0 + tid < p.N) {
+        // start value of the slab reduction that runs after this kernel (no memset)
+        p.stats_sums[n0 + tid] = 0.f;
+        p.stats_sums[p.N + n0 + tid] = 0.f;
+      }
       if (tid < BN && n0 + tid < p.N) {
         float a = 0.f, b = 0.f;
 #pragma unroll

@@ -20,6 +20,8 @@ for step in "$@"; do
     benchk1) MPA_BENCH_ENGINES=1 run benchk1 600 python tools/bench_kernels.py 256 10; rc=$? ;;
     sweep) run sweep 900 python tools/bench_kernels.py 256 5 sweep; rc=$? ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
+    benchbn) for g in 0 256 512 1024; do for u in 1; do MPA_BN_GRID=$g MPA_BN_UNR=$u timeout -k 10 120 python tools/bench_bn.py 20 >> gpurun_out/benchbn.log 2>&1 || exit 1; done; done; rc=0 ;;
+    diageng) run diageng 600 python tools/diag_engines.py inception 299 4; rc=$? ;;
     diag2) run diag2 600 python tools/diag_grads.py twice; rc=$? ;;
     traj) run traj 600 python tools/diag_traj.py 64 25 && MPA_NO_STATS_SHIFT=1 timeout -k 10 600 python tools/diag_traj.py 64 25 > gpurun_out/traj_noshift.log 2>&1; rc=$? ;;
     train) run train 600 python main.py --synthetic_images 2048 --image_size 224 --NUM_EPOCHS 2 --BATCH_SIZE 256 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/training.log; rc=$? ;;

@@ -132,9 +132,23 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        # host shadow of num_batches_tracked (the device buffer is bumped inside the BN
+        # kernel): momentum=None's cumulative average needs the count without a device sync
+        self._batches_host = 0
 
     def momentum_value(self) -> float:
-        return float(self.momentum) if self.momentum is not None else 0.1
+        """Momentum for this training step (nn.BatchNorm2d semantics, incl. None = cumulative
+        moving average 1 / num_batches_tracked), advancing the host batch count."""
+        self._batches_host += 1
+        if self.momentum is None:
+            return 1.0 / self._batches_host
+        return float(self.momentum)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        key = prefix + "num_batches_tracked"
+        if key in state_dict:
+            self._batches_host = int(state_dict[key])
 
     def forward(self, x, relu: bool = False):
         return Fn.bn_act(x, self, relu=relu)

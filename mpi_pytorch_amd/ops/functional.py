@@ -81,8 +81,7 @@ class _ConvBNAct(torch.autograd.Function):
                        _empty(x) if _NO_SHIFT else bn.running_mean)
         y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
                                        bn.momentum_value(), bn.eps,
-                                       _or_empty(residual, x), relu)
-        bn.num_batches_tracked.add_(1)
+                                       _or_empty(residual, x), relu, bn.num_batches_tracked)
         ctx.conv = conv
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -190,8 +189,7 @@ class _BNAct(torch.autograd.Function):
         k = K(x)
         y, mean, rstd = k.bn_fwd_train(x, _empty(x), gamma, beta, bn.running_mean,
                                        bn.running_var, bn.momentum_value(), bn.eps, _empty(x),
-                                       relu)
-        bn.num_batches_tracked.add_(1)
+                                       relu, bn.num_batches_tracked)
         ctx.params = (gamma, beta)
         ctx.save_for_backward(x, y if relu else None, mean, rstd)
         return y

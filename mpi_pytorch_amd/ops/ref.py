@@ -91,7 +91,8 @@ def act_bwd(dy, y, dbias):
 
 
 # ------------------------------------------------------------------------------------ BN
-def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu):
+def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu,
+                 counter=None):
     # the oracle always uses exact two-pass statistics (``stats`` from a fused producer
     # epilogue is accepted for API parity but not needed)
     C = x.shape[-1]
@@ -109,6 +110,8 @@ def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, re
         unbiased = var * (M / max(M - 1, 1))
         rmean.mul_(1 - momentum).add_(mean, alpha=momentum)
         rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+        if _opt(counter) is not None:
+            counter.add_(1)
     return y.reshape(x.shape).to(x.dtype), mean.contiguous(), rstd.contiguous()
 
 
