@@ -79,6 +79,7 @@ class Config:
     max_steps: int = 0                     # stop an epoch early (0 = full epoch)
     checksum_every: int = 0                # cross-rank replica checksum period (steps, 0=off)
     timeout_s: float = 1800.0              # rendezvous/collective timeout
+    watchdog_s: float = 900.0              # abort a rank with no step progress (0: off)
 
     def __post_init__(self) -> None:
         if not self.CHECKPOINT_NAME:

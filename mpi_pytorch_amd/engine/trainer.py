@@ -32,6 +32,7 @@ import torch
 
 from ..config import Config
 from ..checkpoint import save_checkpoint, load_checkpoint, build_state, checkpoint_path
+from ..parallel.watchdog import Watchdog
 from ..data.manifest import (read_manifests, synthetic_manifest, SyntheticImages, FolderImages,
                              images_available)
 from ..data.loader import IMAGENET_MEAN, IMAGENET_STD
@@ -176,6 +177,9 @@ def run_training(cfg: Config) -> dict:
     log.info("_Entering training Loop")
 
     history = []
+    # fail fast on a stalled rank (e.g. a peer died inside a collective): SURVEY.md §5.3
+    dog = Watchdog(cfg.watchdog_s, rank=rank).start()
+    gstep = 0
     for epoch in range(start_epoch, cfg.NUM_EPOCHS):
         model.train()
         if dev.type == "cuda":
@@ -185,7 +189,10 @@ def run_training(cfg: Config) -> dict:
         for x, y in train_loader.epoch(epoch, steps_per_epoch):
             step(x, y)
             nimg += x.shape[0]
+            gstep += 1
+            dog.beat(gstep)
         tr_loss = step.mean_loss()
+        dog.beat(gstep)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -207,6 +214,8 @@ def run_training(cfg: Config) -> dict:
                 log.info("_Epoch: {} | Acc: {}".format(epoch, acc))
         metrics.write(**rec)
         history.append(rec)
+        dog.beat(gstep)
+    dog.stop()
     return {"history": history, "checkpoint": ckpt}
 
 

@@ -5,3 +5,4 @@ from .comm import (num_processes, mpi_all_reduce, mpi_sum, mpi_avg_grads,  # noq
                    mpi_broadcast, sync_params, scatter_object, broadcast_object,
                    reduce_scalar, all_gather_object, replica_checksum)
 from .sharding import array_split_sizes, shard_bounds, shard_dataframe  # noqa: F401
+from .watchdog import Watchdog  # noqa: F401

@@ -73,6 +73,9 @@ def init_world(device: str = "auto", timeout_s: float = 1800.0,
     be = "none"
     if world > 1:
         be = backend or os.environ.get("MPA_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+        # RCCL communicator errors / timeouts raise in the rank that sees them (and tear the
+        # communicator down) instead of leaving the job hung; see parallel/watchdog.py
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         if not dist.is_initialized():

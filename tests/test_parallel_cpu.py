@@ -124,3 +124,32 @@ def test_dp_equivalence_gloo(overlap):
         grad, final = _single(d)
         assert torch.allclose(r0["grad"], grad, atol=1e-5, rtol=1e-4)
         assert torch.allclose(r0["final"], final, atol=1e-5, rtol=1e-4)
+
+
+def test_watchdog_fires_on_stall_and_not_while_beating():
+    import time
+    from mpi_pytorch_amd.parallel.watchdog import Watchdog
+    hits = []
+    dog = Watchdog(0.3, rank=3, on_timeout=hits.append, poll_s=0.02).start()
+    for i in range(10):  # steady progress: never fires
+        time.sleep(0.05)
+        dog.beat(i)
+    assert not hits
+    time.sleep(0.6)  # stall
+    assert hits and "rank 3" in hits[0] and "last completed step 9" in hits[0]
+    dog.stop()
+
+
+def test_watchdog_exits_process_with_stall_code():
+    """A stalled rank terminates with EXIT_STALLED and a stack dump (fail fast)."""
+    import subprocess
+    import sys
+    code = ("import time\n"
+            "from mpi_pytorch_amd.parallel.watchdog import Watchdog\n"
+            "Watchdog(0.2, rank=1, poll_s=0.02).start()\n"
+            "time.sleep(30)\n")
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       cwd=root)
+    assert r.returncode == 75, (r.returncode, r.stderr[-500:])
+    assert "rank 1: no train progress" in r.stderr and "Thread" in r.stderr
