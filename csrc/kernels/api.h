@@ -80,6 +80,7 @@ int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split sl
 int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LDS-DMA all
 void igemm_set_engine(int engine);
 void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
+void igemm_set_dma_uni(int on);  // LDS-DMA uniform-tap fast path (default on)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

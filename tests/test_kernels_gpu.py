@@ -49,13 +49,17 @@ def _pair(v):
     return v if isinstance(v, tuple) else (v, v)
 
 
-@pytest.fixture(params=[2, 0], ids=["dma", "reg"])
+@pytest.fixture(params=[(2, 1), (2, 0), (0, 1)], ids=["dma", "dma-generic", "reg"])
 def engine(request, gpu):
-    """Run a GEMM test on the LDS-DMA engine and on the register-staged engine."""
+    """Run a GEMM test on the LDS-DMA engine (uniform-tap fast path and generic gather)
+    and on the register-staged engine."""
     prev = C().igemm_engine()
-    C().igemm_set_engine(request.param)
-    yield request.param
+    eng, uni = request.param
+    C().igemm_set_engine(eng)
+    C().igemm_set_dma_uni(uni)
+    yield eng
     C().igemm_set_engine(prev)
+    C().igemm_set_dma_uni(1)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -125,19 +129,21 @@ def test_engines_bitwise_equal(gpu, case):
     prev = C().igemm_engine()
     outs = {}
     try:
-        for eng in (0, 2):
+        for eng, uni in ((0, 1), (2, 0), (2, 1)):
             C().igemm_set_engine(eng)
+            C().igemm_set_dma_uni(uni)
             for rep in range(3 if eng else 1):
                 stt = torch.zeros(2, K, device=gpu)
                 y = C().conv_fwd(x, w, e, st, st, ph, pw, False, stt, e)
                 dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
                 dw = torch.zeros(K, R, S, Cc, device=gpu)
                 C().conv_wgrad(dy, x, dw, st, st, ph, pw)
-                outs[(eng, rep)] = (y, stt, dx, dw)
+                outs[(eng, uni, rep)] = (y, stt, dx, dw)
     finally:
         C().igemm_set_engine(prev)
+        C().igemm_set_dma_uni(1)
     torch.cuda.synchronize()
-    base = outs[(0, 0)]
+    base = outs[(0, 1, 0)]
     for key, o in outs.items():
         for a, b, nm in zip(o, base, ("y", "stats", "dx", "dw")):
             assert torch.equal(a, b), (key, nm, rel(a, b))

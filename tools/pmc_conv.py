@@ -1,0 +1,30 @@
+"""Run a few ResNet-18 conv GEMMs (fwd / dgrad / wgrad, batch 256) a handful of times each,
+for hardware-counter collection:
+    rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES ... --kernel-trace --output-format csv \
+        -d out -- python tools/pmc_conv.py"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from mpi_pytorch_amd.ops import _ext
+
+C = _ext.ext()
+dev = torch.device("cuda", 0)
+B = 256
+LAYERS = [("l1.3x3", 56, 64, 64, 3, 1, 1), ("l3.3x3", 14, 256, 256, 3, 1, 1)]
+for name, H, Ci, Co, R, st, pd in LAYERS:
+    x = torch.randn(B, H, H, Ci, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, R, R, Ci, device=dev) * 0.05).to(torch.bfloat16)
+    P = (H + 2 * pd - R) // st + 1
+    dy = torch.randn(B, P, P, Co, device=dev).to(torch.bfloat16)
+    dw = torch.zeros(Co, R, R, Ci, device=dev)
+    e = torch.empty(0, device=dev)
+    stats = torch.empty(2, Co, device=dev)
+    for _ in range(3):
+        C.conv_fwd(x, w, e, st, st, pd, pd, False, stats, e)
+        C.conv_dgrad(dy, w, H, H, st, st, pd, pd)
+        C.conv_wgrad(dy, x, dw, st, st, pd, pd)
+    torch.cuda.synchronize()
+print("done")
