@@ -488,9 +488,9 @@ static int occ_target() {
 }
 
 // Staging engine for 16-B-granular operands: 0 = register-staged (this file),
-// 1 = tuned default: LDS-DMA (igemm_dma.hip) for the rows GEMMs (fwd / dgrad / linear)
-//     and for the wgrad shapes its 8-wave tile wins (wgrad_big), register-staged wgrad
-//     elsewhere (the 4-wave wgrad tiles measure ~10 % faster register-staged),
+// 1 = tuned default: LDS-DMA (igemm_dma.hip) for the rows GEMMs (fwd / dgrad / linear);
+//     for wgrad the 8-wave generic DMA tile where it wins (wgrad_big), the incremental
+//     DMA kernel where it applies, register staging elsewhere,
 // 2 = LDS-DMA for every GEMM.  MPA_IGEMM_ENGINE=0|1|2 sets the start value;
 // igemm_set_engine switches at run time (A/B benchmarks, cross-checking tests).
 static int g_engine = -1;
@@ -738,6 +738,8 @@ static bool wgrad_big(const WGradArgs& a, bool dma_ok) {
 static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bool big) {
   BM = (a.Kout <= 64) ? 64 : 128;
   BN = 128;
+  // few 128-row tiles (e.g. a 1x1 downsample: Ncols = C_in): halve BM for parallelism
+  if (dma && BM == 128 && ((a.Kout + 127) / 128) * ((a.Ncols + 127) / 128) < 4) BM = 64;
   if (big) BN = 256, BM = 128;
   if (g_force_bm && g_force_bn) {
     const bool ok_reg = (g_force_bm == 64 || g_force_bm == 128) && g_force_bn == 128;
@@ -772,7 +774,10 @@ void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   int BM, BN, splits;
   const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
   const bool big = wgrad_big(a, dma_ok);
-  const bool dma = big || (dma_ok && igemm_engine() == 2);
+  // engine 1: big 8-wave tile where it wins, else the incremental-pixel DMA kernel
+  // (tools/bench_kernels.py sweep: equal or faster than register staging on every
+  // ResNet-18 wgrad shape it covers), else register staging
+  const bool dma = big || (dma_ok && (igemm_engine() == 2 || igemm_wgrad_inc_ok(a)));
   wgrad_plan(a, BM, BN, splits, dma, big);
   if (dma && igemm_wgrad_dma(a, BM, BN, splits, s)) {
     // LDS-DMA engine (igemm_dma.hip)

@@ -281,5 +281,6 @@ __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
 // required).  Return false when no instantiation covers the tile shape.
 bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hipStream_t s);
 bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s);
+bool igemm_wgrad_inc_ok(const WGradArgs& a);  // incremental-pixel wgrad kernel applies
 
 }  // namespace mpa

@@ -54,7 +54,8 @@ __device__ __forceinline__ int kc_lane_chunk(int lane) {
 }
 
 // waves per SIMD allowed by the 3-stage ring's LDS (160 KiB per CU) for a block of `nw`
-// waves, capped at 3 (<= 168 VGPRs per lane): the occupancy target of __launch_bounds__
+// waves, capped at 3 (<= 168 VGPRs per lane): the occupancy target of __launch_bounds__.
+// (A cap of 4 for 8-wave blocks forces 22-44 spilled VGPRs on the fast-path kernels.)
 constexpr int dma_occ(int lds_bytes, int nw) {
   return ((160 * 1024) / lds_bytes) * nw / 4 >= 3 ? 3
          : (((160 * 1024) / lds_bytes) * nw / 4 >= 2 ? 2 : 1);
@@ -544,6 +545,162 @@ void igemm_wgrad_dma_kernel(WGradArgs p) {
 }
 
 // ======================================================================================
+//  wgrad kernel, incremental fast path.  Each lane's pixel (kt*32 + its k-row) advances
+//  by exactly 32 per K-step, i.e. by (dP, dQ) = (32 / Q, 32 % Q) output rows/cols; with
+//  32/Q + 1 <= P the column wrap and the image wrap are each ONE conditional, so the
+//  lane keeps (oh*sh, ow*sw, input element offset) as 32-bit state updated by scalar
+//  constants with no division, no 64-bit multiply and no divergent loop.  Output
+//  channels past Kout and columns past R*S*C are clamped instead of masked (their
+//  results are never stored); pixels past Mpix read the zero page.
+// ======================================================================================
+struct WInc {   // per-launch scalar constants of the pixel walk
+  int dq_s, dp_s;          // sw * (32 % Q), sh * (32 / Q): per-step ow*sw / oh*sh advance
+  int qwrap, pwrap;        // Q * sw, P * sh: wrap thresholds of ow*sw and oh*sh
+  int step_off;            // input offset advance per step (no wrap)
+  int qwrap_off, pwrap_off;  // extra input offset on a column / image wrap
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64, dma_occ(3 * (BM + BN) * 64, WM * WN))
+void igemm_wgrad_dma_inc_kernel(WGradArgs p, WInc w) {
+  constexpr int NW = WM * WN;
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int CPRA = BM / 8, RPIA = 64 / CPRA;
+  constexpr int CPRB = BN / 8, RPIB = 64 / CPRB;
+  constexpr int IA = BM / 16, IB = BN / 16;
+  constexpr int IAW = (IA + NW - 1) / NW, IBW = (IB + NW - 1) / NW;
+  constexpr int WAITN = IA / NW + IB / NW;
+  constexpr int TM = BM / WM / 16;
+  constexpr int TN = BN / WN / 16;
+  static_assert(NW == 4 || NW == 8, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ktiles = (p.Mpix + BK - 1) / BK;
+  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kend = min(ktiles, kbeg + p.ktiles_per_split);
+  if (kbeg >= kend) return;
+  const bf16_t* const zp = (const bf16_t*)g_zero16;
+
+  // ---- A (dy [pix][Kout]): row pointer walks by 32 pixels per step
+  const bf16_t* a_ptr[IAW];
+  int a_pix[IAW];
+#pragma unroll
+  for (int i = 0; i < IAW; ++i) {
+    const int ja = min(wave + NW * i, IA - 1);
+    const int row = RPIA * ja + lane / CPRA;
+    const int m = min(m0 + (((lane % CPRA) ^ mn_swz<BM>(row)) << 3), p.Kout - 8);
+    a_pix[i] = kbeg * BK + row;
+    a_ptr[i] = p.dy + (size_t)a_pix[i] * p.Kout + m;
+  }
+  // ---- B (im2col(x)): fixed column (tap, channel) + incremental pixel state
+  int b_dh[IBW], b_dw[IBW], b_col[IBW], b_pix[IBW], b_ohs[IBW], b_ows[IBW], b_off[IBW];
+  const int PQ = p.P * p.Q;
+#pragma unroll
+  for (int i = 0; i < IBW; ++i) {
+    const int jb = min(wave + NW * i, IB - 1);
+    const int krow = RPIB * jb + lane / CPRB;
+    const int n = min(n0 + (((lane % CPRB) ^ mn_swz<BN>(krow)) << 3), p.Ncols - 8);
+    const int tap = n / p.C;
+    const int r = tap / p.S;
+    b_dh[i] = r - p.ph;
+    b_dw[i] = tap - r * p.S - p.pw;
+    b_col[i] = (b_dh[i] * p.W + b_dw[i]) * p.C + (n - tap * p.C);
+    const int pix = kbeg * BK + krow;
+    const int img = pix / PQ;
+    const int rr = pix - img * PQ;
+    const int oh = rr / p.Q;
+    const int ow = rr - oh * p.Q;
+    b_pix[i] = pix;
+    b_ohs[i] = oh * p.sh;
+    b_ows[i] = ow * p.sw;
+    b_off[i] = ((img * p.H + b_ohs[i]) * p.W + b_ows[i]) * p.C;
+  }
+
+  auto issue = [&](char* st) {
+#pragma unroll
+    for (int i = 0; i < IAW; ++i) {
+      const int ja = wave + NW * i;
+      if (ja < IA) {
+        glds16(a_pix[i] < p.Mpix ? a_ptr[i] : zp, st + ja * 1024);
+        a_pix[i] += BK;
+        a_ptr[i] += (size_t)BK * p.Kout;
+      }
+    }
+    char* bimg = st + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < IBW; ++i) {
+      const int jb = wave + NW * i;
+      if (jb < IB) {
+        const bool ok = (b_pix[i] < p.Mpix) &
+                        ((unsigned)(b_ohs[i] + b_dh[i]) < (unsigned)p.H) &
+                        ((unsigned)(b_ows[i] + b_dw[i]) < (unsigned)p.W);
+        glds16(ok ? p.x + (b_off[i] + b_col[i]) : zp, bimg + jb * 1024);
+        // advance this lane's pixel by 32: at most one column wrap, one image wrap
+        b_pix[i] += BK;
+        b_ows[i] += w.dq_s;
+        b_ohs[i] += w.dp_s;
+        b_off[i] += w.step_off;
+        const bool qw = b_ows[i] >= w.qwrap;
+        b_ows[i] -= qw ? w.qwrap : 0;
+        b_ohs[i] += qw ? p.sh : 0;
+        b_off[i] += qw ? w.qwrap_off : 0;
+        const bool pw_ = b_ohs[i] >= w.pwrap;
+        b_ohs[i] -= pw_ ? w.pwrap : 0;
+        b_off[i] += pw_ ? w.pwrap_off : 0;
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wrow0 = wm * (BM / WM);
+  const int wcol0 = wn * (BN / WN);
+  auto compute = [&](const char* st) {
+    const char* bimg = st + A_BYTES;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag_mn<BM>(st, wrow0 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag_mn<BN>(bimg, wcol0 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+  };
+
+  issue(smem);
+  if (kbeg + 1 < kend) issue(smem + STAGE);
+  int kt = kbeg;
+  auto step = [&](auto sc) {
+    constexpr int S = decltype(sc)::value;
+    if (kt + 1 < kend) wait_barrier<WAITN>();
+    else wait_barrier<0>();
+    if (kt + 2 < kend) issue(smem + ((S + 2) % 3) * STAGE);
+    compute(smem + S * STAGE);
+    ++kt;
+  };
+  while (kt + 3 <= kend) {
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+  }
+  if (kt < kend) step(std::integral_constant<int, 0>{});
+  if (kt < kend) step(std::integral_constant<int, 1>{});
+  wgrad_epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wrow0, wcol0, lane);
+}
+
+// ======================================================================================
 //  host launchers (plans are made by igemm.hip)
 // ======================================================================================
 // uniform-tap fast path on/off (A/B and cross-checking; MPA_DMA_UNI=0 disables)
@@ -590,8 +747,36 @@ bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hi
   return bkc ? rows_dma_tile<true>(a, BM, BN, splits, s) : rows_dma_tile<false>(a, BM, BN, splits, s);
 }
 
+// incremental pixel walk applicable: one wrap per step suffices, 32-bit offsets, and
+// 16-B granular operands on both sides (callers guarantee Kout % 8 == 0, C % 8 == 0)
+bool igemm_wgrad_inc_ok(const WGradArgs& a) {
+  return g_dma_uni && (BK / a.Q) + 1 <= a.P && a.Ncols >= 8 && a.Kout >= 8 &&
+         (int64_t)a.Mpix / (a.P * a.Q) * a.H * a.W * a.C < (1ll << 31);
+}
+
+template <int BM, int BN, int WM, int WN>
+static void launch_wgrad_inc(const WGradArgs& a, dim3 grid, hipStream_t s) {
+  WInc w;
+  w.dq_s = a.sw * (BK % a.Q);
+  w.dp_s = a.sh * (BK / a.Q);
+  w.qwrap = a.Q * a.sw;
+  w.pwrap = a.P * a.sh;
+  w.step_off = (w.dp_s * a.W + w.dq_s) * a.C;
+  w.qwrap_off = (a.sh * a.W - a.Q * a.sw) * a.C;
+  w.pwrap_off = (a.H - a.P * a.sh) * a.W * a.C;
+  hipLaunchKernelGGL((igemm_wgrad_dma_inc_kernel<BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0,
+                     s, a, w);
+}
+
 bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
+  // incremental kernel for the 4-wave tiles; the 8-wave tiles keep the generic kernel
+  // (the extra per-lane pixel state costs them their second block per CU: 124 -> 166 VGPR)
+  if (igemm_wgrad_inc_ok(a) && BN == 128 && (BM == 128 || BM == 64)) {
+    if (BM == 128) launch_wgrad_inc<128, 128, 2, 2>(a, grid, s);
+    else launch_wgrad_inc<64, 128, 2, 2>(a, grid, s);
+    return true;
+  }
   if (BM == 256 && BN == 256)
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
   else if (BM == 128 && BN == 256)
