@@ -89,6 +89,20 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
     }
   a.Ktot = a.T * C;
   a.B = bp(w); a.N = K; a.RS = R * S; a.ldb = a.Ktot;
+  if (C == 8 && S > 1 && mpa::igemm_stap_ok()) {
+    // 8-channel image stem: group 4 adjacent kernel columns into one 32-deep K tile (their
+    // input pixels are 64 contiguous bytes in NHWC), so the stem takes the uniform-tap
+    // fast path; columns past S get zero weights.  K grows from R*S*8 to R*ceil(S/4)*32.
+    int t = 0;
+    for (int r = 0; r < R; ++r)
+      for (int s0 = 0; s0 < S; s0 += 4, ++t) {
+        a.taps.dh[t] = r; a.taps.dw[t] = s0;
+        a.taps.bt[t] = (short)((r * S + s0) | (std::min(4, S - s0) << 12));
+      }
+    a.T = t;
+    a.Ktot = t * 32;
+    a.stap = 1;
+  }
   a.C = y.data_ptr(); a.ldc = K;
   a.dH = P; a.dW = Q; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   a.bias = fopt(bias);

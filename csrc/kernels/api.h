@@ -53,6 +53,8 @@ struct IGemmArgs {
   Taps taps;
   int nphase;             // > 0: merged stride-phase dgrad launch (igemm_rows_dgrad_phases)
   PhaseDesc ph[MAXPH];
+  int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
+                          // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
 };
 
 struct WGradArgs {
@@ -81,6 +83,7 @@ int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LD
 void igemm_set_engine(int engine);
 void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
 void igemm_set_dma_uni(int on);  // LDS-DMA uniform-tap fast path (default on)
+bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path on)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

@@ -740,10 +740,11 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
   BN = 128;
   // few 128-row tiles (e.g. a 1x1 downsample: Ncols = C_in): halve BM for parallelism
   if (dma && BM == 128 && ((a.Kout + 127) / 128) * ((a.Ncols + 127) / 128) < 4) BM = 64;
-  if (big) BN = 256, BM = 128;
+  if (big) BN = 256, BM = (a.Kout <= 64) ? 64 : 128;  // 64-row stems: no half-empty tile
   if (g_force_bm && g_force_bn) {
     const bool ok_reg = (g_force_bm == 64 || g_force_bm == 128) && g_force_bn == 128;
-    const bool ok_dma = ok_reg || (g_force_bn == 256 && (g_force_bm == 128 || g_force_bm == 256));
+    const bool ok_dma = ok_reg || (g_force_bn == 256 && (g_force_bm == 64 || g_force_bm == 128 ||
+                                                         g_force_bm == 256));
     if (dma ? ok_dma : ok_reg) { BM = g_force_bm; BN = g_force_bn; }
   }
   a.tiles_n = (a.Ncols + BN - 1) / BN;

@@ -306,6 +306,8 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
 
   const int kch = kc_lane_chunk(lane);
   const int aC = p.aC;
+  // K elements per tap-table entry: aC, or 32 for super-taps (4 kernel columns x 8 ch)
+  const int kpt = p.stap ? BK : aC;
   // ---- A rows (rows past M clamp to M-1: their outputs are discarded)
   const bf16_t* a_ptr[IAW];
   int a_bh[IAW], a_bw[IAW];
@@ -320,6 +322,7 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     a_bw[i] = (r - oh * g.oW) * p.Uw + p.Ow;
     const int64_t base = (((int64_t)img * p.aH + a_bh[i]) * p.aW + a_bw[i]) * aC + kch * 8;
     a_ptr[i] = p.A + base;
+    if (p.stap) a_bw[i] += kch;  // super-tap: chunk kch is the input pixel kch columns right
   }
   // ---- B rows (K-contig) or k-rows x column chunks (N-contig), clamped
   const bf16_t* b_ptr[IBW];
@@ -338,8 +341,8 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const bf16_t* const zp = (const bf16_t*)g_zero16;
 
   // K-step state (wave-uniform): tap index and channel offset of k = kt * 32
-  int t_s = (kbeg * BK) / aC;
-  int c_s = kbeg * BK - t_s * aC;
+  int t_s = (kbeg * BK) / kpt;
+  int c_s = kbeg * BK - t_s * kpt;
   auto issue = [&](int kt, char* st) {
     const int hwv = __builtin_amdgcn_readfirstlane(tap_hw[t_s]);
     const int dh = hwv >> 16, dw = (short)(hwv & 0xffff);
@@ -351,20 +354,21 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
       glds16(ok ? a_ptr[i] + toff : zp, st + (wave * IAW + i) * 1024);
     }
     char* bimg = st + A_BYTES;
+    // weight tap in bits 0..11; super-taps carry their valid column count in bits 12..14
+    const int btv = __builtin_amdgcn_readfirstlane(tap_b[t_s]);
+    const int bt = btv & 0xfff;
     int64_t boff;
-    if constexpr (BKC) {
-      boff = (int64_t)kt * BK;
-    } else {
-      const int bt = __builtin_amdgcn_readfirstlane(tap_b[t_s]);
-      boff = ((int64_t)c_s * p.RS + bt) * p.ldb;
-    }
+    if constexpr (BKC) boff = (int64_t)bt * aC + c_s;  // weight K index (bt, c)
+    else boff = ((int64_t)c_s * p.RS + bt) * p.ldb;
+    // super-tap: chunks past the kernel's last column read zeros (ns valid columns)
+    const bool bok = !p.stap || kch < (btv >> 12);
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
       const int jb = wave + NW * i;
-      if (jb < IB) glds16(b_ptr[i] + boff, bimg + jb * 1024);
+      if (jb < IB) glds16(bok ? b_ptr[i] + boff : zp, bimg + jb * 1024);
     }
     c_s += BK;
-    if (c_s >= aC) { c_s = 0; ++t_s; }
+    if (c_s >= kpt) { c_s = 0; ++t_s; }
   };
 
   f32x4 acc[TM][TN];
@@ -709,9 +713,10 @@ static bool g_dma_uni = [] {
   return !(e && e[0] == '0');
 }();
 void igemm_set_dma_uni(int on) { g_dma_uni = on != 0; }
+bool igemm_stap_ok() { return g_dma_uni && igemm_engine() >= 1; }
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
 static void launch_rows_dma_v(const IGemmArgs& a, dim3 grid, hipStream_t s) {
-  if (a.aC % BK == 0 && g_dma_uni)
+  if ((a.aC % BK == 0 || a.stap) && g_dma_uni)
     hipLaunchKernelGGL((igemm_rows_dma_uni_kernel<BM, BN, WM, WN, BKC, SPLIT, PH>), grid,
                        dim3(WM * WN * 64), 0, s, a);
   else
@@ -781,6 +786,8 @@ bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
   else if (BM == 128 && BN == 256)
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<128, 256, 2, 4>), grid, dim3(512), 0, s, a);
+  else if (BM == 64 && BN == 256)
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<64, 256, 2, 4>), grid, dim3(512), 0, s, a);
   else if (BM == 128 && BN == 128)
     hipLaunchKernelGGL((igemm_wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
   else if (BM == 64 && BN == 128)

@@ -19,6 +19,8 @@ for step in "$@"; do
     benchk) run benchk 600 python tools/bench_kernels.py 256 10; rc=$? ;;
     benchk1) MPA_BENCH_ENGINES=1 run benchk1 600 python tools/bench_kernels.py 256 10; rc=$? ;;
     sweep) run sweep 900 python tools/bench_kernels.py 256 5 sweep; rc=$? ;;
+    dp2) MPA_DIST_BACKEND=gloo run dp2 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 2 --batch 64; rc=$? ;;
+    dp2t) MPA_DIST_BACKEND=gloo run dp2t 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29556 tools/dp_check.py; rc=$? ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
     benchbn) for g in 0 256 512 1024; do for u in 1; do MPA_BN_GRID=$g MPA_BN_UNR=$u timeout -k 10 120 python tools/bench_bn.py 20 >> gpurun_out/benchbn.log 2>&1 || exit 1; done; done; rc=0 ;;
     diageng) run diageng 600 python tools/diag_engines.py inception 299 4; rc=$? ;;

@@ -75,7 +75,7 @@ class GradBucketer:
             self._works[i] = None
 
     def _on_grad(self, p: nn.Parameter) -> None:
-        if not self.overlap:
+        if not (self.active and self.overlap):
             return
         bi = self.bucket_of.get(id(p))
         if bi is None:
