@@ -434,35 +434,47 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
 }
 
 // ------------------------------------------------------------------------ loss / acc
+// logits: [B][NC] bf16 with unit column stride; rows may be padded (stride(0) >= NC, a
+// view of a classifier's padded output)
+static int logits_ld(const Tensor& logits) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == torch::kBFloat16 && logits.dim() == 2,
+              "logits must be a 2-D bf16 GPU tensor");
+  TORCH_CHECK(logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
+              "logits: rows must be unit-stride");
+  return (int)logits.stride(0);
+}
+
 std::vector<Tensor> ce_fwd(Tensor logits, Tensor labels) {
-  CHECK_ACT(logits);
+  const int ld = logits_ld(logits);
   CHECK_CUDA(labels);
   TORCH_CHECK(labels.scalar_type() == torch::kInt64, "labels must be int64");
   const int B = logits.size(0), NC = logits.size(1);
   const c10::OptionalDeviceGuard g(device_of(logits));
   Tensor loss = torch::empty({1}, logits.options().dtype(torch::kFloat32));
   Tensor lse = torch::empty({B}, logits.options().dtype(torch::kFloat32));
-  mpa::ce_fwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), B, NC, loss.data_ptr<float>(),
-              lse.data_ptr<float>(), cur_stream());
+  mpa::ce_fwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), B, NC, ld,
+              loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
   return {loss, lse};
 }
 
+// returns dlogits with the same row stride as logits (a view of a zero-padded buffer when
+// the logits are padded)
 Tensor ce_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor grad_out) {
-  CHECK_ACT(logits);
+  const int ld = logits_ld(logits);
   const int B = logits.size(0), NC = logits.size(1);
   const c10::OptionalDeviceGuard g(device_of(logits));
-  Tensor d = torch::empty_like(logits);
+  Tensor d = torch::empty({B, ld}, logits.options());
   mpa::ce_bwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), fopt(lse), fopt(grad_out), B,
-              NC, bpm(d), cur_stream());
-  return d;
+              NC, ld, bpm(d), cur_stream());
+  return ld == NC ? d : d.narrow(1, 0, NC);
 }
 
 void argmax_correct(Tensor logits, Tensor labels, Tensor count) {
-  CHECK_ACT(logits);
+  const int ld = logits_ld(logits);
   TORCH_CHECK(count.scalar_type() == torch::kInt64, "count must be int64");
   const c10::OptionalDeviceGuard g(device_of(logits));
   mpa::argmax_correct(bp(logits), labels.contiguous().data_ptr<int64_t>(), logits.size(0),
-                      logits.size(1), count.data_ptr<int64_t>(), cur_stream());
+                      logits.size(1), ld, count.data_ptr<int64_t>(), cur_stream());
 }
 
 // ----------------------------------------------------------------------------- optim

@@ -126,11 +126,13 @@ void adaptive_avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P,
                           bf16_raw* dx, hipStream_t s);
 
 // loss.hip
-void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, float* loss,
+// logits rows have stride ld >= NC (padded heads); ce_bwd writes dlogits with stride ld and
+// zeros in columns NC..ld-1
+void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s);
 void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,
-            const float* grad_out, int B, int NC, bf16_raw* dlogits, hipStream_t s);
-void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC,
+            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s);
+void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
                     int64_t* count, hipStream_t s);
 
 // optim.hip (flat fp32 arenas)

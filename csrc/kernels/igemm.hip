@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_wgrad_kernel(WGradArgs p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     if (more) store_tiles(smem + (cur ^ 1) * STAGE);
     __syncthreads();
     cur ^= 1;

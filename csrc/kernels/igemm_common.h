@@ -245,9 +245,11 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
   }
 }
 
-// Wgrad engine: lane owns D[m = mb + r][n = lane&15].  One split: exclusive read-modify-
-// write into the fp32 gradient arena.  Several splits: plain stores of this split's partial
-// into the slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
+// Wgrad engine.  The MFMA is issued with the column (r,s,c) operand first, so lane owns
+// D[n = nb + r][m = lane&15]: four consecutive weight-gradient columns of one output
+// channel -> one 16-B fp32 access per lane.  One split: read-modify-write straight into
+// the fp32 gradient arena.  Several splits: plain stores of this split's partial into the
+// slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
                                                f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
@@ -255,22 +257,26 @@ __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
                                                int lane) {
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
-  const int ml = (lane >> 4) * 4;
+  const int nl = (lane >> 4) * 4;
   const bool direct = gridDim.z == 1;
+  const bool vec = (p.Ncols & 3) == 0;
   float* dst = direct ? p.dw : p.slab + (size_t)blockIdx.z * p.Kout * p.Ncols;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wrow0 + i * 16 + (lane & 15);
+    if (m >= p.Kout) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wcol0 + j * 16 + (lane & 15);
-      if (n >= p.Ncols) continue;
+      const int n = n0 + wcol0 + j * 16 + nl;
+      float* q = dst + (size_t)m * p.Ncols + n;
+      if (vec && n + 3 < p.Ncols) {
+        f32x4 v = acc[i][j];
+        if (direct) v += *(const f32x4*)q;
+        *(f32x4*)q = v;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wrow0 + i * 16 + ml + r;
-        if (m < p.Kout) {
-          float* q = dst + (size_t)m * p.Ncols + n;
-          *q = direct ? *q + acc[i][j][r] : acc[i][j][r];
-        }
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.Ncols) q[r] = direct ? q[r] + acc[i][j][r] : acc[i][j][r];
       }
     }
   }

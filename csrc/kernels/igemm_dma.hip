@@ -542,7 +542,7 @@ void igemm_wgrad_dma_kernel(WGradArgs p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     s = (s == 2) ? 0 : s + 1;
   }
   wgrad_epilogue<BM, BN, WM, WN>(p, acc, m0, n0, wrow0, wcol0, lane);
@@ -680,7 +680,7 @@ void igemm_wgrad_dma_inc_kernel(WGradArgs p, WInc w) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
   };
 
   issue(smem);

@@ -7,6 +7,10 @@
 // (softmax - onehot) * grad_out / B in bf16: logits are read twice in total, the
 // gradient written once.  Reference: nn.CrossEntropyLoss at main.py:134,150 over a
 // 64,500-wide head (utils.py:39); argmax accuracy at main.py:182-183.
+//
+// Rows may be padded (row stride ld >= NC): classifier heads store their output dim
+// rounded up to a multiple of 32 so every GEMM of the head stays 16-B granular; the
+// backward writes zeros into the padding columns of dlogits.
 #include "common.h"
 #include "api.h"
 #include <algorithm>
@@ -36,10 +40,10 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 template <int V>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ logits,
                                                       const int64_t* __restrict__ labels, int B,
-                                                      int NC, float* __restrict__ loss,
+                                                      int NC, int ld, float* __restrict__ loss,
                                                       float* __restrict__ lse_out) {
   const int row = blockIdx.x;
-  const bf16_t* x = logits + (size_t)row * NC;
+  const bf16_t* x = logits + (size_t)row * ld;
   float m = -INFINITY, s = 0.f;
   const int nv = NC / V;
   for (int i = threadIdx.x; i < nv; i += 256) {
@@ -81,9 +85,9 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
                                                       const int64_t* __restrict__ labels,
                                                       const float* __restrict__ lse,
                                                       const float* __restrict__ grad_out, int B,
-                                                      int NC, bf16_t* __restrict__ dlogits) {
+                                                      int NC, int ld, bf16_t* __restrict__ dlogits) {
   const float scale = grad_out[0] / (float)B;
-  const int nv = NC / V;
+  const int nv = ld / V;  // whole padded row: columns >= NC get zero gradient
   const int64_t total = (int64_t)B * nv;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -92,13 +96,13 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
     const float l = lse[row];
     const int64_t lab = labels[row];
     float f[V];
-    const size_t off = (size_t)row * NC + c0;
+    const size_t off = (size_t)row * ld + c0;
     load_v<V>(logits + off, f);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       float p = __expf(f[j] - l);
       if (c0 + j == lab) p -= 1.f;
-      f[j] = p * scale;
+      f[j] = (c0 + j < NC) ? p * scale : 0.f;
     }
     if constexpr (V == 8) {
       *(uint4*)(dlogits + off) = pack8(f);
@@ -112,9 +116,9 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
 
 __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ logits,
                                                       const int64_t* __restrict__ labels, int NC,
-                                                      unsigned long long* __restrict__ count) {
+                                                      int ld, unsigned long long* __restrict__ count) {
   const int row = blockIdx.x;
-  const bf16_t* x = logits + (size_t)row * NC;
+  const bf16_t* x = logits + (size_t)row * ld;
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int i = threadIdx.x; i < NC; i += 256) {
@@ -139,36 +143,40 @@ __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ 
   }
 }
 
-void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, float* loss,
+void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s) {
   (void)hipMemsetAsync(loss, 0, sizeof(float), s);
-  if (NC % 8 == 0)
-    hipLaunchKernelGGL(ce_fwd_kernel<8>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, loss, lse);
-  else if (NC % 4 == 0)
-    hipLaunchKernelGGL(ce_fwd_kernel<4>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, loss, lse);
+  const int g = NC % 8 == 0 && ld % 8 == 0 ? 8 : (NC % 4 == 0 && ld % 4 == 0 ? 4 : 1);
+  if (g == 8)
+    hipLaunchKernelGGL(ce_fwd_kernel<8>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, ld, loss,
+                       lse);
+  else if (g == 4)
+    hipLaunchKernelGGL(ce_fwd_kernel<4>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, ld, loss,
+                       lse);
   else
-    hipLaunchKernelGGL(ce_fwd_kernel<1>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, loss, lse);
+    hipLaunchKernelGGL(ce_fwd_kernel<1>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, ld, loss,
+                       lse);
 }
 
 void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,
-            const float* grad_out, int B, int NC, bf16_raw* dlogits, hipStream_t s) {
-  const int V = (NC % 8 == 0) ? 8 : (NC % 4 == 0 ? 4 : 1);
-  const int64_t total = (int64_t)B * (NC / V);
+            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s) {
+  const int V = (ld % 8 == 0) ? 8 : (ld % 4 == 0 ? 4 : 1);
+  const int64_t total = (int64_t)B * (ld / V);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
   if (V == 8)
     hipLaunchKernelGGL(ce_bwd_kernel<8>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, dlogits);
+                       grad_out, B, NC, ld, dlogits);
   else if (V == 4)
     hipLaunchKernelGGL(ce_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, dlogits);
+                       grad_out, B, NC, ld, dlogits);
   else
     hipLaunchKernelGGL(ce_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, dlogits);
+                       grad_out, B, NC, ld, dlogits);
 }
 
-void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC,
+void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
                     int64_t* count, hipStream_t s) {
-  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, s, logits, labels, NC,
+  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, s, logits, labels, NC, ld,
                      (unsigned long long*)count);
 }
 

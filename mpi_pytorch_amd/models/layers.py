@@ -157,40 +157,67 @@ class BatchNorm2d(nn.Module):
         return "{}, eps={}, momentum={}".format(self.num_features, self.eps, self.momentum)
 
 
+def _pad_rows(n: int) -> int:
+    """Stored output width of a Linear: rounded up to a multiple of 32."""
+    return n if n % 32 == 0 else (n + 31) // 32 * 32
+
+
 class Linear(nn.Module):
     """Linear layer.  ``in_chw=(C,H,W)`` marks a layer fed by an NHWC flatten: its input
     columns are stored in (h,w,c) order internally and exported in torchvision's
-    NCHW-flatten (c,h,w) order."""
+    NCHW-flatten (c,h,w) order.
+
+    The output dim is stored rounded up to a multiple of 32 (``out_store``) with zero
+    weight rows and bias entries: a 64,500-class head becomes 64,512 rows, so its forward,
+    dgrad, wgrad and bias-gradient all run on the 16-B-granular LDS-DMA GEMM paths
+    instead of scalar/8-byte fallbacks.  ``forward`` returns the first ``out_features``
+    columns (a view); the padding is invisible in state_dict and optimizer state, and the
+    padded rows never receive gradient (the cross-entropy backward writes zeros there).
+    """
 
     def __init__(self, in_features: int, out_features: int, bias: bool = True,
                  in_chw: Optional[Tuple[int, int, int]] = None):
         super().__init__()
         self.in_features = in_features
         self.out_features = out_features
+        self.out_store = _pad_rows(out_features)
         self.in_chw = in_chw
         w = torch.empty(out_features, in_features)
         nn.init.kaiming_uniform_(w, a=math.sqrt(5))
         self.weight = nn.Parameter(self._imp(w).contiguous())
-        if in_chw is not None:
+        if in_chw is not None or self.out_store != out_features:
             self.weight._mpa_export = self._exp
             self.weight._mpa_import = self._imp
         if bias:
             bound = 1 / math.sqrt(in_features)
-            self.bias = nn.Parameter(torch.empty(out_features).uniform_(-bound, bound))
+            b = torch.empty(out_features).uniform_(-bound, bound)
+            self.bias = nn.Parameter(self._imp_bias(b))
+            if self.out_store != out_features:
+                self.bias._mpa_export = self._exp_bias
+                self.bias._mpa_import = self._imp_bias
         else:
             self.register_parameter("bias", None)
 
-    def _exp(self, t):  # internal (o, h*w*c) -> torchvision (o, c*h*w)
+    def _exp(self, t):  # internal (o_store, h*w*c) -> torchvision (o, c*h*w)
+        t = t[:self.out_features]
         if self.in_chw is None:
             return t
         C, H, W = self.in_chw
         return t.reshape(t.shape[0], H, W, C).permute(0, 3, 1, 2).reshape(t.shape[0], C * H * W)
 
     def _imp(self, t):
-        if self.in_chw is None:
-            return t
-        C, H, W = self.in_chw
-        return t.reshape(t.shape[0], C, H, W).permute(0, 2, 3, 1).reshape(t.shape[0], H * W * C)
+        if self.in_chw is not None:
+            C, H, W = self.in_chw
+            t = t.reshape(t.shape[0], C, H, W).permute(0, 2, 3, 1).reshape(t.shape[0], H * W * C)
+        if t.shape[0] < self.out_store:
+            t = F.pad(t, (0, 0, 0, self.out_store - t.shape[0]))
+        return t
+
+    def _exp_bias(self, t):
+        return t[:self.out_features]
+
+    def _imp_bias(self, t):
+        return F.pad(t, (0, self.out_store - t.shape[0])) if t.shape[0] < self.out_store else t
 
     def init_(self, fn) -> "Linear":
         with torch.no_grad():
@@ -202,15 +229,22 @@ class Linear(nn.Module):
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         super()._save_to_state_dict(destination, prefix, keep_vars)
         k = prefix + "weight"
-        if k in destination and self.in_chw is not None:
-            w = destination[k]
-            destination[k] = self._exp(w) if keep_vars else self._exp(w).contiguous()
+        if k in destination:
+            w = self._exp(destination[k])
+            destination[k] = w if keep_vars else w.contiguous()
+        k = prefix + "bias"
+        if k in destination and destination[k] is not None:
+            b = self._exp_bias(destination[k])
+            destination[k] = b if keep_vars else b.contiguous()
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
         k = prefix + "weight"
-        if k in state_dict and self.in_chw is not None:
+        if k in state_dict and tuple(state_dict[k].shape) == (self.out_features, self.in_features):
             state_dict[k] = self._imp(state_dict[k])
+        k = prefix + "bias"
+        if k in state_dict and tuple(state_dict[k].shape) == (self.out_features,):
+            state_dict[k] = self._imp_bias(state_dict[k])
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 

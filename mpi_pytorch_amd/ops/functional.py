@@ -215,34 +215,56 @@ def bn_act(x, bn, relu: bool = True):
 
 # ================================================================================ linear
 class _LinearAct(torch.autograd.Function):
+    """y = act(x W^T + b) over the layer's padded output width; returns the first
+    ``nout`` columns (a view) when the layer stores padded rows (layers.Linear)."""
+
     @staticmethod
-    def forward(ctx, x, w, b, relu):
+    def forward(ctx, x, w, b, relu, nout):
         k = K(x)
         y = k.linear_fwd(x, weight_of(w), _or_empty(b, x), relu)
         ctx.relu = relu
         ctx.params = (w, b)
+        ctx.nout = nout
         ctx.save_for_backward(x, y if relu else None)
-        return y
+        return y if nout == y.shape[1] else y[:, :nout]
 
     @staticmethod
     def backward(ctx, dy):
         x, y = ctx.saved_tensors
         w, b = ctx.params
         k = K(dy)
-        dy = dy.contiguous()
+        dy = _padded_grad(dy, w.shape[0])
         g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
         _done(b)
         if w.requires_grad:
             k.linear_wgrad(g, x, w.grad)
             _done(w)
         dx = k.linear_dgrad(g, weight_of(w)) if ctx.needs_input_grad[0] else None
-        return dx, None, None, None
+        return dx, None, None, None, None
+
+
+def _padded_grad(dy, width: int):
+    """Gradient of a padded layer's output view as a contiguous [B, width] tensor.  The
+    cross-entropy backward already returns a view of a [B, width] buffer with zero padding
+    columns - use that buffer (after re-zeroing the padding defensively); anything else
+    is zero-padded by a copy."""
+    if dy.shape[1] == width:
+        return dy.contiguous()
+    base = dy._base
+    if (base is not None and base.dim() == 2 and tuple(base.shape) == (dy.shape[0], width)
+            and base.is_contiguous() and dy.data_ptr() == base.data_ptr()
+            and dy.stride() == base.stride()):
+        base[:, dy.shape[1]:].zero_()
+        return base
+    return torch.nn.functional.pad(dy, (0, width - dy.shape[1])).contiguous()
 
 
 def linear_act(x, lin, relu: bool = False):
+    nout = getattr(lin, "out_features", lin.weight.shape[0])
     if torch.is_grad_enabled() and (lin.weight.requires_grad or x.requires_grad):
-        return _LinearAct.apply(x, lin.weight, lin.bias, relu)
-    return K(x).linear_fwd(x, weight_of(lin.weight), _or_empty(lin.bias, x), relu)
+        return _LinearAct.apply(x, lin.weight, lin.bias, relu, nout)
+    y = K(x).linear_fwd(x, weight_of(lin.weight), _or_empty(lin.bias, x), relu)
+    return y if nout == y.shape[1] else y[:, :nout]
 
 
 # ================================================================================= pools

@@ -334,6 +334,31 @@ def test_adaptive_avgpool(gpu, shape, out):
     assert rel(dx, ref.adaptive_avgpool_bwd(dy, shape[1], shape[2])) < 1e-2
 
 
+def test_cross_entropy_padded_rows(gpu):
+    """Classifier heads store 64,512 rows for 64,500 classes: CE / argmax read the padded
+    row stride, and the backward returns a view of a zero-padded buffer that the Linear
+    backward consumes in place (no pad copy)."""
+    from mpi_pytorch_amd.ops.functional import _padded_grad
+    torch.manual_seed(8)
+    B, NC, LD = 64, 64500, 64512
+    full = bf(B, LD, dev=gpu, scale=3.0)
+    logits = full[:, :NC]
+    labels = torch.randint(0, NC, (B,), device=gpu)
+    loss, lse = C().ce_fwd(logits, labels)
+    lr, lser = ref.ce_fwd(logits, labels)
+    assert rel(loss, lr) < 1e-3 and rel(lse, lser) < 1e-3
+    go = torch.ones(1, device=gpu)
+    d = C().ce_bwd(logits, labels, lse, go)
+    assert d.shape == (B, NC) and d.stride(0) == LD
+    assert rel(d, ref.ce_bwd(logits, labels, lser, go)) < 2e-2
+    base = _padded_grad(d, LD)
+    assert base.data_ptr() == d.data_ptr() and base.shape == (B, LD)  # no copy
+    assert float(base[:, NC:].float().abs().max()) == 0.0
+    cnt = torch.zeros(1, dtype=torch.long, device=gpu)
+    C().argmax_correct(logits, logits.float().argmax(1), cnt)
+    assert int(cnt) == B
+
+
 @pytest.mark.parametrize("B,NC", [(128, 64500), (7, 1000), (5, 33)])
 def test_cross_entropy(gpu, B, NC):
     logits = bf(B, NC, dev=gpu, scale=3.0)
