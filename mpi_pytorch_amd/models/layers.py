@@ -27,6 +27,11 @@ def _pair(v) -> Tuple[int, int]:
     return int(v), int(v)
 
 
+def _pad_rows(n: int) -> int:
+    """Stored output width of a padded classifier (Linear / head conv): a multiple of 32."""
+    return n if n % 32 == 0 else (n + 31) // 32 * 32
+
+
 def _krsc_to_oihw(t):
     return t.permute(0, 3, 1, 2)
 
@@ -46,11 +51,15 @@ class Conv2d(nn.Module):
     """
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size, stride=1, padding=0,
-                 bias: bool = True):
+                 bias: bool = True, pad_out: bool = False):
         super().__init__()
         self.in_channels = in_channels
         self.cin_store = 8 if in_channels < 8 else in_channels
         self.out_channels = out_channels
+        # pad_out: store the output channels rounded up to a multiple of 32 (zero filters) -
+        # for classifier convs (SqueezeNet's 512 -> 64,500 1x1 head) so their dgrad / wgrad
+        # stay on the 16-B LDS-DMA paths; the model slices the logits back
+        self.cout_store = _pad_rows(out_channels) if pad_out else out_channels
         self.kernel_size = _pair(kernel_size)
         self.stride = _pair(stride)
         self.padding = _pair(padding)
@@ -63,20 +72,34 @@ class Conv2d(nn.Module):
         if bias:
             fan_in = in_channels * kh * kw
             bound = 1 / math.sqrt(fan_in)
-            self.bias = nn.Parameter(torch.empty(out_channels).uniform_(-bound, bound))
+            b = torch.empty(out_channels).uniform_(-bound, bound)
+            self.bias = nn.Parameter(self._imp_bias(b))
+            if self.cout_store != out_channels:
+                self.bias._mpa_export = self._exp_bias
+                self.bias._mpa_import = self._imp_bias
         else:
             self.register_parameter("bias", None)
 
     def _exp(self, t):  # internal KRSC (maybe channel padded) -> OIHW
         if self.cin_store != self.in_channels:
             t = t[..., :self.in_channels]
+        if self.cout_store != self.out_channels:
+            t = t[:self.out_channels]
         return _krsc_to_oihw(t)
 
     def _imp(self, t):  # OIHW -> internal KRSC
         t = _oihw_to_krsc(t)
         if self.cin_store != self.in_channels:
             t = F.pad(t, (0, self.cin_store - self.in_channels))
+        if t.shape[0] < self.cout_store:
+            t = F.pad(t, (0, 0, 0, 0, 0, 0, 0, self.cout_store - t.shape[0]))
         return t
+
+    def _exp_bias(self, t):
+        return t[:self.out_channels]
+
+    def _imp_bias(self, t):
+        return F.pad(t, (0, self.cout_store - t.shape[0])) if t.shape[0] < self.cout_store else t
 
     # init helpers operate in OIHW space so the distributions match torchvision
     def init_(self, fn) -> "Conv2d":
@@ -92,6 +115,10 @@ class Conv2d(nn.Module):
         if k in destination:
             w = destination[k]
             destination[k] = self._exp(w) if keep_vars else self._exp(w).contiguous()
+        k = prefix + "bias"
+        if k in destination and destination[k] is not None and self.cout_store != self.out_channels:
+            b = self._exp_bias(destination[k])
+            destination[k] = b if keep_vars else b.contiguous()
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
@@ -100,6 +127,9 @@ class Conv2d(nn.Module):
             w = state_dict[k]
             if tuple(w.shape) == (self.out_channels, self.in_channels, *self.kernel_size):
                 state_dict[k] = self._imp(w)
+        k = prefix + "bias"
+        if k in state_dict and tuple(state_dict[k].shape) == (self.out_channels,):
+            state_dict[k] = self._imp_bias(state_dict[k])
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
@@ -155,11 +185,6 @@ class BatchNorm2d(nn.Module):
 
     def extra_repr(self):
         return "{}, eps={}, momentum={}".format(self.num_features, self.eps, self.momentum)
-
-
-def _pad_rows(n: int) -> int:
-    """Stored output width of a Linear: rounded up to a multiple of 32."""
-    return n if n % 32 == 0 else (n + 31) // 32 * 32
 
 
 class Linear(nn.Module):

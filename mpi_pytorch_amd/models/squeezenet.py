@@ -40,7 +40,7 @@ class SqueezeNet(nn.Module):
             Fire(256, 32, 128, 128), Fire(256, 48, 192, 192), Fire(384, 48, 192, 192),
             Fire(384, 64, 256, 256), MaxPool2d(3, 2, ceil_mode=True),
             Fire(512, 64, 256, 256))
-        final_conv = Conv2d(512, num_classes, 1)
+        final_conv = Conv2d(512, num_classes, 1, pad_out=True)
         self.classifier = FusedSequential(Dropout(dropout), final_conv, ReLU(True),
                                           AdaptiveAvgPool2d((1, 1)))
         for m in self.modules():
@@ -53,13 +53,14 @@ class SqueezeNet(nn.Module):
 
     def replace_head(self, num_classes: int) -> None:
         """``classifier[1] = Conv2d(512, nc, 1)``; ``num_classes = nc`` (models.py:70-71)."""
-        self.classifier[1] = Conv2d(512, num_classes, 1)
+        self.classifier[1] = Conv2d(512, num_classes, 1, pad_out=True)
         self.num_classes = num_classes
 
     def forward(self, x):
         x = self.features(x)
         x = self.classifier(x)
-        return x.reshape(x.shape[0], -1)
+        # the head conv stores its output channels padded to a multiple of 32
+        return x.reshape(x.shape[0], -1)[:, :self.num_classes]
 
 
 def squeezenet1_0(num_classes: int = 1000) -> SqueezeNet:

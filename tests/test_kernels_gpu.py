@@ -42,6 +42,7 @@ CONV_CASES = [
     (8, 56, 56, 64, 64, 3, 3, 1, 1),       # large pixel count: wgrad split slab path
     (2, 32, 32, 8, 64, 7, 7, 2, 3),        # padded stem (C=8: 16-B granular, DMA path)
     (4, 28, 28, 128, 128, 3, 3, 1, 1),     # 128x128 tile, several K-tiles
+    (8, 40, 40, 3, 5, 3, 3, 1, 1),         # split wgrad, Kout*R*S*C % 4 != 0 (scalar reduce)
 ]
 
 
