@@ -120,8 +120,10 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
   return y;
 }
 
+// wt (optional): the transposed weight [C][R*S][K] (arena shadow_t) - the dgrad GEMM then
+// reads B K-contiguous like the forward GEMM
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
-                  int64_t pw) {
+                  int64_t pw, c10::optional<Tensor> wt_opt) {
   CHECK_ACT(dy);
   CHECK_ACT(w);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -137,6 +139,13 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
   a.A = bp(dy); a.aH = P; a.aW = Q; a.aC = K;
   a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
   a.B = bp(w); a.N = C; a.RS = R * S; a.ldb = C;
+  const bool bkc = wt_opt && wt_opt->defined() && wt_opt->numel() == w.numel() && vw == 8;
+  if (bkc) {
+    CHECK_ACT((*wt_opt));
+    a.B = bp(*wt_opt);
+    a.ldb = R * S * K;
+    a.b_tapmap = 1;
+  }
   a.C = dx.data_ptr(); a.ldc = C;
   a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw;
   a.bias = nullptr; a.stats = nullptr; a.relu = 0;
@@ -164,7 +173,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
     a.M = d.M; a.oH = d.oH; a.oW = d.oW; a.T = d.T; a.Ktot = d.Ktot; a.Poh = 0; a.Pow = 0;
     Tensor ws;
     float* wsp = alloc_ws(ws, dy, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
-    mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream());
+    mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream(), bkc);
   } else {
     // phases with no taps (stride > kernel) leave their dx pixels zero
     bool empty = false;
@@ -174,7 +183,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
     for (int i = 0; i < nph; ++i)
       if (a.ph[i].T > 0) a.ph[k++] = a.ph[i];
     a.nphase = k;
-    mpa::igemm_rows_dgrad_phases(a, vw, cur_stream());
+    mpa::igemm_rows_dgrad_phases(a, vw, cur_stream(), bkc);
   }
   return dx;
 }
@@ -393,7 +402,7 @@ Tensor linear_fwd(Tensor x, Tensor w, Tensor bias, bool relu) {
   return y;
 }
 
-Tensor linear_dgrad(Tensor dy, Tensor w) {
+Tensor linear_dgrad(Tensor dy, Tensor w, c10::optional<Tensor> wt_opt) {
   CHECK_ACT(dy);
   CHECK_ACT(w);
   const int B = dy.size(0), Cout = dy.size(1), Cin = w.size(1);
@@ -407,11 +416,18 @@ Tensor linear_dgrad(Tensor dy, Tensor w) {
   a.T = 1; a.taps.dh[0] = 0; a.taps.dw[0] = 0; a.taps.bt[0] = 0;
   a.Ktot = Cout;
   a.B = bp(w); a.N = Cin; a.RS = 1; a.ldb = Cin;
+  const int vw = std::min(vec_width(Cout), vec_width(Cin));
+  const bool bkc = wt_opt && wt_opt->defined() && wt_opt->numel() == w.numel() && vw == 8;
+  if (bkc) {  // transposed weight [Cin][Cout]: B K-contiguous
+    CHECK_ACT((*wt_opt));
+    a.B = bp(*wt_opt);
+    a.ldb = Cout;
+  }
   a.C = dx.data_ptr(); a.ldc = Cin;
   a.dH = 1; a.dW = 1; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   Tensor ws;
   float* wsp = alloc_ws(ws, dy, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
-  mpa::igemm_rows_dgrad(a, std::min(vec_width(Cout), vec_width(Cin)), wsp, cur_stream());
+  mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream(), bkc);
   return dx;
 }
 
@@ -498,6 +514,17 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor shadow, Tensor step, double
                 momentum, dampening, wd, nesterov ? 1 : 0, gs, cur_stream());
 }
 
+void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles) {
+  CHECK_CUDA(w);
+  CHECK_CUDA(wt);
+  CHECK_CUDA(seg);
+  TORCH_CHECK(seg.scalar_type() == torch::kInt64 && seg.dim() == 2 && seg.size(1) == 6,
+              "transpose_krsc: seg [n][6] int64");
+  const c10::OptionalDeviceGuard g(device_of(w));
+  mpa::transpose_krsc(bp(w), bpm(wt), seg.contiguous().data_ptr<int64_t>(), (int)seg.size(0),
+                      (int)total_tiles, cur_stream());
+}
+
 void cast_f32_bf16(Tensor x, Tensor y) {
   CHECK_F32(x);
   CHECK_BF16(y);
@@ -550,7 +577,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_bwd", &act_bwd);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
@@ -566,7 +594,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adaptive_avgpool_fwd", &adaptive_avgpool_fwd);
   m.def("adaptive_avgpool_bwd", &adaptive_avgpool_bwd);
   m.def("linear_fwd", &linear_fwd);
-  m.def("linear_dgrad", &linear_dgrad);
+  m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt") = py::none());
   m.def("linear_wgrad", &linear_wgrad);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
@@ -574,6 +602,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_step", &adam_step);
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("transpose_krsc", &transpose_krsc);
   m.def("preprocess", &preprocess);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);

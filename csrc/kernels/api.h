@@ -53,6 +53,9 @@ struct IGemmArgs {
   Taps taps;
   int nphase;             // > 0: merged stride-phase dgrad launch (igemm_rows_dgrad_phases)
   PhaseDesc ph[MAXPH];
+  int b_tapmap;           // K-contiguous B whose rows are indexed by weight tap: B element of
+                          // GEMM k = (t, c) is B[n][taps.bt[t] * aC + c] (dgrad from the
+                          // transposed weight [C][RS][K]); 0: B[n][k]
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
 };
@@ -72,10 +75,12 @@ struct WGradArgs {
 // igemm.hip
 int64_t igemm_slab_floats(int M, int N);
 void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s);  // B K-contig
-void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s);  // B N-contiguous
+// dgrad GEMMs: B N-contiguous (the forward weight, read with transposing LDS loads) or,
+// with bkc, K-contiguous (the transposed weight copy; set a.b_tapmap)
+void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc = false);
 // all stride phases of a strided-conv dgrad (a.nphase, a.ph[], shared a.taps) in one launch
 // on the LDS-DMA engine when eligible, else one igemm_rows_dgrad per phase
-void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s);
+void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc = false);
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
@@ -143,6 +148,9 @@ void sgd_step(float* p, const float* g, float* buf, bf16_raw* shadow, const floa
               int64_t n, float lr, float momentum, float dampening, float wd, int nesterov,
               float grad_scale, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s);
+// wt[c][t][k] = w[k][t][c] per segment (src_off, dst_off, K, RS, C, first_tile) of seg
+void transpose_krsc(const bf16_raw* w, bf16_raw* wt, const int64_t* seg, int nseg,
+                    int total_tiles, hipStream_t s);
 
 // preprocess.hip
 struct Norm3 {

@@ -150,7 +150,12 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
                              e[6] | (e[7] << 16));
         } else {
           const bool ok = (row < BN) && (n < p.N);
-          rb[i] = ld_chunk<VW>(p.B + (size_t)n * p.ldb + kk, ok ? nvalid(kk, p.Ktot) : 0);
+          int kb = kk;
+          if (VW == 8 && p.b_tapmap && kk < p.Ktot) {  // weight-tap row map (dgrad, wT)
+            const int t = kk / p.aC;
+            kb = p.taps.bt[t] * p.aC + (kk - t * p.aC);
+          }
+          rb[i] = ld_chunk<VW>(p.B + (size_t)n * p.ldb + kb, ok ? nvalid(kk, p.Ktot) : 0);
         }
       }
     } else {
@@ -669,16 +674,16 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
   run_rows(a, true, vw, ws, slab, s);
 }
 
-void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s) {
+void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc) {
   a.stats = nullptr;
   a.nphase = 0;
-  run_rows(a, false, vw, ws, nullptr, s);
+  run_rows(a, bkc, vw, ws, nullptr, s);
 }
 
 // All stride phases in ONE launch on the LDS-DMA engine: a stride-2 conv's dgrad is 4
 // GEMMs of a quarter of the pixels each; launched separately each fills a fraction of the
 // 256 CUs (ResNet-18 layer4 at batch 256: 196 tiles per phase), merged they fill it.
-void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s) {
+void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
   a.stats = nullptr;
   a.bias = nullptr;
   if (a.nphase <= 0) return;
@@ -701,7 +706,7 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s) {
     const int tot = most * a.nphase;
     a.tiles_total = tot;
     a.ktiles_per_split = 1 << 30;
-    if (tot > 0 && igemm_rows_dma(a, BM, BN, false, 1, s)) return;
+    if (tot > 0 && igemm_rows_dma(a, BM, BN, bkc, 1, s)) return;
   }
   for (int i = 0; i < a.nphase; ++i) {  // one launch per phase
     const PhaseDesc& d = a.ph[i];
@@ -714,7 +719,7 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s) {
       b.taps.dw[t] = a.taps.dw[d.tap0 + t];
       b.taps.bt[t] = a.taps.bt[d.tap0 + t];
     }
-    run_rows(b, false, vw, nullptr, nullptr, s);
+    run_rows(b, bkc, vw, nullptr, nullptr, s);
   }
 }
 

@@ -180,7 +180,9 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
         if (jb < IB) {
           const int n = n0 + 16 * jb + (lane >> 2);
           const bool ok = kok & (n < p.N);
-          const bf16_t* src = ok ? p.B + (size_t)n * p.ldb + kk : zp;
+          // K index of the weight row: GEMM k, or (weight tap of a_t, channel a_c)
+          const int kb = p.b_tapmap ? tap_b[min(a_t, tlast)] * p.aC + a_c : kk;
+          const bf16_t* src = ok ? p.B + (size_t)n * p.ldb + kb : zp;
           glds16(src, bimg + jb * 1024);
         }
       }
@@ -727,11 +729,9 @@ static void launch_rows_dma_v(const IGemmArgs& a, dim3 grid, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, bool BKC>
 static void launch_rows_dma(const IGemmArgs& a, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
-  if constexpr (!BKC) {
-    if (a.nphase > 0) {  // merged stride phases (dgrad): never split
-      launch_rows_dma_v<BM, BN, WM, WN, BKC, false, true>(a, grid, s);
-      return;
-    }
+  if (a.nphase > 0) {  // merged stride phases (dgrad): never split
+    launch_rows_dma_v<BM, BN, WM, WN, BKC, false, true>(a, grid, s);
+    return;
   }
   if (splits > 1) launch_rows_dma_v<BM, BN, WM, WN, BKC, true, false>(a, grid, s);
   else launch_rows_dma_v<BM, BN, WM, WN, BKC, false, false>(a, grid, s);

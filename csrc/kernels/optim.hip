@@ -109,4 +109,48 @@ void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(cast_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, x, y, n4);
 }
 
+// ------------------------------------------------------------ transposed weight shadow
+// wt[c][t][k] = w[k][t][c] for every registered conv / linear weight, from the bf16 shadow
+// the optimizer just wrote: dgrad then reads its B operand K-contiguous, exactly like the
+// forward GEMM.  seg: [nseg][6] int64 = (src_off, dst_off, K, RS, C, first_tile); one
+// 64x64 (k, c) tile of one tap per block, tiles of all weights in one flat grid.
+__global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __restrict__ w,
+                                                              bf16_t* __restrict__ wt,
+                                                              const int64_t* __restrict__ seg,
+                                                              int nseg) {
+  __shared__ bf16_t tile[64][66];
+  const int b = blockIdx.x;
+  int lo = 0, hi = nseg - 1;  // last segment whose first_tile <= b (uniform)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg[mid * 6 + 5] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* d = seg + lo * 6;
+  const int64_t so = d[0], dof = d[1];
+  const int K = (int)d[2], RS = (int)d[3], C = (int)d[4];
+  const int tk = (K + 63) / 64, tc = (C + 63) / 64;
+  int r = b - (int)d[5];
+  const int t = r / (tk * tc);
+  r -= t * tk * tc;
+  const int k0 = (r / tc) * 64, c0 = (r % tc) * 64;
+  const int row = threadIdx.x >> 2, q = (threadIdx.x & 3) * 16;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = k0 + row, c = c0 + q + j;
+    tile[row][q + j] = (k < K && c < C) ? w[so + ((size_t)k * RS + t) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = c0 + row, k = k0 + q + j;
+    if (c < C && k < K) wt[dof + ((size_t)c * RS + t) * K + k] = tile[q + j][row];
+  }
+}
+
+void transpose_krsc(const bf16_raw* w, bf16_raw* wt, const int64_t* seg, int nseg,
+                    int total_tiles, hipStream_t s) {
+  if (nseg <= 0 || total_tiles <= 0) return;
+  hipLaunchKernelGGL(transpose_krsc_kernel, dim3(total_tiles), dim3(256), 0, s, w, wt, seg, nseg);
+}
+
 }  // namespace mpa

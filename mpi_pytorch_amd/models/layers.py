@@ -69,6 +69,8 @@ class Conv2d(nn.Module):
         self.weight = nn.Parameter(self._imp(w).contiguous())
         self.weight._mpa_export = self._exp
         self.weight._mpa_import = self._imp
+        # (K, R*S, C) of the stored KRSC weight: the arena keeps a [C][R*S][K] copy for dgrad
+        self.weight._mpa_tlayout = (self.cout_store, kh * kw, self.cin_store)
         if bias:
             fan_in = in_channels * kh * kw
             bound = 1 / math.sqrt(fan_in)
@@ -213,6 +215,7 @@ class Linear(nn.Module):
         if in_chw is not None or self.out_store != out_features:
             self.weight._mpa_export = self._exp
             self.weight._mpa_import = self._imp
+        self.weight._mpa_tlayout = (self.out_store, 1, in_features)  # [in][out] copy for dgrad
         if bias:
             bound = 1 / math.sqrt(in_features)
             b = torch.empty(out_features).uniform_(-bound, bound)

@@ -28,7 +28,7 @@ import torch
 
 from . import ref
 from . import _ext
-from ..parallel.arena import weight_of, grad_sink, grad_done
+from ..parallel.arena import weight_of, weight_t_of, grad_sink, grad_done
 
 _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
@@ -110,7 +110,8 @@ class _ConvBNAct(torch.autograd.Function):
         _done(ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw)
+            dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
+                               weight_t_of(w))
         dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
         return dx, dres, None, None, None, None, None, None, None
 
@@ -167,7 +168,8 @@ class _ConvAct(torch.autograd.Function):
             _done(w)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k.conv_dgrad(g, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw)
+            dx = k.conv_dgrad(g, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
+                               weight_t_of(w))
         return dx, None, None, None, None
 
 
@@ -239,7 +241,8 @@ class _LinearAct(torch.autograd.Function):
         if w.requires_grad:
             k.linear_wgrad(g, x, w.grad)
             _done(w)
-        dx = k.linear_dgrad(g, weight_of(w)) if ctx.needs_input_grad[0] else None
+        dx = (k.linear_dgrad(g, weight_of(w), weight_t_of(w)) if ctx.needs_input_grad[0]
+              else None)
         return dx, None, None, None, None
 
 

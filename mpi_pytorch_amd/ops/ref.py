@@ -62,7 +62,7 @@ def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None):
     return y
 
 
-def conv_dgrad(dy, w, H, W, sh, sw, ph, pw):
+def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None):  # wt: transposed copy (unused here)
     N, P, Q, K = dy.shape
     Kw, R, S, C = w.shape
     gi = torch.ops.aten.convolution_backward(
@@ -211,7 +211,7 @@ def linear_fwd(x, w, bias, relu):
     return y.to(x.dtype)
 
 
-def linear_dgrad(dy, w):
+def linear_dgrad(dy, w, wt=None):
     return (_f(dy) @ _f(w)).to(dy.dtype)
 
 

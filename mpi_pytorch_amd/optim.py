@@ -124,6 +124,7 @@ class FusedAdam(_FlatOptimizer):
                                  float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                                  float(g["weight_decay"]), float(self.grad_scale))
         self.step_t.add_(1.0)
+        self.arena.refresh_transposed()
 
     def _param_state(self, p, o, e, step):
         return {"step": torch.tensor(step),
@@ -163,6 +164,7 @@ class FusedSGD(_FlatOptimizer):
                                 float(g["weight_decay"]), bool(g["nesterov"]),
                                 float(self.grad_scale))
         self.step_t.add_(1.0)
+        self.arena.refresh_transposed()
 
     def _param_state(self, p, o, e, step):
         return {"momentum_buffer":

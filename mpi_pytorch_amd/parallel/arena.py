@@ -81,7 +81,42 @@ class ParamArena:
                     p.grad = self.grad[o:o + p.numel()].view_as(p)
                 p._mpa_arena = self
         self._listeners: List[Callable[[nn.Parameter], None]] = []
+        self._init_transposed()
         self.sync_shadow()
+
+    def _init_transposed(self) -> None:
+        """Transposed bf16 weight shadow for dgrad: a conv weight stored KRSC is also kept
+        as [C][R*S][K] (``p._mpa_shadow_t``), so the dgrad GEMM reads its B operand
+        K-contiguous like the forward GEMM instead of through transposing LDS reads.  One
+        batched transpose launch refreshes every such weight after the optimizer step."""
+        self.shadow_t = None
+        self._tseg = None
+        self._ttiles = 0
+        if self.shadow is None:
+            return
+        rows, off, tiles = [], 0, 0
+        tp = [p for p in self.params if getattr(p, "_mpa_tlayout", None) is not None]
+        for p in tp:
+            K, RS, C = p._mpa_tlayout
+            if K * RS * C != p.numel() or K % 8 or C % 8:
+                continue
+            rows.append((p, [self.offsets[id(p)], off, K, RS, C, tiles]))
+            tiles += RS * ((K + 63) // 64) * ((C + 63) // 64)
+            off += _align(p.numel())
+        if not rows:
+            return
+        self.shadow_t = torch.zeros(off, dtype=torch.bfloat16, device=self.device)
+        for p, r in rows:
+            K, RS, C = p._mpa_tlayout
+            p._mpa_shadow_t = self.shadow_t[r[1]:r[1] + p.numel()].view(C, RS, K)
+        self._tseg = torch.tensor([r for _, r in rows], dtype=torch.int64, device=self.device)
+        self._ttiles = tiles
+
+    def refresh_transposed(self) -> None:
+        """Re-derive the transposed shadow from the bf16 shadow (after each update)."""
+        if self._tseg is not None:
+            from ..ops import _ext
+            _ext.ext().transpose_krsc(self.shadow, self.shadow_t, self._tseg, self._ttiles)
 
     # ------------------------------------------------------------------------------
     def slice_of(self, p: nn.Parameter):
@@ -93,6 +128,7 @@ class ParamArena:
         if self.shadow is not None:
             with torch.no_grad():
                 self.shadow.copy_(self.master)
+            self.refresh_transposed()
 
     def zero_grad(self) -> None:
         self.grad.zero_()
@@ -115,6 +151,11 @@ def weight_of(p: nn.Parameter) -> torch.Tensor:
     """The tensor a compute kernel should read for parameter ``p`` (bf16 on GPU)."""
     s = getattr(p, "_mpa_shadow", None)
     return s if s is not None else p
+
+
+def weight_t_of(p: nn.Parameter) -> Optional[torch.Tensor]:
+    """The [C][R*S][K] transposed bf16 shadow of a conv/linear weight, or None."""
+    return getattr(p, "_mpa_shadow_t", None)
 
 
 def grad_sink(p: nn.Parameter) -> Optional[torch.Tensor]:

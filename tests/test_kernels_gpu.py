@@ -97,6 +97,51 @@ def test_conv_dgrad(gpu, engine, case):
     assert rel(dx, dxr) < 2e-2
 
 
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0])
+def test_conv_dgrad_transposed_weight(gpu, engine, case):
+    """dgrad from the transposed weight copy [C][R*S][K] (K-contiguous B, weight-tap row
+    map) feeds the MFMAs the same fragments in the same K order as the N-contiguous path:
+    bitwise equal, on every engine and stride-phase layout."""
+    torch.manual_seed(1)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * K))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, R * S, K).contiguous()
+    dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
+    dxt = C().conv_dgrad(dy, w, H, W, st, st, ph, pw, wt)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dxt), rel(dxt, dx)
+
+
+def test_transpose_krsc_and_linear_dgrad_transposed(gpu):
+    torch.manual_seed(9)
+    shapes = [(64, 9, 8), (200, 1, 512), (136, 9, 264), (64512, 1, 512)]
+    ws = [bf(K, RS, Cc, dev=gpu) for K, RS, Cc in shapes]
+    src = torch.cat([w.reshape(-1) for w in ws])
+    dst = torch.zeros_like(src)
+    rows, off, tiles = [], 0, 0
+    for (K, RS, Cc), w in zip(shapes, ws):
+        rows.append([off, off, K, RS, Cc, tiles])
+        tiles += RS * ((K + 63) // 64) * ((Cc + 63) // 64)
+        off += w.numel()
+    C().transpose_krsc(src, dst, torch.tensor(rows, device=gpu), tiles)
+    off = 0
+    for (K, RS, Cc), w in zip(shapes, ws):
+        got = dst[off:off + w.numel()].view(Cc, RS, K)
+        assert torch.equal(got, w.permute(2, 1, 0)), (K, RS, Cc)
+        off += w.numel()
+    # linear dgrad through the transposed weight [in][out]
+    B, Cin, Cout = 32, 512, 64512
+    w = bf(Cout, Cin, dev=gpu, scale=1.0 / math.sqrt(Cout))
+    dy = bf(B, Cout, dev=gpu)
+    a = C().linear_dgrad(dy, w)
+    b = C().linear_dgrad(dy, w, w.t().contiguous())
+    assert rel(b, ref.linear_dgrad(dy, w)) < 2e-2 and rel(a, b) < 1e-2
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_wgrad(gpu, engine, case):
     torch.manual_seed(2)
