@@ -30,7 +30,7 @@ for step in "$@"; do
     diag2) run diag2 600 python tools/diag_grads.py twice; rc=$? ;;
     traj) run traj 600 python tools/diag_traj.py 64 25 && MPA_NO_STATS_SHIFT=1 timeout -k 10 600 python tools/diag_traj.py 64 25 > gpurun_out/traj_noshift.log 2>&1; rc=$? ;;
     train) run train 600 python main.py --synthetic_images 2048 --image_size 224 --NUM_EPOCHS 2 --BATCH_SIZE 256 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/training.log; rc=$? ;;
-    evalp) run evalp 600 python evaluation_pipeline.py --synthetic_images 1024 --image_size 224 --eval_lanes 3 --eval_batch 128 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/evaluation.log; rc=$? ;;
+    evalp) run evalp 600 python evaluation_pipeline.py --synthetic_images 16384 --image_size 224 --eval_lanes 3 --eval_batch 256 --CHECKPOINT_DIR /tmp/mpa_ck/ --log_file gpurun_out/evaluation.log; rc=$? ;;
     *) echo "unknown step $step"; rc=0 ;;
   esac
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $step rc=$rc"; exit $rc; fi

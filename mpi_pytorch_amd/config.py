@@ -122,7 +122,9 @@ class Config:
                            help="(default: {})".format(f.default))
 
     @classmethod
-    def from_args(cls, argv: Optional[List[str]] = None, **overrides) -> "Config":
+    def from_args(cls, argv: Optional[List[str]] = None, **defaults) -> "Config":
+        """Config from command-line flags; ``defaults`` are entry-point defaults (e.g.
+        ``log_file="evaluation.log"``) that explicit flags override."""
         p = argparse.ArgumentParser(add_help=True)
         cls.add_arguments(p)
         ns, _unknown = p.parse_known_args(argv)
@@ -131,7 +133,8 @@ class Config:
         for k, v in vars(ns).items():
             if v is not None:
                 kw[k] = _coerce(types[k], v)
-        kw.update(overrides)
+        for k, v in defaults.items():
+            kw.setdefault(k, v)
         return cls.from_env(**kw)
 
 

@@ -78,11 +78,35 @@ class StreamPipeline:
         self.counts = [torch.zeros(1, dtype=torch.int64, device=self.device)
                        for _ in range(self.lanes)]
         self.seen = [0] * self.lanes
+        self._pinned = {}
+        self._last_slot = None
 
     def _lane_for(self, i: int) -> int:
         if self.assign == "roundrobin":
             return i % self.lanes
         return int(self.rng.integers(0, self.lanes))
+
+    def _staging(self, g: torch.Tensor) -> torch.Tensor:
+        """Copy a host batch into a reusable pinned buffer (a ring of ``depth + 2``
+        slots; a slot is reused only after the copy that read it has completed)."""
+        key = (tuple(g.shape), g.dtype)
+        ring = self._pinned.setdefault(key, [])
+        for slot in ring:
+            if slot[1] is None or slot[1].query():
+                buf = slot[0]
+                break
+        else:
+            if len(ring) >= self.depth + 2:
+                ring[0][1].synchronize()
+                buf = ring[0][0]
+                slot = ring[0]
+            else:
+                buf = torch.empty(g.shape, dtype=g.dtype).pin_memory()
+                slot = [buf, None]
+                ring.append(slot)
+        buf.copy_(g)
+        self._last_slot = slot
+        return buf
 
     def _preprocess(self, imgs):
         if isinstance(imgs, np.ndarray):
@@ -92,9 +116,12 @@ class StreamPipeline:
         outs = []
         for g in groups:
             if self.cuda:
-                g = g.pin_memory()
+                g = self._staging(g)
                 with torch.cuda.stream(self.copy_stream):
                     gd = g.to(self.device, non_blocking=True)
+                    copied = torch.cuda.Event()
+                    copied.record(self.copy_stream)
+                self._last_slot[1] = copied  # pinned slot free once this copy is done
                 self.prep_stream.wait_stream(self.copy_stream)
                 with torch.cuda.stream(self.prep_stream):
                     gd.record_stream(self.prep_stream)

@@ -33,6 +33,9 @@ def test_config_fields_and_overrides(monkeypatch):
     assert c.CHECKPOINT_NAME == "checkpoint_resnet34.pt"
     with pytest.raises(ValueError):
         Config(MODEL_NAME="lenet")
+    # entry-point defaults (evaluation_pipeline.py: log_file) yield to explicit flags
+    assert Config.from_args([], log_file="evaluation.log").log_file == "evaluation.log"
+    assert Config.from_args(["--log_file", "x.log"], log_file="evaluation.log").log_file == "x.log"
 
 
 def test_utils_shim():

@@ -57,8 +57,10 @@ def tensors(H, Ci, Co, R, st, pd):
     e = torch.empty(0, device=dev)
     stats = torch.empty(2, Co, device=dev)
     flop = 2.0 * B * P * P * Co * R * R * Ci
+    # dgrad as training runs it: from the transposed weight copy [C][R*S][K] (arena shadow_t)
+    wt = w.permute(3, 1, 2, 0).reshape(Ci, R * R, Co).contiguous() if Ci % 8 == 0 else None
     fns = (lambda: C.conv_fwd(x, w, e, st, st, pd, pd, False, stats, e),
-           lambda: C.conv_dgrad(dy, w, H, H, st, st, pd, pd),
+           lambda: C.conv_dgrad(dy, w, H, H, st, st, pd, pd, wt),
            lambda: C.conv_wgrad(dy, x, dw, st, st, pd, pd))
     return flop, fns
 
