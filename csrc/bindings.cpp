@@ -121,9 +121,16 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
 }
 
 // wt (optional): the transposed weight [C][R*S][K] (arena shadow_t) - the dgrad GEMM then
-// reads B K-contiguous like the forward GEMM
-Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
-                  int64_t pw, c10::optional<Tensor> wt_opt) {
+// reads B K-contiguous like the forward GEMM.  bnred (optional): fuse the backward
+// reduction of the ReLU(BN) that produced this conv's input (see igemm_rows_dgrad_bnred);
+// then dx = g (masked) and bnred->sums receives [sum g | sum g*xhat].
+struct BnRed {
+  Tensor z, y, mean, rstd, sums;
+};
+
+static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw,
+                              int64_t ph, int64_t pw, c10::optional<Tensor> wt_opt,
+                              BnRed* bnred) {
   CHECK_ACT(dy);
   CHECK_ACT(w);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -168,6 +175,33 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
       TORCH_CHECK(nph < mpa::MAXPH, "conv_dgrad: too many stride phases");
       a.ph[nph++] = mpa::PhaseDesc{N * Hp * Wp, Hp, Wp, (T - t0) * K, t0, T - t0, a_, b_, 0};
     }
+  if (bnred) {
+    a.ep_z = bp(bnred->z);
+    a.ep_y = bopt(bnred->y);
+    a.ep_mean = fopt(bnred->mean);
+    a.ep_rstd = fopt(bnred->rstd);
+    bnred->sums = torch::empty({2 * C}, dy.options().dtype(torch::kFloat32));
+    int k = 0;
+    bool empty = false;
+    for (int i = 0; i < nph; ++i) {
+      empty |= a.ph[i].T == 0;
+      if (a.ph[i].T > 0) a.ph[k++] = a.ph[i];
+    }
+    if (empty) dx.zero_();
+    if (sh == 1 && sw == 1) {
+      const mpa::PhaseDesc& d = a.ph[0];
+      a.M = d.M; a.oH = d.oH; a.oW = d.oW; a.T = d.T; a.Ktot = d.Ktot; a.Poh = 0; a.Pow = 0;
+      a.nphase = 0;
+    } else {
+      a.nphase = k;
+    }
+    TORCH_CHECK(!empty, "conv_dgrad_bnred: stride-phase without taps");
+    Tensor slab = torch::empty({mpa::igemm_bnred_slab_floats(N * H * W, C, std::max(a.nphase, 1))},
+                               dy.options().dtype(torch::kFloat32));
+    mpa::igemm_rows_dgrad_bnred(a, vw, bkc, slab.data_ptr<float>(),
+                                bnred->sums.data_ptr<float>(), cur_stream());
+    return dx;
+  }
   if (sh == 1 && sw == 1) {
     const mpa::PhaseDesc& d = a.ph[0];
     a.M = d.M; a.oH = d.oH; a.oW = d.oW; a.T = d.T; a.Ktot = d.Ktot; a.Poh = 0; a.Pow = 0;
@@ -186,6 +220,46 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
     mpa::igemm_rows_dgrad_phases(a, vw, cur_stream(), bkc);
   }
   return dx;
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
+                  int64_t pw, c10::optional<Tensor> wt_opt) {
+  return conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt_opt, nullptr);
+}
+
+// fused-reduction dgrad available: LDS-DMA engine, 16-B granular dy (K) and dx (C), and
+// the transposed weight (K-contiguous B)
+bool conv_bnred_ok(int64_t K, int64_t C) {
+  return mpa::igemm_engine() >= 1 && vec_width(K) == 8 && vec_width(C) == 8 && C % 8 == 0;
+}
+
+std::vector<Tensor> conv_dgrad_bnred(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh,
+                                     int64_t sw, int64_t ph, int64_t pw, Tensor wt, Tensor z,
+                                     Tensor y, Tensor mean, Tensor rstd) {
+  CHECK_ACT(z);
+  TORCH_CHECK(conv_bnred_ok(w.size(0), w.size(3)), "conv_dgrad_bnred: unsupported shape/engine");
+  TORCH_CHECK(wt.defined() && wt.numel() == w.numel(), "conv_dgrad_bnred: needs the transposed weight");
+  BnRed r{z, y, mean, rstd, Tensor()};
+  Tensor dx = conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt, &r);
+  TORCH_CHECK(z.sizes() == dx.sizes(), "conv_dgrad_bnred: z must have dx's shape");
+  return {dx, r.sums};
+}
+
+std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd,
+                                 Tensor gamma, Tensor dgamma, Tensor dbeta, Tensor sums,
+                                 bool want_dx, bool want_g) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && sums.numel() == 2 * C, "bn_bwd_apply: shapes");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
+  Tensor gout = want_g ? torch::empty_like(x) : Tensor();
+  mpa::bn_bwd_apply(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma),
+                    fopt_mut(dgamma), fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr,
+                    want_g ? bpm(gout) : nullptr, fopt(sums), cur_stream());
+  return {dx, gout};
 }
 
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
@@ -580,6 +654,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_bnred_ok", &conv_bnred_ok);
+  m.def("conv_dgrad_bnred", &conv_dgrad_bnred);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("act_bwd", &act_bwd);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),

@@ -56,6 +56,15 @@ struct IGemmArgs {
   int b_tapmap;           // K-contiguous B whose rows are indexed by weight tap: B element of
                           // GEMM k = (t, c) is B[n][taps.bt[t] * aC + c] (dgrad from the
                           // transposed weight [C][RS][K]); 0: B[n][k]
+  // fused BN-backward reduction (dgrad epilogue, ep_bnred = 1): the GEMM output v is the
+  // gradient dy of a ReLU(BN(z)) whose z / y / mean / rstd are given (same layout as C);
+  // the epilogue writes g = dy * (y > 0) and slab-reduces (sum g, sum g * (z - mean) * rstd)
+  // per column into `stats` exactly like the forward statistics (row `stat` of the slab)
+  int ep_bnred;
+  const bf16_raw* ep_z;
+  const bf16_raw* ep_y;
+  const float* ep_mean;
+  const float* ep_rstd;
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
 };
@@ -81,6 +90,11 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc = 
 // all stride phases of a strided-conv dgrad (a.nphase, a.ph[], shared a.taps) in one launch
 // on the LDS-DMA engine when eligible, else one igemm_rows_dgrad per phase
 void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc = false);
+// dgrad with the fused BN-backward reduction (a.ep_* set): sums[2][N] receives
+// (sum g, sum g * xhat); slab holds igemm_bnred_slab_floats(a) floats
+int64_t igemm_bnred_slab_floats(int M, int N, int nphase);
+void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* sums,
+                            hipStream_t s);
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
@@ -109,6 +123,9 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s);
+void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
+                  const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
+                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
              float* ws, hipStream_t s);
 void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s);

@@ -536,6 +536,15 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
                      gamma, ws, dgamma, dbeta, M, C, dx, g);
 }
 
+// apply pass only, with the reduction sums [sum g | sum g*xhat] already in `sums` (e.g.
+// from the fused dgrad epilogue, igemm_rows_dgrad_bnred)
+void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
+                  const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
+                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s) {
+  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, sums, dgamma,
+            dbeta, M, C, dx, g);
+}
+
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
              float* ws, hipStream_t s) {
   if (C % 8 == 0) {

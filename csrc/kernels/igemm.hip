@@ -680,6 +680,57 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc) {
   run_rows(a, bkc, vw, ws, nullptr, s);
 }
 
+// dgrad + fused BN-backward reduction (LDS-DMA engine only: one launch, dense slab rows)
+int64_t igemm_bnred_slab_floats(int M, int N, int nphase) {
+  const int64_t rows = (int64_t)((M + 127) / 128 + 1) * std::max(nphase, 1);
+  return rows * 2 * N;
+}
+
+// tile plan of a merged stride-phase launch; returns the number of (phase, m-tile) rows
+static int plan_phases(IGemmArgs& a, int& BM, int& BN) {
+  IGemmArgs probe = a;
+  probe.M = 0;
+  probe.Ktot = 0;
+  for (int i = 0; i < a.nphase; ++i) {
+    probe.M = std::max(probe.M, a.ph[i].M);
+    probe.Ktot = std::max(probe.Ktot, a.ph[i].Ktot);
+  }
+  int splits;
+  rows_plan(probe, BM, BN, splits, false, true);
+  a.tiles_n = (a.N + BN - 1) / BN;
+  int most = 0, rows = 0;
+  for (int i = 0; i < a.nphase; ++i) {
+    const int mts = (a.ph[i].M + BM - 1) / BM;
+    a.ph[i].tiles = mts * a.tiles_n;
+    most = std::max(most, a.ph[i].tiles);
+    rows += mts;
+  }
+  a.tiles_total = most * a.nphase;
+  a.ktiles_per_split = 1 << 30;
+  return rows;
+}
+
+void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* sums,
+                            hipStream_t s) {
+  (void)vw;  // callers guarantee 16-B granular operands (LDS-DMA engine)
+  a.bias = nullptr;
+  a.relu = 0;
+  a.stats_shift = nullptr;
+  a.ep_bnred = 1;
+  a.stats = slab;
+  a.stats_sums = sums;
+  int BM, BN, rows;
+  if (a.nphase > 0) {
+    rows = plan_phases(a, BM, BN);
+  } else {
+    int splits;
+    rows_plan(a, BM, BN, splits, false, true);
+    rows = (a.M + BM - 1) / BM;
+  }
+  igemm_rows_dma(a, BM, BN, bkc, 1, s);
+  slab_reduce(slab, rows, 2 * a.N, sums, false, s);
+}
+
 // All stride phases in ONE launch on the LDS-DMA engine: a stride-2 conv's dgrad is 4
 // GEMMs of a quarter of the pixels each; launched separately each fills a fraction of the
 // 256 CUs (ResNet-18 layer4 at batch 256: 196 tiles per phase), merged they fill it.
@@ -688,25 +739,9 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
   a.bias = nullptr;
   if (a.nphase <= 0) return;
   if (use_dma(vw) && a.nphase <= MAXPH) {
-    IGemmArgs probe = a;
-    probe.M = 0;
-    probe.Ktot = 0;
-    for (int i = 0; i < a.nphase; ++i) {
-      probe.M = std::max(probe.M, a.ph[i].M);
-      probe.Ktot = std::max(probe.Ktot, a.ph[i].Ktot);
-    }
-    int BM, BN, splits;
-    rows_plan(probe, BM, BN, splits, false, true);
-    a.tiles_n = (a.N + BN - 1) / BN;
-    int most = 0;
-    for (int i = 0; i < a.nphase; ++i) {
-      a.ph[i].tiles = ((a.ph[i].M + BM - 1) / BM) * a.tiles_n;
-      most = std::max(most, a.ph[i].tiles);
-    }
-    const int tot = most * a.nphase;
-    a.tiles_total = tot;
-    a.ktiles_per_split = 1 << 30;
-    if (tot > 0 && igemm_rows_dma(a, BM, BN, bkc, 1, s)) return;
+    int BM, BN;
+    plan_phases(a, BM, BN);
+    if (a.tiles_total > 0 && igemm_rows_dma(a, BM, BN, bkc, 1, s)) return;
   }
   for (int i = 0; i < a.nphase; ++i) {  // one launch per phase
     const PhaseDesc& d = a.ph[i];

@@ -107,7 +107,9 @@ template <int BM, int BN, int WM, int WN, bool SPLIT>
 __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                               char* smem, int mt, int m0, int n0, int wm,
-                                              int wrow0, int wcol0, int tid, const RowsGeom& g) {
+                                              int wrow0, int wcol0, int tid, const RowsGeom& g,
+                                              int stat_row = -1) {
+  if (stat_row < 0) stat_row = mt;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
   const int lane = tid & 63;
@@ -137,19 +139,23 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
+    // bias / stats shift; in BN-reduce mode the same registers carry mean / rstd
     f32x4 bias[TN], shift[TN];
+    const bool bnred = p.ep_bnred != 0;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       shift[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int n = n0 + wcol0 + j * 16 + nl;
-      if (p.bias) {
+      const float* bsrc = bnred ? p.ep_mean : p.bias;
+      const float* ssrc = bnred ? p.ep_rstd : p.stats_shift;
+      if (bsrc) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? p.bias[n + r] : 0.f;
+        for (int r = 0; r < 4; ++r) bias[j][r] = (n + r < p.N) ? bsrc[n + r] : 0.f;
       }
-      if (p.stats_shift) {
+      if (ssrc) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? p.stats_shift[n + r] : 0.f;
+        for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? ssrc[n + r] : 0.f;
       }
     }
 #pragma unroll
@@ -170,11 +176,42 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wcol0 + j * 16 + nl;
         float v[4];
+        float zr[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bnred) {
+          // dy (bf16-rounded like the unfused path) masked by ReLU(y); x_hat from z
+          bool live[4] = {true, true, true, true};
+          if (mok && n + 3 < p.N) {
+            const uint2 zz = *(const uint2*)(p.ep_z + orow + n);
+            zr[0] = bf2f(zz.x & 0xffff); zr[1] = bf2f(zz.x >> 16);
+            zr[2] = bf2f(zz.y & 0xffff); zr[3] = bf2f(zz.y >> 16);
+            if (p.ep_y) {
+              const uint2 yy = *(const uint2*)(p.ep_y + orow + n);
+              live[0] = (yy.x & 0x7fff) != 0 && !(yy.x & 0x8000);
+              live[1] = ((yy.x >> 16) & 0x7fff) != 0 && !(yy.x & 0x80000000u);
+              live[2] = (yy.y & 0x7fff) != 0 && !(yy.y & 0x8000);
+              live[3] = ((yy.y >> 16) & 0x7fff) != 0 && !(yy.y & 0x80000000u);
+            }
+          } else if (mok) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = acc[i][j][r] + bias[j][r];
-          if (p.relu) t = fmaxf(t, 0.f);
-          v[r] = t;
+            for (int r = 0; r < 4; ++r) {
+              if (n + r < p.N) {
+                zr[r] = bf2f(p.ep_z[orow + n + r]);
+                if (p.ep_y) live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = bf2f(f2bf(acc[i][j][r]));
+            v[r] = live[r] ? d : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = acc[i][j][r] + bias[j][r];
+            if (p.relu) t = fmaxf(t, 0.f);
+            v[r] = t;
+          }
         }
         const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
         if (mok) {
@@ -187,14 +224,23 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
             for (int r = 0; r < 4; ++r)
               if (n + r < p.N) out[orow + n + r] = e[r];
           }
-          // statistics on the bf16-rounded values BN will read, shifted by K ~ mean
-          // (BN running mean) so the sum of squares does not cancel when |mean| >> std
-          const float rv[4] = {bf2f(lo & 0xffff) - shift[j][0], bf2f(lo >> 16) - shift[j][1],
-                               bf2f(hi & 0xffff) - shift[j][2], bf2f(hi >> 16) - shift[j][3]};
+          if (bnred) {
+            // (sum g, sum g * (z - mean) * rstd) - BN backward's reduction
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[j][r] += rv[r];
-            q[j][r] += rv[r] * rv[r];
+            for (int r = 0; r < 4; ++r) {
+              s[j][r] += v[r];
+              q[j][r] += v[r] * (zr[r] - bias[j][r]) * shift[j][r];
+            }
+          } else {
+            // statistics on the bf16-rounded values BN will read, shifted by K ~ mean
+            // (BN running mean) so the sum of squares does not cancel when |mean| >> std
+            const float rv[4] = {bf2f(lo & 0xffff) - shift[j][0], bf2f(lo >> 16) - shift[j][1],
+                                 bf2f(hi & 0xffff) - shift[j][2], bf2f(hi >> 16) - shift[j][3]};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s[j][r] += rv[r];
+              q[j][r] += rv[r] * rv[r];
+            }
           }
         }
       }
@@ -226,7 +272,7 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
         }
       }
       __syncthreads();
-      if (mt == 0 && blockIdx.z == 0 && tid < BN && n0 + tid < p.N) {
+      if (stat_row == 0 && blockIdx.z == 0 && tid < BN && n0 + tid < p.N) {
         // start value of the slab reduction that runs after this kernel (no memset)
         p.stats_sums[n0 + tid] = 0.f;
         p.stats_sums[p.N + n0 + tid] = 0.f;
@@ -238,8 +284,8 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
           a += red[(w * BN + tid) * 2];
           b += red[(w * BN + tid) * 2 + 1];
         }
-        p.stats[(size_t)mt * 2 * p.N + n0 + tid] = a;
-        p.stats[(size_t)mt * 2 * p.N + p.N + n0 + tid] = b;
+        p.stats[(size_t)stat_row * 2 * p.N + n0 + tid] = a;
+        p.stats[(size_t)stat_row * 2 * p.N + p.N + n0 + tid] = b;
       }
     }
   }

@@ -91,11 +91,13 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
   // merged stride-phase launch: the block's phase sets output geometry, K and taps
   RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
+  int row_base = 0;  // statistics-slab row of m-tile 0 of this block's phase (dense rows)
   if constexpr (PH) {
     const int ph = tile % p.nphase;
     tile /= p.nphase;
     const PhaseDesc& d = p.ph[ph];
     if (tile >= d.tiles) return;  // padding tile of a shorter phase (whole block)
+    for (int q = 0; q < ph; ++q) row_base += p.ph[q].tiles / p.tiles_n;
     g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow};
     Ktot = d.Ktot;
     T = d.T;
@@ -240,7 +242,8 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
     }
   }
   __syncthreads();  // every DMA waited (vmcnt(0) on the last step); LDS free for the epilogue
-  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid, g);
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid, g,
+                                       row_base + mt);
 }
 
 // ======================================================================================
@@ -283,11 +286,13 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   int tile = xcd_remap(blockIdx.x, p.tiles_total);
   RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
+  int row_base = 0;  // statistics-slab row of m-tile 0 of this block's phase (dense rows)
   if constexpr (PH) {
     const int ph = tile % p.nphase;
     tile /= p.nphase;
     const PhaseDesc& d = p.ph[ph];
     if (tile >= d.tiles) return;
+    for (int q = 0; q < ph; ++q) row_base += p.ph[q].tiles / p.tiles_n;
     g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow};
     Ktot = d.Ktot;
     T = d.T;
@@ -419,7 +424,8 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     if (kt < kend) step(std::integral_constant<int, 1>{});
   }
   __syncthreads();
-  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid, g);
+  rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid, g,
+                                       row_base + mt);
 }
 
 // ======================================================================================

@@ -118,7 +118,9 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __res
                                                               bf16_t* __restrict__ wt,
                                                               const int64_t* __restrict__ seg,
                                                               int nseg) {
-  __shared__ bf16_t tile[64][66];
+  // 64 (k) x 64 (c) tile; rows padded to 72 elements so the column gathers of the store
+  // phase spread over banks
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
   const int b = blockIdx.x;
   int lo = 0, hi = nseg - 1;  // last segment whose first_tile <= b (uniform)
   while (lo < hi) {
@@ -127,23 +129,36 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __res
   }
   const int64_t* d = seg + lo * 6;
   const int64_t so = d[0], dof = d[1];
-  const int K = (int)d[2], RS = (int)d[3], C = (int)d[4];
+  const int K = (int)d[2], RS = (int)d[3], C = (int)d[4];  // K % 8 == 0, C % 8 == 0
   const int tk = (K + 63) / 64, tc = (C + 63) / 64;
   int r = b - (int)d[5];
   const int t = r / (tk * tc);
   r -= t * tk * tc;
   const int k0 = (r / tc) * 64, c0 = (r % tc) * 64;
-  const int row = threadIdx.x >> 2, q = (threadIdx.x & 3) * 16;
+  // load: 512 16-B chunks (64 k-rows x 8 c-chunks), 2 per thread
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int k = k0 + row, c = c0 + q + j;
-    tile[row][q + j] = (k < K && c < C) ? w[so + ((size_t)k * RS + t) * C + c] : (bf16_t)0;
+  for (int h = 0; h < 2; ++h) {
+    const int q = threadIdx.x + 256 * h;
+    const int row = q >> 3, cc = (q & 7) * 8;
+    const int k = k0 + row, c = c0 + cc;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k < K && c < C) v = *(const uint4*)(w + so + ((size_t)k * RS + t) * C + c);
+    *(uint4*)&tile[row][cc] = v;
   }
   __syncthreads();
+  // store: 512 16-B chunks (64 c-rows x 8 k-chunks), each gathered from a tile column
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int c = c0 + row, k = k0 + q + j;
-    if (c < C && k < K) wt[dof + ((size_t)c * RS + t) * K + k] = tile[q + j][row];
+  for (int h = 0; h < 2; ++h) {
+    const int q = threadIdx.x + 256 * h;
+    const int crow = q >> 3, kk = (q & 7) * 8;
+    const int c = c0 + crow, k = k0 + kk;
+    if (c < C && k < K) {
+      uint32_t e[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        e[u] = (uint32_t)tile[kk + 2 * u][crow] | ((uint32_t)tile[kk + 2 * u + 1][crow] << 16);
+      *(uint4*)(wt + dof + ((size_t)c * RS + t) * K + k) = make_uint4(e[0], e[1], e[2], e[3]);
+    }
   }
 }
 

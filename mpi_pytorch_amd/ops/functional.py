@@ -68,9 +68,22 @@ def _done(*ps) -> None:
 
 
 # =============================================================================== conv+BN
+class BNLink:
+    """Backward hand-off between two fused conv+BN ops when the first op's output feeds ONLY
+    the second (ResNet BasicBlock: conv1 -> bn1 -> relu -> conv2).  The consumer's dgrad
+    epilogue then performs the producer's BN-backward reduction - it applies the ReLU
+    mask and sums (g, g * x_hat) while the gradient is still in registers - and the
+    producer's backward runs only the BN apply pass (no reduce pass, no re-read of dy/y)."""
+
+    __slots__ = ("z", "y", "mean", "rstd", "sums")
+
+    def __init__(self):
+        self.z = self.y = self.mean = self.rstd = self.sums = None
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu):
+    def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None):
         k = K(x)
         sh, sw = conv.stride
         ph, pw = conv.padding
@@ -89,6 +102,11 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.params = (w, gamma, beta)
         ctx.in_hw = (x.shape[1], x.shape[2])
         ctx.save_for_backward(x, z, y if relu else None, mean, rstd)
+        ctx.link_in = link_in
+        ctx.link_out = link_out
+        if link_out is not None:
+            link_out.z, link_out.y, link_out.mean, link_out.rstd = z, (y if relu else None), mean, rstd
+            link_out.sums = None
         return y
 
     @staticmethod
@@ -99,8 +117,15 @@ class _ConvBNAct(torch.autograd.Function):
         k = K(dy)
         dy = dy.contiguous()
         want_g = bool(ctx.has_res and ctx.needs_input_grad[1])
-        dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
-                         _sink(beta, dy), True, want_g)
+        lo = ctx.link_out
+        if lo is not None and lo.sums is not None:
+            # the consumer's dgrad already masked dy and reduced (sum g, sum g*xhat)
+            dz, g = k.bn_bwd_apply(dy, z, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
+                                   _sink(beta, dy), lo.sums, True, want_g)
+            lo.sums = None
+        else:
+            dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
+                             _sink(beta, dy), True, want_g)
         _done(gamma, beta)
         sh, sw = conv.stride
         ph, pw = conv.padding
@@ -110,13 +135,22 @@ class _ConvBNAct(torch.autograd.Function):
         _done(ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
-                               weight_t_of(w))
+            li = ctx.link_in
+            wt = weight_t_of(w)
+            if (li is not None and li.z is not None and (wt is not None or not dz.is_cuda)
+                    and k.conv_bnred_ok(w.shape[0], w.shape[3])):
+                dx, li.sums = k.conv_dgrad_bnred(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1],
+                                                 sh, sw, ph, pw, wt, li.z,
+                                                 _or_empty(li.y, dz), li.mean, li.rstd)
+            else:
+                dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
+                                   wt)
         dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
-        return dx, dres, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None
 
 
-def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None):
+def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None,
+                link_in: Optional[BNLink] = None, link_out: Optional[BNLink] = None):
     """relu(bn(conv(x)) [+ residual]); BN in train or eval mode per ``bn.training``.
 
     A conv bias in front of a train-mode BN (VGG11_bn) is added before the statistics, so
@@ -126,7 +160,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
     x = conv.fit_input(x)
     if bn.training:
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
-                                bn, relu)
+                                bn, relu, link_in, link_out)
     k = K(x)
     sh, sw = conv.stride
     ph, pw = conv.padding

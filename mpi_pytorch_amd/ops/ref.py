@@ -148,6 +148,42 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True):
     return dx, g.reshape(x.shape).to(dy.dtype)
 
 
+def bn_bwd_apply(dy, x, y, mean, rstd, gamma, dgamma, dbeta, sums, want_dx, want_g=True):
+    """bn_bwd's apply pass with precomputed sums = [sum g | sum g*xhat]."""
+    C = x.shape[-1]
+    g = _f(dy).reshape(-1, C)
+    if _opt(y) is not None:
+        g = g * (_f(y).reshape(-1, C) > 0)
+    M = g.shape[0]
+    xhat = (_f(x).reshape(-1, C) - mean) * rstd
+    sg, sgx = sums[:C], sums[C:]
+    if _opt(dgamma) is not None:
+        dgamma.add_(sgx)
+    if _opt(dbeta) is not None:
+        dbeta.add_(sg)
+    dx = None
+    if want_dx:
+        dx = ((gamma * rstd) * (g - sg / M - xhat * (sgx / M))).reshape(x.shape).to(dy.dtype)
+    return dx, g.reshape(x.shape).to(dy.dtype)
+
+
+def conv_bnred_ok(K, C):
+    return True
+
+
+def conv_dgrad_bnred(dy, w, H, W, sh, sw, ph, pw, wt, z, y, mean, rstd):
+    """dgrad fused with the backward reduction of the ReLU(BN) that produced the conv
+    input: returns (g = dx * (y > 0), [sum g | sum g * xhat])."""
+    dx = conv_dgrad(dy, w, H, W, sh, sw, ph, pw)
+    C = dx.shape[-1]
+    g = _f(dx).reshape(-1, C)
+    if _opt(y) is not None:
+        g = g * (_f(y).reshape(-1, C) > 0)
+    xhat = (_f(z).reshape(-1, C) - mean) * rstd
+    sums = torch.cat([g.sum(0), (g * xhat).sum(0)])
+    return g.reshape(dx.shape).to(dx.dtype), sums
+
+
 # ---------------------------------------------------------------------------------- pool
 def _pool_out(H, k, s, p, ceil):
     if ceil:

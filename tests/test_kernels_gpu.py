@@ -116,6 +116,40 @@ def test_conv_dgrad_transposed_weight(gpu, engine, case):
     assert torch.equal(dx, dxt), rel(dxt, dx)
 
 
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 3, 1, 1), (2, 14, 14, 64, 128, 3, 3, 2, 1),
+                                  (4, 28, 28, 128, 128, 3, 3, 1, 1), (3, 9, 11, 96, 48, 3, 3, 1, 1)])
+def test_conv_dgrad_fused_bn_reduction(gpu, case):
+    """dgrad whose epilogue applies the producer's ReLU mask and reduces (sum g,
+    sum g*xhat) == unfused dgrad + oracle reduction; apply pass with the sums == bn_bwd."""
+    torch.manual_seed(11)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * K))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, R * S, K).contiguous()
+    z = bf(N, H, W, Cc, dev=gpu, scale=2.0)
+    mean = torch.randn(Cc, device=gpu) * 0.3
+    rstd = torch.rand(Cc, device=gpu) + 0.5
+    y = torch.relu(z.float() - 0.2).to(torch.bfloat16)  # a ReLU output: mask source
+    assert C().conv_bnred_ok(K, Cc)
+    g, sums = C().conv_dgrad_bnred(dy, w, H, W, st, st, ph, pw, wt, z, y, mean, rstd)
+    dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw, wt)
+    gr, sr = ref.conv_dgrad_bnred(dy, w, H, W, st, st, ph, pw, None, z, y, mean, rstd)
+    torch.cuda.synchronize()
+    # (the unfused dgrad may split K where the fused one does not: compare with tolerance)
+    assert rel(g, (dx.float() * (y.float() > 0)).to(torch.bfloat16)) < 1e-2
+    assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+    gamma = torch.rand(Cc, device=gpu) + 0.5
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    e = torch.empty(0, device=gpu)
+    dz, _ = C().bn_bwd_apply(g, z, e, mean, rstd, gamma, dg, db, sums, True, False)
+    dzr, _ = ref.bn_bwd(dx, z, y, mean, rstd, gamma, dg2, db2, True)
+    assert rel(dz, dzr) < 3e-2 and rel(dg, dg2) < 2e-2 and rel(db, db2) < 2e-2
+
+
 def test_transpose_krsc_and_linear_dgrad_transposed(gpu):
     torch.manual_seed(9)
     shapes = [(64, 9, 8), (200, 1, 512), (136, 9, 264), (64512, 1, 512)]
