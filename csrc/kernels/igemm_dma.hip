@@ -749,6 +749,7 @@ static bool rows_dma_tile(const IGemmArgs& a, int BM, int BN, int splits, hipStr
   else if (BM == 256 && BN == 128) launch_rows_dma<256, 128, 4, 2, BKC>(a, splits, s);
   else if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, BKC>(a, splits, s);
   else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, BKC>(a, splits, s);
+  else if (BM == 128 && BN == 64) launch_rows_dma<128, 64, 2, 2, BKC>(a, splits, s);
   else if (BM == 128 && BN == 32) launch_rows_dma<128, 32, 4, 1, BKC>(a, splits, s);
   else return false;
   return true;

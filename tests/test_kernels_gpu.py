@@ -230,6 +230,9 @@ def test_engines_bitwise_equal(gpu, case):
                 # 8-channel stem on the super-tap path: K is grouped by 4 kernel columns
                 # (zero-padded), a different fp32 summation order than (r, s, c) tiles
                 assert rel(a, b) < 1e-2, (key, nm, rel(a, b))
+            elif nm == "stats":
+                # per-tile partial sums: the engines may pick different tile heights
+                assert rel(a, b) < 1e-5, (key, nm, rel(a, b))
             else:
                 assert torch.equal(a, b), (key, nm, rel(a, b))
 

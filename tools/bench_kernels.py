@@ -31,7 +31,7 @@ SHAPES = [  # name, H, Cin, Cout, R, stride, pad
     ("l4.3x3s2", 14, 256, 512, 3, 2, 1),
     ("l4.3x3", 7, 512, 512, 3, 1, 1),
 ]
-ROWS_TILES = [(0, 0), (256, 256), (256, 128), (128, 128), (256, 64)]
+ROWS_TILES = [(0, 0), (256, 128), (128, 128), (256, 64), (128, 64)]
 WGRAD_TILES = [(0, 0), (256, 256), (128, 256), (128, 128), (64, 128)]
 
 
