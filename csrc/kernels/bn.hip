@@ -497,6 +497,352 @@ void stats_finalize(const float* sums, const float* shift, int M, int C, float* 
                      M, C, out);
 }
 
+// ----------------------------------------------- BN + ReLU + max-pool (network stems)
+// conv -> BN -> ReLU -> max-pool (ResNet / DenseNet stems) as ONE pass over z: the BN
+// output (411 MB for ResNet at batch 256) is never materialised.  Forward writes the pooled
+// output and the window argmax; backward gathers the pooled gradient through the argmax
+// and recomputes the ReLU mask from z (bn(z) > 0), so neither pass reads or writes the
+// full-size activation gradient either.
+struct PoolGeom {
+  int N, H, W, P, Q, kh, kw, sh, sw, ph, pw;
+};
+
+__device__ __forceinline__ void bn_coeffs(const float* __restrict__ mean,
+                                          const float* __restrict__ rstd,
+                                          const float* __restrict__ gamma,
+                                          const float* __restrict__ beta, int c0, float* sc,
+                                          float* sh) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = gamma[c0 + j] * rstd[c0 + j];
+    sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
+  }
+}
+
+template <bool K3S2>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
+    const bf16_t* __restrict__ z, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, int C, PoolGeom g, bf16_t* __restrict__ y,
+    uint8_t* __restrict__ idx, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    unsigned long long* __restrict__ counter) {
+  if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  const int M = g.N * g.H * g.W;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float mu = stats[c0 + j], var = stats[C + c0 + j];
+    const float rs = rsqrtf(var + eps);
+    sc[j] = gamma[c0 + j] * rs;
+    sh[j] = beta[c0 + j] - mu * sc[j];
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+      mean_out[c0 + j] = mu;
+      rstd_out[c0 + j] = rs;
+      const float unb = var * ((float)M / (float)max(M - 1, 1));
+      rmean[c0 + j] = (1.f - momentum) * rmean[c0 + j] + momentum * mu;
+      rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
+    }
+  }
+  const int MP = g.N * g.P * g.Q;
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
+    const int q = r % g.Q;
+    const int t = r / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    if constexpr (K3S2) {
+      // 3x3 / stride 2 / pad 1: all nine loads issued before any is consumed (out-of-range
+      // taps read a clamped in-range pixel and are masked)
+      const int h0 = 2 * p - 1, w0 = 2 * q - 1;
+      uint4 v9[9];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int h = min(max(h0 + i, 0), g.H - 1), w = min(max(w0 + k, 0), g.W - 1);
+          v9[i * 3 + k] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
+        }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const bool ok = (unsigned)(h0 + i) < (unsigned)g.H && (unsigned)(w0 + k) < (unsigned)g.W;
+          float f[8];
+          unpack8(v9[i * 3 + k], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+            if (ok && v > best[j]) { best[j] = v; bi[j] = i * 3 + k; }
+          }
+        }
+    } else {
+      const int h0 = p * g.sh - g.ph, w0 = q * g.sw - g.pw;
+      for (int i = 0; i < g.kh; ++i) {
+        const int h = h0 + i;
+        if ((unsigned)h >= (unsigned)g.H) continue;
+        for (int k = 0; k < g.kw; ++k) {
+          const int w = w0 + k;
+          if ((unsigned)w >= (unsigned)g.W) continue;
+          float f[8];
+          unpack8(*(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+            if (v > best[j]) { best[j] = v; bi[j] = i * g.kw + k; }
+          }
+        }
+      }
+    }
+    const size_t o = (size_t)r * C + c0;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 ib;
+    ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + o) = ib;
+  }
+}
+
+// gradient at input pixel (n, h, w): pooled gradients whose argmax is this pixel, times
+// the ReLU mask bn(z) > 0; also returns z
+__device__ __forceinline__ void pool_bn_grad(const bf16_t* __restrict__ dp,
+                                             const uint8_t* __restrict__ idx,
+                                             const bf16_t* __restrict__ z, int C, int c0,
+                                             const PoolGeom& g, int r, const float* sc,
+                                             const float* sh, float* gr, float* zr) {
+  const int w = r % g.W;
+  const int t = r / g.W;
+  const int h = t % g.H;
+  const int n = t / g.H;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gr[j] = 0.f;
+  const int plo = max(0, (h + g.ph - g.kh + g.sh) / g.sh), phi = min(g.P - 1, (h + g.ph) / g.sh);
+  const int qlo = max(0, (w + g.pw - g.kw + g.sw) / g.sw), qhi = min(g.Q - 1, (w + g.pw) / g.sw);
+  for (int p = plo; p <= phi; ++p) {
+    const int i = h - (p * g.sh - g.ph);
+    if (i < 0 || i >= g.kh) continue;
+    for (int q = qlo; q <= qhi; ++q) {
+      const int k = w - (q * g.sw - g.pw);
+      if (k < 0 || k >= g.kw) continue;
+      const size_t o = (((size_t)n * g.P + p) * g.Q + q) * C + c0;
+      const uint2 ib = *(const uint2*)(idx + o);
+      const int me = i * g.kw + k;
+      float d[8];
+      unpack8(*(const uint4*)(dp + o), d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t word = j < 4 ? ib.x : ib.y;
+        if ((int)((word >> (8 * (j & 3))) & 0xff) == me) gr[j] += d[j];
+      }
+    }
+  }
+  unpack8(*(const uint4*)(z + (size_t)r * C + c0), zr);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gr[j] = (zr[j] * sc[j] + sh[j] > 0.f) ? gr[j] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int C, PoolGeom g,
+    float* __restrict__ slab, float* __restrict__ sums) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sums[c0 + j] = 0.f; sums[C + c0 + j] = 0.f; }
+    }
+    float sc[8], sh[8], mu[8], rs[8];
+    bn_coeffs(mean, rstd, gamma, beta, c0, sc, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+    const int M = g.N * g.H * g.W;
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+      float gr[8], zr[8];
+      pool_bn_grad(dp, idx, z, C, c0, g, r, sc, sh, gr, zr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] += gr[j];
+        sgx[j] += gr[j] * (zr[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  block_reduce8(sg, cm, red);
+  block_reduce8(sgx, cm, red);
+  if (cm.active && cm.r0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      slab[(size_t)blockIdx.x * 2 * C + cm.cc * 8 + j] = sg[j];
+      slab[(size_t)blockIdx.x * 2 * C + C + cm.cc * 8 + j] = sgx[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
+    PoolGeom g, bf16_t* __restrict__ dz) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  const int M = g.N * g.H * g.W;
+  float sc[8], sh[8], a[8], b[8], cco[8];
+  bn_coeffs(mean, rstd, gamma, beta, c0, sc, sh);
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sgv = sums[c0 + j], sgx = sums[C + c0 + j];
+    const float rs = rstd[c0 + j];
+    a[j] = sc[j];
+    cco[j] = -sc[j] * rs * sgx * invM;
+    b[j] = -sc[j] * sgv * invM - cco[j] * mean[c0 + j];
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+      if (dgamma) dgamma[c0 + j] += sgx;
+      if (dbeta) dbeta[c0 + j] += sgv;
+    }
+  }
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+    float gr[8], zr[8];
+    pool_bn_grad(dp, idx, z, C, c0, g, r, sc, sh, gr, zr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zr[j] = a[j] * gr[j] + b[j] + cco[j] * zr[j];
+    *(uint4*)(dz + (size_t)r * C + c0) = pack8(zr);
+  }
+}
+
+// 3x3 / stride 2 / pad 1 pool over an even H x W (H == 2P, W == 2Q): thread = one 2x2 input
+// cell (2p..2p+1, 2q..2q+1) x 8 channels.  Row 2p is covered only by window row p (tap 1),
+// row 2p+1 by window p (tap 2) and p+1 (tap 0); same for columns.  So the cell needs the
+// four pooled positions (p|p+1, q|q+1), and every load is independent.
+// APPLY = false: reduce (sum g, sum g*xhat) into the slab; true: write dz.
+template <bool APPLY>
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
+    const bf16_t* __restrict__ dp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ sums, float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
+    PoolGeom g, float* __restrict__ slab, float* __restrict__ zsums, bf16_t* __restrict__ dz) {
+  __shared__ float red[APPLY ? 1 : 256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    float sc[8], sh[8], mu[8], rs[8], a[8], b[8], cco[8];
+    bn_coeffs(mean, rstd, gamma, beta, c0, sc, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+    if constexpr (APPLY) {
+      const float invM = 1.f / (float)(g.N * g.H * g.W);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sgv = sums[c0 + j], sgxv = sums[C + c0 + j];
+        a[j] = sc[j];
+        cco[j] = -sc[j] * rs[j] * sgxv * invM;
+        b[j] = -sc[j] * sgv * invM - cco[j] * mu[j];
+        if (blockIdx.x == 0 && cm.r0 == 0) {
+          if (dgamma) dgamma[c0 + j] += sgxv;
+          if (dbeta) dbeta[c0 + j] += sgv;
+        }
+      }
+    } else if (blockIdx.x == 0 && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { zsums[c0 + j] = 0.f; zsums[C + c0 + j] = 0.f; }
+    }
+    const int cells = g.N * g.P * g.Q;
+#pragma unroll 1
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < cells; r += gridDim.x * cm.rpi) {
+      const int q = r % g.Q;
+      const int t = r / g.Q;
+      const int p = t % g.P;
+      const int n = t / g.P;
+      const bool pn = p + 1 < g.P, qn = q + 1 < g.Q;
+      // pooled neighbours (dp, idx): [0]=(p,q) [1]=(p,q+1) [2]=(p+1,q) [3]=(p+1,q+1)
+      uint4 dv[4];
+      uint2 iv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pp = p + (u >> 1), qq = q + (u & 1);
+        const bool ok = (!(u >> 1) || pn) && (!(u & 1) || qn);
+        const size_t o = (((size_t)n * g.P + (ok ? pp : p)) * g.Q + (ok ? qq : q)) * C + c0;
+        dv[u] = *(const uint4*)(dp + o);
+        iv[u] = *(const uint2*)(idx + o);
+        if (!ok) { dv[u] = make_uint4(0, 0, 0, 0); iv[u] = make_uint2(~0u, ~0u); }
+      }
+      uint4 zv[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int h = 2 * p + (v >> 1), w = 2 * q + (v & 1);
+        zv[v] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
+      }
+      float d[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) unpack8(dv[u], d[u]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int a0 = v >> 1, b0 = v & 1;  // input pixel (2p+a0, 2q+b0)
+        float zr[8], gr[8];
+        unpack8(zv[v], zr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float acc = 0.f;
+          // covering windows: rows {p: tap 1+a0} (+ {p+1: tap 0} if a0), cols likewise
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int du = u >> 1, eu = u & 1;
+            if ((du && !a0) || (eu && !b0)) continue;
+            const int ti = du ? 0 : 1 + a0, tk = eu ? 0 : 1 + b0;
+            const uint32_t word = j < 4 ? iv[u].x : iv[u].y;
+            if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[u][j];
+          }
+          gr[j] = (zr[j] * sc[j] + sh[j] > 0.f) ? acc : 0.f;
+        }
+        if constexpr (APPLY) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) zr[j] = a[j] * gr[j] + b[j] + cco[j] * zr[j];
+          const int h = 2 * p + a0, w = 2 * q + b0;
+          *(uint4*)(dz + (((size_t)n * g.H + h) * g.W + w) * C + c0) = pack8(zr);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sg[j] += gr[j];
+            sgx[j] += gr[j] * (zr[j] - mu[j]) * rs[j];
+          }
+        }
+      }
+    }
+  }
+  if constexpr (!APPLY) {
+    block_reduce8(sg, cm, red);
+    block_reduce8(sgx, cm, red);
+    if (cm.active && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        slab[(size_t)blockIdx.x * 2 * C + cm.cc * 8 + j] = sg[j];
+        slab[(size_t)blockIdx.x * 2 * C + C + cm.cc * 8 + j] = sgx[j];
+      }
+    }
+  }
+}
+
+static bool pool_k3s2p1_even(const PoolGeom& g) {
+  return g.kh == 3 && g.kw == 3 && g.sh == 2 && g.sw == 2 && g.ph == 1 && g.pw == 1 &&
+         g.H == 2 * g.P && g.W == 2 * g.Q;
+}
+
 // ------------------------------------------------------------------------ launchers
 void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,
               hipStream_t s) {
@@ -561,6 +907,60 @@ void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s) {
   const int64_t n8 = n / 8;
   const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
   hipLaunchKernelGGL(relu_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, s, x, n8, y);
+}
+
+// grid targets of the fused stem kernels (forward, backward reduce, backward apply); the
+// gathers are latency-bound, so they want more waves in flight than the streaming passes
+static int stem_grid(int which) {
+  static const int v[3] = {
+      [] { const char* e = getenv("MPA_STEM_GRID_F"); return e ? atoi(e) : 1024; }(),
+      [] { const char* e = getenv("MPA_STEM_GRID_R"); return e ? atoi(e) : 1024; }(),
+      [] { const char* e = getenv("MPA_STEM_GRID_A"); return e ? atoi(e) : 4096; }()};
+  return std::max(64, v[which]);
+}
+
+void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gamma,
+                         const float* beta, float* rmean, float* rvar, float momentum, float eps,
+                         int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
+                         int ph, int pw, bf16_raw* y, uint8_t* idx, float* mean, float* rstd,
+                         int64_t* counter, hipStream_t s) {
+  const PoolGeom g{N, H, W, P, Q, kh, kw, sh, sw, ph, pw};
+  const bool k3 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1;
+  hipLaunchKernelGGL(k3 ? bn_relu_maxpool_fwd_kernel<true> : bn_relu_maxpool_fwd_kernel<false>,
+                     grid_for(N * P * Q, C, stem_grid(0)), dim3(256), 0, s, z, stats, gamma, beta,
+                     rmean, rvar, momentum, eps, C, g, y, idx, mean, rstd,
+                     (unsigned long long*)counter);
+}
+
+int64_t maxpool_bn_ws_floats(int M, int C) {
+  return (int64_t)grid_for(M, C, stem_grid(1)).x * 2 * C + 2 * C;
+}
+
+void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,
+                    const float* rstd, const float* gamma, const float* beta, float* dgamma,
+                    float* dbeta, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh,
+                    int sw, int ph, int pw, bf16_raw* dz, float* ws, hipStream_t s) {
+  // ws layout: [2C] final sums | [gx][2C] per-block partials (as bn_bwd)
+  const PoolGeom g{N, H, W, P, Q, kh, kw, sh, sw, ph, pw};
+  const int M = N * H * W;
+  float* slab = ws + 2 * C;
+  if (pool_k3s2p1_even(g)) {
+    const int cells = N * P * Q;
+    const dim3 gr = grid_for(cells, C, stem_grid(1));
+    hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<false>, gr, dim3(256), 0, s, dp, idx, z, mean,
+                       rstd, gamma, beta, nullptr, nullptr, nullptr, C, g, slab, ws, nullptr);
+    slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+    hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<true>, grid_for(cells, C, stem_grid(2)),
+                       dim3(256), 0, s, dp, idx, z, mean, rstd, gamma, beta, ws, dgamma, dbeta, C,
+                       g, nullptr, nullptr, dz);
+    return;
+  }
+  const dim3 gr = grid_for(M, C, stem_grid(1));
+  hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, gr, dim3(256), 0, s, dp, idx, z, mean, rstd,
+                     gamma, beta, C, g, slab, ws);
+  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+  hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, grid_for(M, C, stem_grid(2)), dim3(256), 0, s, dp, idx, z,
+                     mean, rstd, gamma, beta, ws, dgamma, dbeta, C, g, dz);
 }
 
 }  // namespace mpa

@@ -25,6 +25,8 @@ for step in "$@"; do
     profinc) run profinc 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profinc -o inc --output-format csv -- python bench.py --model inception --image-size 299 --batch 128 --steps 3 --warmup 2; rc=$? ;;
     zoo2) for m in "squeezenet 224 256" "inception 299 128"; do set -- $m; timeout -k 10 300 python bench.py --model $1 --image-size $2 --batch $3 --steps 10 --warmup 3 >> gpurun_out/zoo2.log 2>&1 || { echo "zoo $1 failed rc=$?"; exit 1; }; done; rc=0 ;;
     linkab) MPA_BN_LINK=0 run link0 300 python bench.py --steps 20 --warmup 5 && MPA_BN_LINK=1 run link1 300 python bench.py --steps 20 --warmup 5 && MPA_BN_LINK=0 run link0b 300 python bench.py --steps 20 --warmup 5 && MPA_BN_LINK=1 run link1b 300 python bench.py --steps 20 --warmup 5; rc=$? ;;
+    stemab) MPA_NO_STEM_FUSE=1 run stem0 300 python bench.py --steps 20 --warmup 5 && run stem1 300 python bench.py --steps 20 --warmup 5 && MPA_NO_STEM_FUSE=1 run stem0b 300 python bench.py --steps 20 --warmup 5 && run stem1b 300 python bench.py --steps 20 --warmup 5; rc=$? ;;
+    stemgrid) for f in 1024 4096; do for r in 512 1024 2048; do for a in 1024 4096; do echo "F=$f R=$r A=$a" >> gpurun_out/stemgrid.log; MPA_STEM_GRID_F=$f MPA_STEM_GRID_R=$r MPA_STEM_GRID_A=$a timeout -k 10 120 python bench.py --steps 20 --warmup 5 >> gpurun_out/stemgrid.log 2>&1 || exit 1; done; done; done; rc=0 ;;
     diag) run diag 600 python tools/diag_grads.py; rc=$? ;;
     benchbn) for g in 0 256 512 1024; do for u in 1; do MPA_BN_GRID=$g MPA_BN_UNR=$u timeout -k 10 120 python tools/bench_bn.py 20 >> gpurun_out/benchbn.log 2>&1 || exit 1; done; done; rc=0 ;;
     diageng) run diageng 600 python tools/diag_engines.py inception 299 4; rc=$? ;;

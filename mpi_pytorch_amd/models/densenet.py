@@ -87,8 +87,7 @@ class DenseNet(nn.Module):
 
     def forward(self, x):
         f = self.features
-        x = Fn.conv_bn_act(x, f.conv0, f.norm0, relu=True)
-        x = f.pool0(x)
+        x = Fn.conv_bn_relu_maxpool(x, f.conv0, f.norm0, f.pool0)
         for name, m in f.named_children():
             if name.startswith("denseblock") or name.startswith("transition"):
                 x = m(x)

@@ -80,8 +80,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        x = self.maxpool(x)
+        x = Fn.conv_bn_relu_maxpool(x, self.conv1, self.bn1, self.maxpool)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 x = blk(x)

@@ -32,6 +32,7 @@ from ..parallel.arena import weight_of, weight_t_of, grad_sink, grad_done
 
 _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
+_NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
 
 
 def K(t: torch.Tensor):
@@ -168,6 +169,66 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
                    _empty(x), _empty(x))
     return k.bn_fwd_eval(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
                          _or_empty(residual, x), relu)
+
+
+class _ConvBNReLUPool(torch.autograd.Function):
+    """maxpool(relu(bn(conv(x)))) -- the ResNet / DenseNet stem -- with BN, ReLU and the
+    pool fused into one pass over the conv output z (forward) and the pool's gradient
+    gathered straight into the BN backward (backward): the full-size BN output and its
+    gradient never exist.  Reference: torchvision stems reached from ``models.py:24-30``
+    (resnet) and ``models.py:74-80`` (densenet)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, conv, bn, cfg):
+        k = K(x)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        C = w.shape[0]
+        stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
+        z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
+                       _empty(x) if _NO_SHIFT else bn.running_mean)
+        y, idx, mean, rstd = k.bn_relu_maxpool_fwd(z, stats, gamma, beta, bn.running_mean,
+                                                   bn.running_var, bn.momentum_value(), bn.eps,
+                                                   *cfg, bn.num_batches_tracked)
+        ctx.conv = conv
+        ctx.cfg = cfg
+        ctx.bias = b
+        ctx.params = (w, gamma, beta)
+        ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, z, idx, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, idx, mean, rstd = ctx.saved_tensors
+        w, gamma, beta = ctx.params
+        conv = ctx.conv
+        k = K(dy)
+        dz = k.maxpool_bn_bwd(dy.contiguous(), idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
+                              _sink(beta, dy), *ctx.cfg[:6])
+        _done(gamma, beta)
+        sh, sw = conv.stride
+        ph, pw = conv.padding
+        if w.requires_grad:
+            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            _done(w)
+        _done(ctx.bias)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
+                              weight_t_of(w))
+        return dx, None, None, None, None, None, None, None
+
+
+def conv_bn_relu_maxpool(x, conv, bn, pool):
+    """``pool(relu(bn(conv(x))))`` for a MaxPool2d ``pool``; fused in train mode."""
+    cfg = (pool.kernel_size[0], pool.kernel_size[1], pool.stride[0], pool.stride[1],
+           pool.padding[0], pool.padding[1], bool(pool.ceil_mode))
+    if bn.training and not _NO_STEM_FUSE and cfg[0] * cfg[1] <= 256:
+        x = conv.fit_input(x)
+        return _ConvBNReLUPool.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, conv, bn,
+                                     cfg)
+    return pool(conv_bn_act(x, conv, bn, relu=True))
 
 
 # ============================================================================ conv + bias

@@ -208,6 +208,23 @@ def maxpool_bwd(dy, idx, H, W, kh, kw, sh, sw, ph, pw, ceil):
     return _nhwc(out.reshape(N, C, H, W)).to(dy.dtype)
 
 
+def bn_relu_maxpool_fwd(z, stats, gamma, beta, rmean, rvar, momentum, eps, kh, kw, sh, sw, ph,
+                        pw, ceil, counter=None):
+    y, mean, rstd = bn_fwd_train(z, stats, gamma, beta, rmean, rvar, momentum, eps, None, True,
+                                 counter)
+    p, idx = maxpool_fwd(y, kh, kw, sh, sw, ph, pw, ceil)
+    return p, idx, mean, rstd
+
+
+def maxpool_bn_bwd(dp, idx, z, mean, rstd, gamma, beta, dgamma, dbeta, kh, kw, sh, sw, ph, pw):
+    N, H, W, C = z.shape
+    g = maxpool_bwd(dp, idx, H, W, kh, kw, sh, sw, ph, pw, False)
+    # ReLU mask recomputed from z: bn(z) > 0
+    y = (_f(z) - mean) * (rstd * gamma) + beta
+    dz, _ = bn_bwd(g, z, y, mean, rstd, gamma, dgamma, dbeta, True, False)
+    return dz
+
+
 def avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
     y = F.avg_pool2d(_nchw(_f(x)), (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
                      count_include_pad=count_include_pad)

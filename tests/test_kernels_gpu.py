@@ -391,6 +391,59 @@ def test_maxpool(gpu, case):
     assert rel(dx, dxr) < 1e-2
 
 
+def _global_idx(idx, H, W, kh, kw, sh, sw, ph, pw):
+    """window-local argmax (native) -> flat h*W+w index (oracle's maxpool_bwd)."""
+    N, P, Q, Cc = idx.shape
+    i, k = idx.long() // kw, idx.long() % kw
+    p = torch.arange(P, device=idx.device).view(1, P, 1, 1)
+    q = torch.arange(Q, device=idx.device).view(1, 1, Q, 1)
+    h = p * sh - ph + i
+    w = q * sw - pw + k
+    assert bool(((h >= 0) & (h < H) & (w >= 0) & (w < W)).all())
+    return (h * W + w).to(torch.int32)
+
+
+@pytest.mark.parametrize("case", [(4, 112, 112, 64, 3, 3, 2, 2, 1, 1, False),  # resnet stem
+                                  (2, 55, 55, 96, 3, 3, 2, 2, 0, 0, True),     # ceil mode
+                                  (2, 21, 17, 16, 3, 3, 2, 2, 1, 1, False)])
+def test_bn_relu_maxpool_fused(gpu, case):
+    """Fused stem BN+ReLU+max-pool (forward) and pool-gather+BN backward vs the oracle's
+    bn -> relu -> maxpool composition.  The backward oracle routes the pooled gradient
+    through the native argmax: values that tie after bf16 rounding may legitimately pick
+    a different window element."""
+    N, H, W, Cc, kh, kw, sh, sw, ph, pw, ceil = case
+    torch.manual_seed(11)
+    z = bf(N, H, W, Cc, dev=gpu, scale=1.5) + 0.2
+    z = z.to(torch.bfloat16)
+    st = torch.stack([z.float().reshape(-1, Cc).mean(0), z.float().reshape(-1, Cc).var(0, unbiased=False)])
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu) * 0.5
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    rm2, rv2 = rm.clone(), rv.clone()
+    cnt = torch.tensor(3, dtype=torch.long, device=gpu)
+    y, idx, mean, rstd = C().bn_relu_maxpool_fwd(z, st, g, b, rm, rv, 0.1, 1e-5, kh, kw, sh, sw,
+                                                 ph, pw, ceil, cnt)
+    yr, _, meanr, rstdr = ref.bn_relu_maxpool_fwd(z, st, g, b, rm2, rv2, 0.1, 1e-5, kh, kw, sh,
+                                                  sw, ph, pw, ceil)
+    assert int(cnt) == 4
+    assert y.shape == yr.shape and rel(y, yr) < 1e-2
+    assert rel(mean, meanr) < 1e-3 and rel(rstd, rstdr) < 1e-3
+    assert rel(rm, rm2) < 1e-3 and rel(rv, rv2) < 1e-3
+    gi = _global_idx(idx, H, W, kh, kw, sh, sw, ph, pw)
+    # the argmax points at a maximal element of relu(bn(z)) in its window
+    yfull = torch.relu((z.float() - mean) * (rstd * g) + b)
+    picked = torch.gather(yfull.permute(0, 3, 1, 2).reshape(N, Cc, -1), 2,
+                          gi.permute(0, 3, 1, 2).reshape(N, Cc, -1).long())
+    assert rel(picked.reshape(N, Cc, *y.shape[1:3]).permute(0, 2, 3, 1), y) < 1e-2
+    dp = bf(*y.shape, dev=gpu)
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    dz = C().maxpool_bn_bwd(dp, idx, z, mean, rstd, g, b, dg, db, kh, kw, sh, sw, ph, pw)
+    dzr = ref.maxpool_bn_bwd(dp, gi, z, mean, rstd, g, b, dg2, db2, kh, kw, sh, sw, ph, pw)
+    assert rel(dz, dzr) < 2e-2
+    assert rel(dg, dg2) < 1e-2 and rel(db, db2) < 1e-2
+
+
 @pytest.mark.parametrize("case", POOL_CASES + [(2, 35, 35, 64, 3, 3, 1, 1, 1, 1, False),
                                                (2, 17, 17, 64, 5, 5, 3, 3, 0, 0, False)])
 @pytest.mark.parametrize("cip", [True, False])
