@@ -130,7 +130,7 @@ struct BnRed {
 
 static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw,
                               int64_t ph, int64_t pw, c10::optional<Tensor> wt_opt,
-                              BnRed* bnred) {
+                              BnRed* bnred, c10::optional<Tensor> accum = c10::nullopt) {
   CHECK_ACT(dy);
   CHECK_ACT(w);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -138,7 +138,20 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
   TORCH_CHECK(Kw == K, "conv_dgrad: channel mismatch");
   TORCH_CHECK(R * S <= mpa::MAXT, "conv_dgrad: too many taps");
   const c10::OptionalDeviceGuard g(device_of(dy));
-  Tensor dx = empty_like_shape(dy, {N, (int64_t)H, (int64_t)W, C}, torch::kBFloat16);
+  // accum: dx accumulates into this tensor (a second gradient contribution to the same
+  // activation, e.g. a residual block's input: conv1 dgrad + shortcut) - no separate add
+  const bool acc = accum && accum->defined();
+  Tensor dx;
+  if (acc) {
+    CHECK_ACT((*accum));
+    TORCH_CHECK(accum->dim() == 4 && accum->size(0) == N && accum->size(1) == H &&
+                    accum->size(2) == W && accum->size(3) == C,
+                "conv_dgrad: accum shape mismatch");
+    TORCH_CHECK(!bnred, "conv_dgrad: accum and the fused BN reduction are exclusive");
+    dx = *accum;
+  } else {
+    dx = empty_like_shape(dy, {N, (int64_t)H, (int64_t)W, C}, torch::kBFloat16);
+  }
   const int vw = std::min(vec_width(K), vec_width(C));
   // sub-pixel decomposition: output phase (a_, b_) of dx is a stride-1 conv of dy with the
   // taps (r, s) congruent to it; stride 1 has one phase
@@ -156,6 +169,7 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
   a.C = dx.data_ptr(); a.ldc = C;
   a.dH = H; a.dW = W; a.Uoh = sh; a.Uow = sw;
   a.bias = nullptr; a.stats = nullptr; a.relu = 0;
+  a.beta = acc ? 1 : 0;
   int T = 0, nph = 0;
   for (int a_ = 0; a_ < sh; ++a_)
     for (int b_ = 0; b_ < sw; ++b_) {
@@ -209,10 +223,11 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
     float* wsp = alloc_ws(ws, dy, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
     mpa::igemm_rows_dgrad(a, vw, wsp, cur_stream(), bkc);
   } else {
-    // phases with no taps (stride > kernel) leave their dx pixels zero
+    // phases with no taps (stride > kernel) leave their dx pixels zero (or, accumulating,
+    // untouched)
     bool empty = false;
     for (int i = 0; i < nph; ++i) empty |= a.ph[i].T == 0;
-    if (empty) dx.zero_();
+    if (empty && !acc) dx.zero_();
     int k = 0;
     for (int i = 0; i < nph; ++i)
       if (a.ph[i].T > 0) a.ph[k++] = a.ph[i];
@@ -223,8 +238,8 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
-                  int64_t pw, c10::optional<Tensor> wt_opt) {
-  return conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt_opt, nullptr);
+                  int64_t pw, c10::optional<Tensor> wt_opt, c10::optional<Tensor> accum) {
+  return conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt_opt, nullptr, accum);
 }
 
 // fused-reduction dgrad available: LDS-DMA engine, 16-B granular dy (K) and dx (C), and
@@ -697,7 +712,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
-        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none());
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none(),
+        py::arg("accum") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred);

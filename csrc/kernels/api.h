@@ -67,6 +67,8 @@ struct IGemmArgs {
   const float* ep_rstd;
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
+  int beta;               // 1: accumulate, C = acc + C (bf16 read-add-write, one rounding):
+                          // a second gradient contribution lands in the first one's buffer
 };
 
 struct WGradArgs {
@@ -109,6 +111,10 @@ bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path
 int64_t bn_ws_floats(int M, int C);
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
 // sums [2][C] of (x - shift) and (x - shift)^2 over M rows -> out [mean(C), var(C)]
+// slab [S][2C] of shifted (sum, sumsq) rows -> sums [2C] and out [mean(C), var(C)] (the
+// slab may be folded in place); replaces slab_reduce + stats_finalize
+void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sums, float* out,
+                hipStream_t s);
 void stats_finalize(const float* sums, const float* shift, int M, int C, float* out,
                     hipStream_t s);
 void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,

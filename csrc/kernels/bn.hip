@@ -449,15 +449,30 @@ __global__ void relu_kernel(const bf16_t* __restrict__ x, int64_t n8, bf16_t* __
 // Cross-block reduction of per-block partial sums (replaces same-address fp32 atomics,
 // which serialise at the memory-side atomic unit when thousands of blocks target the
 // same 2*C words - MI355X_MICROARCH.md "Global float atomics", contention row).
-// out[w] += sum_s slab[s*W + w]; 64 columns x 4 slab groups per block, <= 32 adds/word.
+// out[w] += sum_s slab[s*W + w]; 64 columns x 4 slab groups per block.  Each thread keeps
+// four independent partial sums so four slab loads are in flight per iteration (the
+// kernels are latency-bound: a few hundred KiB, one dependent add chain per thread).
+__device__ __forceinline__ float slab_col_sum(const float* __restrict__ slab, size_t rstride,
+                                              int s0, int S, int step) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s_ = s0;
+  for (; s_ + 3 * step < S; s_ += 4 * step) {
+    a0 += slab[(size_t)s_ * rstride];
+    a1 += slab[(size_t)(s_ + step) * rstride];
+    a2 += slab[(size_t)(s_ + 2 * step) * rstride];
+    a3 += slab[(size_t)(s_ + 3 * step) * rstride];
+  }
+  for (; s_ < S; s_ += step) a0 += slab[(size_t)s_ * rstride];
+  return (a0 + a1) + (a2 + a3);
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int S,
                                                            int W, float* __restrict__ out) {
   __shared__ float red[256];
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   float acc = 0.f;
-  if (w < W)
-    for (int s_ = blockIdx.y * 4 + g; s_ < S; s_ += gridDim.y * 4) acc += slab[(size_t)s_ * W + w];
+  if (w < W) acc = slab_col_sum(slab + w, W, blockIdx.y * 4 + g, S, gridDim.y * 4);
   red[threadIdx.x] = acc;
   __syncthreads();
   if (g == 0 && w < W) {
@@ -495,6 +510,74 @@ void stats_finalize(const float* sums, const float* shift, int M, int C, float* 
                     hipStream_t s) {
   hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, shift,
                      M, C, out);
+}
+
+// Statistics slab [S][2C] (rows of shifted (sum, sum of squares)) -> sums [2C] and the
+// finalized [mean(C), biased var(C)], in ONE launch for slabs of <= 64 rows (the slab
+// reduction and the finalize used to be two dependent launches per BN layer).  Larger
+// slabs (the 3.2 M-pixel stem: 25,088 rows) first fold each chunk of `chunk` rows into
+// the chunk's first row in place (deterministic, no atomics; every block owns its chunk),
+// then the finalize kernel reads the chunk heads.  Thread (g, c) sums rows g, g+4, ... of
+// columns c and C + c; the 4 groups combine through LDS in a fixed order.
+__global__ __launch_bounds__(256) void slab_fold_kernel(float* __restrict__ slab, int S, int W,
+                                                        int chunk) {
+  __shared__ float red[256];
+  const int w = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * chunk;
+  const int r1 = min(S, r0 + chunk);
+  float acc = 0.f;
+  if (w < W) acc = slab_col_sum(slab + w, W, r0 + g, r1, 4);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (g == 0 && w < W)
+    slab[(size_t)r0 * W + w] =
+        (red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192]);
+}
+
+__global__ __launch_bounds__(256) void slab_stats_kernel(const float* __restrict__ slab, int S,
+                                                         int rstep, int C,
+                                                         const float* __restrict__ shift, int M,
+                                                         float* __restrict__ sums,
+                                                         float* __restrict__ out) {
+  __shared__ float red[2][256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const size_t W = 2 * (size_t)C;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    a = slab_col_sum(slab + c, W * rstep, g, S, 4);
+    b = slab_col_sum(slab + C + c, W * rstep, g, S, 4);
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    const int t = threadIdx.x;
+    a = (red[0][t] + red[0][t + 64]) + (red[0][t + 128] + red[0][t + 192]);
+    b = (red[1][t] + red[1][t + 64]) + (red[1][t + 128] + red[1][t + 192]);
+    sums[c] = a;
+    sums[C + c] = b;
+    const float inv = 1.f / (float)M;
+    const float d = a * inv;  // mean of (x - K)
+    const float k = shift ? shift[c] : 0.f;
+    out[c] = k + d;
+    out[C + c] = fmaxf(b * inv - d * d, 0.f);
+  }
+}
+
+void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sums, float* out,
+                hipStream_t s) {
+  int rstep = 1, rows = S;
+  if (S > 64) {  // fold to <= 64 chunk heads: the finalize has only C/64 blocks
+    const int chunk = (S + 63) / 64;
+    rows = (S + chunk - 1) / chunk;
+    rstep = chunk;
+    hipLaunchKernelGGL(slab_fold_kernel, dim3((2 * C + 63) / 64, rows), dim3(256), 0, s, slab, S,
+                       2 * C, chunk);
+  }
+  hipLaunchKernelGGL(slab_stats_kernel, dim3((C + 63) / 64), dim3(256), 0, s, slab, rows, rstep,
+                     C, shift, M, sums, out);
 }
 
 // ----------------------------------------------- BN + ReLU + max-pool (network stems)
@@ -849,8 +932,7 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
   const dim3 g = grid_for(M, C);
   float* sums = ws + (int64_t)g.x * 2 * C;
   BN_LAUNCH(bn_stats_kernel, g, s, x, M, C, shift, ws, sums);
-  slab_reduce(ws, g.x, 2 * C, sums, false, s);
-  stats_finalize(sums, shift, M, C, stats, s);
+  slab_stats(ws, g.x, C, shift, M, sums, stats, s);
 }
 
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,

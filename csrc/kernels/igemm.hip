@@ -455,8 +455,9 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
                                        const float* __restrict__ bias, int relu,
                                        float* __restrict__ slab,
                                        const float* __restrict__ shift,
-                                       float* __restrict__ sums) {
-  // sums the S split partials [S][M][N]; one block per 64 columns x (rows strided by
+                                       float* __restrict__ sums, int beta) {
+  // sums the S split partials [S][M][N] (+ the existing output when beta); one block per
+  // 64 columns x (rows strided by
   // gridDim.y); statistics go to the per-block-row slab [gridDim.y][2N]
   __shared__ float red[2][256];
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -469,6 +470,7 @@ __global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
     for (int m = r0; m < M; m += gridDim.y * 4) {
       float v = b;
       for (int z = 0; z < S; ++z) v += ws[z * MN + (size_t)m * N + n];
+      if (beta) v += bf2f(out[(size_t)m * N + n]);
       if (relu) v = fmaxf(v, 0.f);
       const bf16_t o = f2bf(v);
       out[(size_t)m * N + n] = o;
@@ -660,13 +662,10 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     dim3 grid((a.N + 63) / 64, gy);
     hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, splits,
                        (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
-                       stats ? slab : (float*)nullptr, a.stats_shift, sums);
+                       stats ? slab : (float*)nullptr, a.stats_shift, sums, a.beta);
     slab_rows = gy;
   }
-  if (stats) {
-    slab_reduce(slab, slab_rows, 2 * a.N, sums, false, s);
-    stats_finalize(sums, a.stats_shift, a.M, a.N, stats, s);
-  }
+  if (stats) slab_stats(slab, slab_rows, a.N, a.stats_shift, a.M, sums, stats, s);
 }
 
 // `a.stats` (if set) receives the finalized per-column statistics [mean(N), var(N)]

@@ -158,20 +158,40 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
         for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? ssrc[n + r] : 0.f;
       }
     }
+    size_t orows[TM];
+    bool moks[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wrow0 + i * 16 + (lane & 15);
-      const bool mok = m < g.M;
-      size_t orow = 0;
-      if (mok) {
+      moks[i] = m < g.M;
+      orows[i] = 0;
+      if (moks[i]) {
         const int hw = g.oH * g.oW;
         const int img = m / hw;
         const int rr = m - img * hw;
         const int oh = rr / g.oW;
         const int ow = rr - oh * g.oW;
-        orow = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + g.Poh) * p.dW +
-                (ow * p.Uow + g.Pow)) * p.ldc;
+        orows[i] = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + g.Poh) * p.dW +
+                    (ow * p.Uow + g.Pow)) * p.ldc;
       }
+    }
+    // accumulate mode: issue every read of the existing output up front (one exposed
+    // latency for the tile instead of one per fragment)
+    uint2 oldv[TM][TN];
+    if (p.beta) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wcol0 + j * 16 + nl;
+          oldv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(out + orows[i] + n)
+                                                 : make_uint2(0u, 0u);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bool mok = moks[i];
+      const size_t orow = orows[i];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wcol0 + j * 16 + nl;
@@ -206,9 +226,21 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
             v[r] = live[r] ? d : 0.f;
           }
         } else {
+          float old[4] = {0.f, 0.f, 0.f, 0.f};
+          if (p.beta && mok) {
+            if (n + 3 < p.N) {
+              const uint2 oo = oldv[i][j];
+              old[0] = bf2f(oo.x & 0xffff); old[1] = bf2f(oo.x >> 16);
+              old[2] = bf2f(oo.y & 0xffff); old[3] = bf2f(oo.y >> 16);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) old[r] = bf2f(out[orow + n + r]);
+            }
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float t = acc[i][j][r] + bias[j][r];
+            float t = acc[i][j][r] + bias[j][r] + old[r];
             if (p.relu) t = fmaxf(t, 0.f);
             v[r] = t;
           }

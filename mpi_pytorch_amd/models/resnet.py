@@ -19,6 +19,8 @@ from ..ops import functional as Fn
 # default: on ResNet-18 / batch 256 it removes 8 reduce passes but the dgrad epilogue's
 # strided z / y reads cost as much (same-box A/B: 11.45 ms off vs 11.50 ms on).
 _LINK = os.environ.get("MPA_BN_LINK", "0") == "1"
+# MPA_GRAD_JOIN=0 restores autograd's separate add of the two input-gradient contributions
+_JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
 
 
 class BasicBlock(nn.Module):
@@ -37,13 +39,18 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         # conv1's output feeds only conv2: conv2's dgrad performs bn1's backward reduction
         link = Fn.BNLink() if (self.bn1.training and _LINK) else None
-        out = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True, link_out=link)
+        # x's gradient = conv1's dgrad + the shortcut's: summed inside the second dgrad
+        join = Fn.GradJoin() if (self.bn1.training and _JOIN and x.requires_grad) else None
+        out = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True, link_out=link, join_x=join)
         if self.downsample is not None:
-            identity = Fn.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
+            identity = Fn.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False,
+                                      join_x=join)
+            join_res = None
         else:
             identity = x
+            join_res = join
         return Fn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=identity,
-                              link_in=link)
+                              link_in=link, join_res=join_res)
 
 
 class Downsample(nn.Sequential):

@@ -82,9 +82,86 @@ class BNLink:
         self.z = self.y = self.mean = self.rstd = self.sums = None
 
 
+class GradJoin:
+    """Two gradient contributions to ONE activation, summed without a separate add pass.
+
+    A residual block's input x feeds two ops (conv1 and the shortcut: identity or the
+    downsample conv), so autograd would sum two bf16 gradients with an elementwise add -
+    a full extra read/read/write sweep of the activation per block.  Instead both ops hold
+    the same join.  Whichever backward runs first PARKS its contribution here and returns
+    None for x: an already computed tensor (the identity shortcut's BN gradient), or, for
+    a dgrad, the deferred launch itself.  The second op then produces the sum: one dgrad
+    writes fresh, the other accumulates into it in its GEMM epilogue
+    (``conv_dgrad(..., accum=)``: fp32 add, one rounding).  The fresh one is chosen to be a
+    dgrad that covers every pixel, so a 1x1/s2 downsample (three of four stride phases
+    without taps) never needs a zero fill.  Independent of autograd's execution order."""
+
+    __slots__ = ("partial",)
+
+    def __init__(self):
+        self.partial = None
+
+    def take(self):
+        p, self.partial = self.partial, None
+        return p
+
+
+class _Deferred:
+    """A parked dgrad: ``run(accum)`` launches it (fresh when accum is None)."""
+
+    __slots__ = ("run", "full")
+
+    def __init__(self, run, full: bool):
+        self.run = run
+        self.full = full
+
+
+def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
+    """Offer a computed contribution ``t`` to ``join``; returns what the op hands back to
+    autograd."""
+    if join is None or t is None:
+        return t
+    prev = join.take()
+    if prev is None:
+        join.partial = t
+        return None
+    if isinstance(prev, _Deferred):
+        return prev.run(t)  # the parked dgrad accumulates into t
+    return prev.add_(t)  # two computed tensors (not produced by the ResNet blocks)
+
+
+def _dgrad_full(conv, in_hw) -> bool:
+    """Every pixel of dx receives taps (no tap-less stride phase)."""
+    (sh, sw), (R, S) = conv.stride, conv.kernel_size
+    return sh <= R and sw <= S
+
+
+def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
+    """conv dgrad, summed with the join's other contribution (see GradJoin)."""
+    sh, sw = conv.stride
+    ph, pw = conv.padding
+
+    def run(acc):
+        return k.conv_dgrad(dz, w, in_hw[0], in_hw[1], sh, sw, ph, pw, wt, acc)
+
+    if join is None:
+        return run(None)
+    prev = join.take()
+    full = _dgrad_full(conv, in_hw)
+    if prev is None:
+        join.partial = _Deferred(run, full)
+        return None
+    if isinstance(prev, _Deferred):
+        if full or not prev.full:
+            return prev.run(run(None))
+        return run(prev.run(None))
+    return run(prev)
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None):
+    def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None,
+                join_x=None, join_res=None):
         k = K(x)
         sh, sw = conv.stride
         ph, pw = conv.padding
@@ -105,6 +182,8 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.save_for_backward(x, z, y if relu else None, mean, rstd)
         ctx.link_in = link_in
         ctx.link_out = link_out
+        ctx.join_x = join_x
+        ctx.join_res = join_res
         if link_out is not None:
             link_out.z, link_out.y, link_out.mean, link_out.rstd = z, (y if relu else None), mean, rstd
             link_out.sums = None
@@ -134,6 +213,8 @@ class _ConvBNAct(torch.autograd.Function):
             k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
             _done(w)
         _done(ctx.bias)
+        dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
+        dres = _join_grad(ctx.join_res, dres)
         dx = None
         if ctx.needs_input_grad[0]:
             li = ctx.link_in
@@ -143,15 +224,15 @@ class _ConvBNAct(torch.autograd.Function):
                 dx, li.sums = k.conv_dgrad_bnred(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1],
                                                  sh, sw, ph, pw, wt, li.z,
                                                  _or_empty(li.y, dz), li.mean, li.rstd)
+                dx = _join_grad(ctx.join_x, dx)
             else:
-                dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
-                                   wt)
-        dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
-        return dx, dres, None, None, None, None, None, None, None, None, None
+                dx = _dgrad_joined(k, ctx.join_x, dz, weight_of(w), ctx.in_hw, conv, wt)
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None,
-                link_in: Optional[BNLink] = None, link_out: Optional[BNLink] = None):
+                link_in: Optional[BNLink] = None, link_out: Optional[BNLink] = None,
+                join_x: Optional[GradJoin] = None, join_res: Optional[GradJoin] = None):
     """relu(bn(conv(x)) [+ residual]); BN in train or eval mode per ``bn.training``.
 
     A conv bias in front of a train-mode BN (VGG11_bn) is added before the statistics, so
@@ -161,7 +242,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
     x = conv.fit_input(x)
     if bn.training:
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
-                                bn, relu, link_in, link_out)
+                                bn, relu, link_in, link_out, join_x, join_res)
     k = K(x)
     sh, sw = conv.stride
     ph, pw = conv.padding

@@ -62,13 +62,18 @@ def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None):
     return y
 
 
-def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None):  # wt: transposed copy (unused here)
+def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None, accum=None):
+    """wt: transposed weight copy (unused here); accum: add the result into this tensor
+    (in place, one rounding of the fp32 sum) and return it."""
     N, P, Q, K = dy.shape
     Kw, R, S, C = w.shape
     gi = torch.ops.aten.convolution_backward(
         _nchw(_f(dy)).contiguous(), torch.empty(N, C, H, W, device=dy.device),
         _f(w).permute(0, 3, 1, 2).contiguous(), None, [sh, sw], [ph, pw], [1, 1], False,
         [0, 0], 1, [True, False, False])[0]
+    if accum is not None:
+        accum.copy_((_f(accum) + _nhwc(gi)).to(accum.dtype))
+        return accum
     return _nhwc(gi).to(dy.dtype)
 
 

@@ -97,6 +97,33 @@ def test_conv_dgrad(gpu, engine, case):
     assert rel(dx, dxr) < 2e-2
 
 
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad_accumulate(gpu, engine, case):
+    """dgrad accumulated into an existing gradient (GradJoin: residual-block inputs):
+    dx = acc + dgrad in the epilogue, on every engine, split-K and stride-phase layout
+    (including the 1x1/s2 downsample whose tap-less phases must keep `acc` untouched)."""
+    torch.manual_seed(2)
+    N, H, W, Cc, K, R, S, st, pd = case
+    ph, pw = _pair(pd)
+    P = (H + 2 * ph - R) // st + 1
+    Q = (W + 2 * pw - S) // st + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    w = bf(K, R, S, Cc, dev=gpu, scale=1.0 / math.sqrt(R * S * K))
+    acc0 = bf(N, H, W, Cc, dev=gpu)
+    acc = acc0.clone()
+    out = C().conv_dgrad(dy, w, H, W, st, st, ph, pw, None, acc)
+    exp = acc0.float() + ref.conv_dgrad(dy, w, H, W, st, st, ph, pw).float()
+    torch.cuda.synchronize()
+    assert out.data_ptr() == acc.data_ptr()
+    assert rel(out, exp) < 2e-2
+    if Cc % 8 == 0 and K % 8 == 0:  # transposed-weight (K-contiguous B) path too
+        wt = w.permute(3, 1, 2, 0).reshape(Cc, R * S, K).contiguous()
+        acc2 = acc0.clone()
+        C().conv_dgrad(dy, w, H, W, st, st, ph, pw, wt, acc2)
+        torch.cuda.synchronize()
+        assert torch.equal(acc2, out)
+
+
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0])
 def test_conv_dgrad_transposed_weight(gpu, engine, case):
     """dgrad from the transposed weight copy [C][R*S][K] (K-contiguous B, weight-tap row

@@ -141,3 +141,55 @@ def test_models_train_step_cpu(name, hw):
     m.eval()
     with torch.no_grad():
         assert m(x).shape == (2, 20)
+
+
+def _block_grads(join_on: bool):
+    from mpi_pytorch_amd.models import resnet as R
+    prev = R._JOIN
+    R._JOIN = join_on
+    try:
+        torch.manual_seed(0)
+        ds = R.Downsample(R.Conv2d(8, 16, 1, 2, 0, bias=False), R.BatchNorm2d(16))
+        blocks = torch.nn.Sequential(R.BasicBlock(8, 8), R.BasicBlock(8, 16, 2, ds)).train()
+        from mpi_pytorch_amd.parallel import ParamArena
+        ParamArena(blocks, "cpu")  # weight gradients land in the flat arena (as in training)
+        x = torch.randn(2, 10, 10, 8, requires_grad=True)
+        out = blocks(x)
+        (out.float() * torch.linspace(-1, 1, out.numel()).view_as(out)).sum().backward()
+        return [x.grad.clone()] + [p.grad.clone() for p in blocks.parameters()]
+    finally:
+        R._JOIN = prev
+
+
+def test_residual_grad_join_matches_autograd_sum():
+    """GradJoin (residual-input gradients summed inside the second dgrad's epilogue)
+    gives the same gradients as autograd's separate add, for the identity shortcut and
+    the 1x1/s2 downsample shortcut."""
+    a = _block_grads(True)
+    b = _block_grads(False)
+    assert len(a) == len(b)
+    for ga, gb in zip(a, b):
+        assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("order", ["ds_first", "conv_first"])
+def test_grad_join_order_independent(order):
+    """The deferred-dgrad protocol sums both contributions whichever op autograd runs
+    first, and the fresh launch is the full-coverage 3x3/s2 dgrad."""
+    from mpi_pytorch_amd.ops import functional as Fn
+    from mpi_pytorch_amd.ops import ref
+    from mpi_pytorch_amd.models.layers import Conv2d
+    torch.manual_seed(1)
+    c3 = Conv2d(8, 16, 3, 2, 1, bias=False)
+    c1 = Conv2d(8, 16, 1, 2, 0, bias=False)
+    w3 = torch.randn(16, 3, 3, 8)
+    w1 = torch.randn(16, 1, 1, 8)
+    dz = torch.randn(2, 5, 5, 16)
+    exp = ref.conv_dgrad(dz, w3, 10, 10, 2, 2, 1, 1) + ref.conv_dgrad(dz, w1, 10, 10, 2, 2, 0, 0)
+    j = Fn.GradJoin()
+    calls = [(w3, c3), (w1, c1)] if order == "conv_first" else [(w1, c1), (w3, c3)]
+    r0 = Fn._dgrad_joined(ref, j, dz, calls[0][0], (10, 10), calls[0][1], None)
+    assert r0 is None and j.partial is not None
+    r1 = Fn._dgrad_joined(ref, j, dz, calls[1][0], (10, 10), calls[1][1], None)
+    assert j.partial is None
+    assert torch.allclose(r1, exp, rtol=1e-4, atol=1e-4)
