@@ -53,6 +53,7 @@ def main(argv=None):
     from mpi_pytorch_amd.parallel import init_world, barrier, get_world
     from mpi_pytorch_amd.engine import build_training
     from mpi_pytorch_amd.data import DevicePrefetcher
+    from mpi_pytorch_amd.models import input_spec
 
     world = init_world("cuda")
     if world.world_size != args.gpus and world.rank == 0:
@@ -64,8 +65,10 @@ def main(argv=None):
     model, opt, step, _ = build_training(args.model, args.classes, dev, world, args.lr,
                                          args.optimizer, bucket_mb=args.bucket_mb,
                                          comm_dtype=args.comm_dtype)
+    spec = input_spec(model, hw)  # the stem's image layout, written by the preprocess kernel
     data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
-                            world=world.world_size, depth=6, threads=4)
+                            world=world.world_size, depth=6, threads=4, cpad=spec["cpad"],
+                            pad=spec["pad"])
 
     if args.static_data:
         xs, ys = data.next()

@@ -668,19 +668,26 @@ void cast_f32_bf16(Tensor x, Tensor y) {
 }
 
 // ------------------------------------------------------------------------ preprocess
+// pad: (top, bottom, left, right) zero border of the output canvas (empty = none)
 Tensor preprocess(Tensor img, int64_t OH, int64_t OW, std::vector<double> mean,
-                  std::vector<double> stdv, int64_t mode, int64_t cpad) {
+                  std::vector<double> stdv, int64_t mode, int64_t cpad, std::vector<int64_t> pad) {
   CHECK_CUDA(img);
   CHECK_CONTIG(img);
   TORCH_CHECK(img.scalar_type() == torch::kUInt8 && img.dim() == 4 && img.size(3) == 3,
               "preprocess: expects uint8 [B,H,W,3]");
   TORCH_CHECK(mean.size() == 3 && stdv.size() == 3 && cpad >= 3, "preprocess: args");
+  TORCH_CHECK(pad.empty() || pad.size() == 4, "preprocess: pad = (top, bottom, left, right)");
+  mpa::OutPad pd{0, 0, 0, 0};
+  if (pad.size() == 4) pd = mpa::OutPad{(int)pad[0], (int)pad[1], (int)pad[2], (int)pad[3]};
+  TORCH_CHECK(pd.top >= 0 && pd.bottom >= 0 && pd.left >= 0 && pd.right >= 0, "preprocess: pad");
   const c10::OptionalDeviceGuard g(device_of(img));
   const int B = img.size(0), H = img.size(1), W = img.size(2);
-  Tensor out = empty_like_shape(img, {B, OH, OW, cpad}, torch::kBFloat16);
+  Tensor out = empty_like_shape(
+      img, {B, OH + pd.top + pd.bottom, OW + pd.left + pd.right, cpad}, torch::kBFloat16);
   mpa::Norm3 n;
   for (int i = 0; i < 3; ++i) { n.mean[i] = mean[i]; n.std[i] = stdv[i]; }
-  mpa::preprocess(img.data_ptr<uint8_t>(), B, H, W, OH, OW, n, mode, cpad, bpm(out), cur_stream());
+  mpa::preprocess(img.data_ptr<uint8_t>(), B, H, W, OH, OW, n, mode, cpad, pd, bpm(out),
+                  cur_stream());
   return out;
 }
 
@@ -746,7 +753,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("transpose_krsc", &transpose_krsc);
-  m.def("preprocess", &preprocess);
+  m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
+        py::arg("std"), py::arg("mode"), py::arg("cpad"),
+        py::arg("pad") = std::vector<int64_t>{});
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   mpa_runtime::register_bindings(m);

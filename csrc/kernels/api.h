@@ -193,8 +193,12 @@ struct Norm3 {
   float mean[3];
   float std[3];
 };
+// zero border around the resized image (pre-padded pixel-pair stem input); all 0 = none
+struct OutPad {
+  int top, bottom, left, right;
+};
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
-                int cpad, bf16_raw* out, hipStream_t s);
+                int cpad, OutPad pad, bf16_raw* out, hipStream_t s);
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,
                  bf16_raw* y, uint8_t* mask, hipStream_t s);
 void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,

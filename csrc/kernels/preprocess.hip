@@ -25,21 +25,52 @@ __device__ __forceinline__ float cubic_w(float x) {
   return 0.f;
 }
 
+// One output pixel: 3 normalized channels + zero channels up to cpad, one 8-B store for
+// the 4-channel pixel-pair stem layout, one 16-B store for 8 channels.
+__device__ __forceinline__ void store_px(bf16_t* o, float c0, float c1, float c2, int cpad) {
+  const uint32_t lo = (uint32_t)f2bf(c0) | ((uint32_t)f2bf(c1) << 16);
+  const uint32_t hi = (uint32_t)f2bf(c2);
+  if (cpad == 4) {
+    *(uint2*)o = make_uint2(lo, hi);
+  } else if (cpad == 8) {
+    *(uint4*)o = make_uint4(lo, hi, 0u, 0u);
+  } else {
+    o[0] = (bf16_t)(lo & 0xffff); o[1] = (bf16_t)(lo >> 16); o[2] = (bf16_t)hi;
+    for (int ch = 3; ch < cpad; ++ch) o[ch] = 0;
+  }
+}
+
+// Output geometry: the resized image sits at (pad.top, pad.left) of a zero-bordered
+// [OH + top + bottom][OW + left + right] canvas (the pre-padded input of a pixel-pair
+// stem conv, models/layers.py); a thread per canvas pixel, border pixels write zeros.
+__device__ __forceinline__ bool canvas_px(int64_t t, const OutPad& pd, int OH, int OW, int& b,
+                                          int& oy, int& ox) {
+  const int owp = OW + pd.left + pd.right, ohp = OH + pd.top + pd.bottom;
+  const int px = (int)(t % owp);
+  const int64_t r = t / owp;
+  const int py = (int)(r % ohp);
+  b = (int)(r / ohp);
+  oy = py - pd.top;
+  ox = px - pd.left;
+  return (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW;
+}
+
 __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
     const uint8_t* __restrict__ img, int B, int H, int W, int OH, int OW,
-    Norm3 nrm, int cpad, bf16_t* __restrict__ out) {
+    Norm3 nrm, int cpad, OutPad pd, bf16_t* __restrict__ out) {
   const float* mean = nrm.mean;
   const float* stdv = nrm.std;
-  const int64_t total = (int64_t)B * OH * OW;
+  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
   const float sh = (float)H / OH, sw = (float)W / OW;
   const float m0 = mean[0], m1 = mean[1], m2 = mean[2];
   const float i0 = 1.f / (255.f * stdv[0]), i1 = 1.f / (255.f * stdv[1]), i2 = 1.f / (255.f * stdv[2]);
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int ox = (int)(t % OW);
-    int64_t r = t / OW;
-    const int oy = (int)(r % OH);
-    const int b = (int)(r / OH);
+    int b, oy, ox;
+    if (!canvas_px(t, pd, OH, OW, b, oy, ox)) {
+      store_px(out + t * cpad, 0.f, 0.f, 0.f, cpad);
+      continue;
+    }
     float sy = fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
     float sx = fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
     int y0 = min((int)sy, H - 1), x0 = min((int)sx, W - 1);
@@ -55,11 +86,8 @@ __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
       const float v11 = base[((size_t)y1 * W + x1) * 3 + ch];
       c[ch] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
     }
-    bf16_t* o = out + t * cpad;
-    o[0] = f2bf(c[0] * i0 - m0 / stdv[0]);
-    o[1] = f2bf(c[1] * i1 - m1 / stdv[1]);
-    o[2] = f2bf(c[2] * i2 - m2 / stdv[2]);
-    for (int ch = 3; ch < cpad; ++ch) o[ch] = 0;
+    store_px(out + t * cpad, c[0] * i0 - m0 / stdv[0], c[1] * i1 - m1 / stdv[1],
+             c[2] * i2 - m2 / stdv[2], cpad);
   }
 }
 
@@ -77,16 +105,17 @@ __device__ __forceinline__ void aa_window(int i, int in, int out, int& xmin, int
 
 __global__ __launch_bounds__(256) void preprocess_bicubic_aa_kernel(
     const uint8_t* __restrict__ img, int B, int H, int W, int OH, int OW,
-    Norm3 nrm, int cpad, bf16_t* __restrict__ out) {
+    Norm3 nrm, int cpad, OutPad pd, bf16_t* __restrict__ out) {
   const float* mean = nrm.mean;
   const float* stdv = nrm.std;
-  const int64_t total = (int64_t)B * OH * OW;
+  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int ox = (int)(t % OW);
-    int64_t r = t / OW;
-    const int oy = (int)(r % OH);
-    const int b = (int)(r / OH);
+    int b, oy, ox;
+    if (!canvas_px(t, pd, OH, OW, b, oy, ox)) {
+      store_px(out + t * cpad, 0.f, 0.f, 0.f, cpad);
+      continue;
+    }
     int ymin, ysize, xmin, xsize;
     float cy, isy, suy, cx, isx, sux;
     aa_window(oy, H, OH, ymin, ysize, cy, isy, suy);
@@ -112,10 +141,8 @@ __global__ __launch_bounds__(256) void preprocess_bicubic_aa_kernel(
       acc[1] += wy * row[1];
       acc[2] += wy * row[2];
     }
-    bf16_t* o = out + t * cpad;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) o[ch] = f2bf((acc[ch] / 255.f - mean[ch]) / stdv[ch]);
-    for (int ch = 3; ch < cpad; ++ch) o[ch] = 0;
+    store_px(out + t * cpad, (acc[0] / 255.f - mean[0]) / stdv[0],
+             (acc[1] / 255.f - mean[1]) / stdv[1], (acc[2] / 255.f - mean[2]) / stdv[2], cpad);
   }
 }
 
@@ -155,14 +182,14 @@ static int blocks_n(int64_t n) {
 }
 
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
-                int cpad, bf16_raw* out, hipStream_t s) {
-  const int64_t total = (int64_t)B * OH * OW;
+                int cpad, OutPad pd, bf16_raw* out, hipStream_t s) {
+  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
   if (mode == 0)
     hipLaunchKernelGGL(preprocess_bilinear_kernel, dim3(blocks_n(total)), dim3(256), 0, s, img, B,
-                       H, W, OH, OW, nrm, cpad, out);
+                       H, W, OH, OW, nrm, cpad, pd, out);
   else
     hipLaunchKernelGGL(preprocess_bicubic_aa_kernel, dim3(blocks_n(total)), dim3(256), 0, s, img,
-                       B, H, W, OH, OW, nrm, cpad, out);
+                       B, H, W, OH, OW, nrm, cpad, pd, out);
 }
 
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,

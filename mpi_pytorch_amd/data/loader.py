@@ -58,13 +58,14 @@ class DevicePrefetcher:
     def __init__(self, device: torch.device, batch: int, src_hw: Tuple[int, int],
                  out_hw: Tuple[int, int], num_classes: int, seed: int = 0, rank: int = 0,
                  world: int = 1, depth: int = 4, threads: int = 2, mode: int = 0,
-                 cpad: int = 8, ring=None):
+                 cpad: int = 8, ring=None, pad=None):
         self.device = torch.device(device)
         self.batch = batch
         self.src_hw = src_hw
         self.out_hw = out_hw
         self.mode = mode
         self.cpad = cpad
+        self.pad = list(pad) if pad else []  # zero canvas border (models.input_spec)
         self.cuda = self.device.type == "cuda"
         if self.cuda:
             self.ring = ring if ring is not None else _ext().BatchRing(
@@ -89,7 +90,7 @@ class DevicePrefetcher:
         if not self.cuda:
             img, lab = self.src.next()
             x = Fn.preprocess(img, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode, self.cpad,
-                              out_dtype=torch.float32)
+                              out_dtype=torch.float32, pad=self.pad)
             return x, lab
         self._recycle()
         slot, img_h, lab_h, _bidx = self.ring.acquire()
@@ -105,7 +106,7 @@ class DevicePrefetcher:
         img_d.record_stream(cur)
         lab_d.record_stream(cur)
         x = _ext().preprocess(img_d, self.out_hw[0], self.out_hw[1], list(IMAGENET_MEAN),
-                              list(IMAGENET_STD), self.mode, self.cpad)
+                              list(IMAGENET_STD), self.mode, self.cpad, self.pad)
         return x, lab_d
 
     def __iter__(self) -> Iterator:

@@ -37,7 +37,7 @@ from ..config import Config
 from ..checkpoint import read_checkpoint
 from ..data.loader import IMAGENET_MEAN, IMAGENET_STD
 from ..data.manifest import SyntheticImages, FolderImages, images_available, synthetic_manifest
-from ..models import initialize_model
+from ..models import initialize_model, input_spec
 from ..ops import functional as Fn
 from ..parallel import init_world, reduce_scalar, shard_dataframe, broadcast_object, ParamArena
 from ..utils.logging import init_logger
@@ -60,8 +60,12 @@ def load_predictor(cfg: Config, device, ckpt_path: Optional[str] = None):
 
 class StreamPipeline:
     def __init__(self, model, device, out_hw, lanes: int = 1, depth: int = 4,
-                 assign: str = "random", seed: int = 0, mode: int = 1, cpad: int = 8):
+                 assign: str = "random", seed: int = 0, mode: int = 1, cpad=None, pad=None):
         self.model = model
+        if cpad is None:  # the model stem's input layout (models.input_spec)
+            spec = input_spec(model, out_hw)
+            cpad, pad = spec["cpad"], spec["pad"]
+        self.pad = pad
         self.device = torch.device(device)
         self.out_hw = out_hw
         self.lanes = max(1, lanes)
@@ -126,10 +130,11 @@ class StreamPipeline:
                 with torch.cuda.stream(self.prep_stream):
                     gd.record_stream(self.prep_stream)
                     outs.append(Fn.preprocess(gd, self.out_hw, IMAGENET_MEAN, IMAGENET_STD,
-                                              self.mode, self.cpad))
+                                              self.mode, self.cpad, pad=self.pad))
             else:
                 outs.append(Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD,
-                                          self.mode, self.cpad, out_dtype=torch.float32))
+                                          self.mode, self.cpad, out_dtype=torch.float32,
+                                          pad=self.pad))
         if self.cuda:
             with torch.cuda.stream(self.prep_stream):
                 x = outs[0] if len(outs) == 1 else torch.cat(outs, 0)

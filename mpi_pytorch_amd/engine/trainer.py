@@ -42,6 +42,7 @@ from ..parallel import (init_world, get_world, barrier, scatter_object, broadcas
 from ..parallel.sharding import equal_step_count
 from ..utils.logging import init_logger, MetricsWriter
 from .step import build_training
+from ..models import input_spec
 
 
 class ManifestBatches:
@@ -53,7 +54,8 @@ class ManifestBatches:
     reference's ToTensor -> Resize -> Normalize on tensors, main.py:62-65)."""
 
     def __init__(self, names: Sequence[str], labels: Sequence[int], batch: int, out_hw,
-                 device, source, shuffle: bool, seed: int = 0, mode: int = 0, cpad: int = 8):
+                 device, source, shuffle: bool, seed: int = 0, mode: int = 0, cpad: int = 8,
+                 pad=None):
         self.names = list(names)
         self.labels = np.asarray(labels, dtype=np.int64)
         self.batch = batch
@@ -64,7 +66,13 @@ class ManifestBatches:
         self.seed = seed
         self.mode = mode
         self.cpad = cpad
+        self.pad = pad
         self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def set_layout(self, spec: dict) -> None:
+        """Produce the model stem's input layout (``models.input_spec``)."""
+        self.cpad = spec["cpad"]
+        self.pad = spec["pad"]
 
     def __len__(self):
         return (len(self.names) + self.batch - 1) // self.batch
@@ -84,7 +92,7 @@ class ManifestBatches:
             if cuda:
                 g = g.pin_memory().to(self.device, non_blocking=True)
             outs.append(Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
-                                      self.cpad, out_dtype=torch.float32))
+                                      self.cpad, out_dtype=torch.float32, pad=self.pad))
         x = outs[0] if len(outs) == 1 else torch.cat(outs, 0)
         y = labels.to(self.device, non_blocking=cuda)
         return x, y
@@ -163,6 +171,10 @@ def run_training(cfg: Config) -> dict:
         cfg.weight_decay, cfg.FEATURE_EXTRACT, cfg.bucket_mb, cfg.overlap_comm,
         cfg.grad_comm_dtype)
     log.info("_Model Created: {}".format(cfg.MODEL_NAME))
+    spec = input_spec(model, out_hw)
+    for ld in (train_loader, val_loader):
+        if ld is not None:
+            ld.set_layout(spec)
     log.info("_Optimizer Created")
     start_epoch = 0
     ckpt = os.path.join(cfg.CHECKPOINT_DIR, cfg.CHECKPOINT_NAME)

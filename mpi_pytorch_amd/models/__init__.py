@@ -81,6 +81,17 @@ def initialize_model(model_name: str, num_classes: int, feature_extract: bool,
     return model, input_size
 
 
+def input_spec(model: nn.Module, hw) -> dict:
+    """Image layout the model's stem wants from the data pipeline for ``hw`` images:
+    ``{"cpad": channels, "pad": (top, bottom, left, right) | None}`` - a 4-channel zero
+    canvas for pixel-pair stems (``layers.Conv2d``), 8 channels otherwise.  The preprocess
+    kernel writes it directly; any other layout is converted by the stem (slower)."""
+    for m in model.modules():
+        if isinstance(m, Conv2d) and m.in_channels <= 4:
+            return m.input_spec(tuple(hw))
+    return {"cpad": 8, "pad": None}
+
+
 def head_parameters(model: nn.Module):
     """Parameters of the replaced classifier head(s)."""
     for name in ("fc", "classifier", "AuxLogits"):
@@ -90,5 +101,6 @@ def head_parameters(model: nn.Module):
 
 
 __all__ = ["initialize_model", "set_parameter_requires_grad", "ARCH", "InceptionOutputs",
+           "input_spec",
            "resnet18", "resnet34", "vgg11_bn", "vgg16", "alexnet", "squeezenet1_0",
            "densenet121", "inception_v3"]

@@ -12,6 +12,7 @@ loaded by ``evaluation_pipeline.py:142-144`` / ``helpers.py:13``).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -40,6 +41,9 @@ def _oihw_to_krsc(t):
     return t.permute(0, 2, 3, 1)
 
 
+_PAIR_STEM = os.environ.get("MPA_PAIR_STEM", "1") == "1"
+
+
 class Conv2d(nn.Module):
     """Conv2d with KRSC weight storage. ``state_dict`` exposes OIHW like ``nn.Conv2d``.
 
@@ -48,12 +52,27 @@ class Conv2d(nn.Module):
     preprocess kernel, so the stem conv takes the 16-byte vector gather path; the zero
     channels contribute exactly nothing and receive exactly zero gradient.  The padding is
     invisible in state_dict / optimizer state (sliced off on export, re-added on import).
+
+    **Pixel-pair stems** (image input, horizontal stride 2 - the 7x7/s2 stems of ResNet,
+    DenseNet and SqueezeNet, Inception's 3x3/s2): the image is stored with 4 channels
+    (RGB + 0) on a zero-bordered canvas (``input_spec``, written directly by the preprocess
+    kernel), so two horizontally adjacent pixels are one 16-B, 8-"channel" vector.  A
+    stride-2 conv with an S-wide kernel over 4-channel pixels is then exactly a stride-1
+    conv with a ceil(S/2)-wide kernel over 8-channel pixel pairs, padding 0: weight
+    ``[K][R][S][3]`` is stored as ``[K][R][ceil(S/2)][2 x 4]`` (zero for the 4th channel
+    and, for odd S, the column past the kernel).  Against the plain 8-channel layout this
+    halves the stem's MFMA work (K = R x 32 instead of R x 2 x 32 for 7x7), its wgrad
+    columns (224 vs 392) and the image bytes.  The column past an odd kernel would get a
+    nonzero gradient (its input pixels are real), so ``fix_grad`` zeroes it after wgrad;
+    the 4th channel's gradient is exactly zero (its input is).
     """
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size, stride=1, padding=0,
                  bias: bool = True, pad_out: bool = False):
         super().__init__()
         self.in_channels = in_channels
+        kh0, kw0 = _pair(kernel_size)
+        self.pair = (_PAIR_STEM and in_channels <= 4 and _pair(stride)[1] == 2 and kw0 >= 2)
         self.cin_store = 8 if in_channels < 8 else in_channels
         self.out_channels = out_channels
         # pad_out: store the output channels rounded up to a multiple of 32 (zero filters) -
@@ -64,13 +83,20 @@ class Conv2d(nn.Module):
         self.stride = _pair(stride)
         self.padding = _pair(padding)
         kh, kw = self.kernel_size
+        self.sp = (kw + 1) // 2  # pixel-pair kernel width
+        # geometry of the conv the kernels actually run: (sh, sw, ph, pw)
+        if self.pair:
+            self.kgeom = (self.stride[0], 1, 0, 0)
+        else:
+            self.kgeom = (self.stride[0], self.stride[1], self.padding[0], self.padding[1])
         w = torch.empty(out_channels, in_channels, kh, kw)
         nn.init.kaiming_uniform_(w, a=math.sqrt(5))
         self.weight = nn.Parameter(self._imp(w).contiguous())
         self.weight._mpa_export = self._exp
         self.weight._mpa_import = self._imp
         # (K, R*S, C) of the stored KRSC weight: the arena keeps a [C][R*S][K] copy for dgrad
-        self.weight._mpa_tlayout = (self.cout_store, kh * kw, self.cin_store)
+        ks = self.sp if self.pair else kw
+        self.weight._mpa_tlayout = (self.cout_store, kh * ks, self.cin_store)
         if bias:
             fan_in = in_channels * kh * kw
             bound = 1 / math.sqrt(fan_in)
@@ -82,8 +108,11 @@ class Conv2d(nn.Module):
         else:
             self.register_parameter("bias", None)
 
-    def _exp(self, t):  # internal KRSC (maybe channel padded) -> OIHW
-        if self.cin_store != self.in_channels:
+    def _exp(self, t):  # internal KRSC (maybe channel padded / pixel pairs) -> OIHW
+        if self.pair:  # [K][R][Sp][2 x 4] -> [K][R][S][3]
+            kh, kw = self.kernel_size
+            t = t.reshape(t.shape[0], kh, 2 * self.sp, 4)[:, :, :kw, :self.in_channels]
+        elif self.cin_store != self.in_channels:
             t = t[..., :self.in_channels]
         if self.cout_store != self.out_channels:
             t = t[:self.out_channels]
@@ -91,7 +120,11 @@ class Conv2d(nn.Module):
 
     def _imp(self, t):  # OIHW -> internal KRSC
         t = _oihw_to_krsc(t)
-        if self.cin_store != self.in_channels:
+        if self.pair:
+            kh, kw = self.kernel_size
+            t = F.pad(t, (0, 4 - self.in_channels, 0, 2 * self.sp - kw))
+            t = t.reshape(t.shape[0], kh, self.sp, 8)
+        elif self.cin_store != self.in_channels:
             t = F.pad(t, (0, self.cin_store - self.in_channels))
         if t.shape[0] < self.cout_store:
             t = F.pad(t, (0, 0, 0, 0, 0, 0, 0, self.cout_store - t.shape[0]))
@@ -138,12 +171,45 @@ class Conv2d(nn.Module):
     def forward(self, x, relu: bool = False):
         return Fn.conv_act(x, self, relu=relu)
 
+    def input_spec(self, hw) -> dict:
+        """Layout the data pipeline should produce for an ``hw`` image fed to this conv:
+        ``cpad`` channels on a zero canvas ``pad`` = (top, bottom, left, right)."""
+        if not self.pair:
+            return {"cpad": self.cin_store, "pad": None}
+        H, W = hw
+        (kh, kw), (ph, pw) = self.kernel_size, self.padding
+        Q = (W + 2 * pw - kw) // 2 + 1
+        right = 2 * (Q - 1 + self.sp) - W - pw
+        return {"cpad": 4, "pad": (ph, ph, pw, right)}
+
     def fit_input(self, x):
-        """Zero-pad an image input's channel dim to the stored width (no-op normally)."""
+        """Bring an image input into the stored layout.  Plain convs: zero-pad the channel
+        dim to the stored width (no-op normally).  Pixel-pair stems: a 4-channel input is
+        taken to be the pre-padded canvas of ``input_spec`` (what the data pipeline
+        produces); 3/8-channel images are converted here.  Returns the [N][Hp][Wp/2][8]
+        pixel-pair view."""
         c = x.shape[-1]
+        if self.pair:
+            if c != 4:
+                N, H, W = x.shape[:3]
+                t, b, l, r = self.input_spec((H, W))["pad"]
+                if r < 0:
+                    raise ValueError("pixel-pair stem: image width %d too small" % W)
+                x = F.pad(x[..., :3], (0, 1, l, r, t, b))
+            N, Hp, Wp = x.shape[:3]
+            if Wp % 2:
+                raise ValueError("pixel-pair stem: canvas width %d is odd" % Wp)
+            return x.contiguous().view(N, Hp, Wp // 2, 8)
         if c < self.cin_store:
             x = F.pad(x, (0, self.cin_store - c))
         return x
+
+    def fix_grad(self, g) -> None:
+        """Pixel-pair stem with an odd kernel width: the stored column past the kernel
+        (second pixel of the last pair) must keep exactly zero weight."""
+        kw = self.kernel_size[1]
+        if self.pair and kw % 2 and g is not None:
+            g.view(g.shape[0], self.kernel_size[0], self.sp, 8)[:, :, self.sp - 1, 4:].zero_()
 
     def extra_repr(self):
         return "{}, {}, kernel_size={}, stride={}, padding={}, bias={}".format(

@@ -132,14 +132,14 @@ def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
 
 def _dgrad_full(conv, in_hw) -> bool:
     """Every pixel of dx receives taps (no tap-less stride phase)."""
-    (sh, sw), (R, S) = conv.stride, conv.kernel_size
+    sh, sw = conv.kgeom[:2]
+    R, S = conv.weight.shape[1:3]
     return sh <= R and sw <= S
 
 
 def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
     """conv dgrad, summed with the join's other contribution (see GradJoin)."""
-    sh, sw = conv.stride
-    ph, pw = conv.padding
+    sh, sw, ph, pw = conv.kgeom
 
     def run(acc):
         return k.conv_dgrad(dz, w, in_hw[0], in_hw[1], sh, sw, ph, pw, wt, acc)
@@ -163,8 +163,7 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None,
                 join_x=None, join_res=None):
         k = K(x)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
         # BN statistics come out of the conv epilogue, shifted by the running mean
@@ -207,10 +206,10 @@ class _ConvBNAct(torch.autograd.Function):
             dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
                              _sink(beta, dy), True, want_g)
         _done(gamma, beta)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
             k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            conv.fix_grad(w.grad)
             _done(w)
         _done(ctx.bias)
         dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
@@ -244,8 +243,7 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
                                 bn, relu, link_in, link_out, join_x, join_res)
     k = K(x)
-    sh, sw = conv.stride
-    ph, pw = conv.padding
+    sh, sw, ph, pw = conv.kgeom
     z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,
                    _empty(x), _empty(x))
     return k.bn_fwd_eval(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
@@ -262,8 +260,7 @@ class _ConvBNReLUPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, conv, bn, cfg):
         k = K(x)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
         z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
@@ -288,10 +285,10 @@ class _ConvBNReLUPool(torch.autograd.Function):
         dz = k.maxpool_bn_bwd(dy.contiguous(), idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
                               _sink(beta, dy), *ctx.cfg[:6])
         _done(gamma, beta)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
             k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            conv.fix_grad(w.grad)
             _done(w)
         _done(ctx.bias)
         dx = None
@@ -317,8 +314,7 @@ class _ConvAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, conv, relu):
         k = K(x)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu, _empty(x),
                        _empty(x))
         ctx.conv = conv
@@ -337,10 +333,10 @@ class _ConvAct(torch.autograd.Function):
         dy = dy.contiguous()
         g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
         _done(b)
-        sh, sw = conv.stride
-        ph, pw = conv.padding
+        sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
             k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw)
+            conv.fix_grad(w.grad)
             _done(w)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -354,8 +350,7 @@ def conv_act(x, conv, relu: bool = False):
     if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
         return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu)
     k = K(x)
-    sh, sw = conv.stride
-    ph, pw = conv.padding
+    sh, sw, ph, pw = conv.kgeom
     return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,
                       _empty(x), _empty(x))
 
@@ -568,9 +563,13 @@ def count_correct(logits, labels, count: torch.Tensor) -> None:
 
 
 def preprocess(img_u8, out_hw, mean, std, mode: int = 0, cpad: int = 3,
-               out_dtype=torch.bfloat16):
+               out_dtype=torch.bfloat16, pad=None):
+    """u8 [B,H,W,3] -> resized, normalized NHWC with ``cpad`` channels, optionally on a
+    zero-bordered canvas ``pad`` = (top, bottom, left, right) (the pre-padded input layout
+    of a pixel-pair stem, ``models.layers.Conv2d.input_spec``)."""
     k = K(img_u8)
+    pad = list(pad) if pad else []
     if img_u8.is_cuda:
-        return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad)
+        return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad, pad)
     return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad,
-                        out_dtype)
+                        out_dtype, pad)

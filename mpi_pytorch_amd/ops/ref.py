@@ -331,8 +331,9 @@ def sgd_step(master, grad, buf, shadow, step_t, lr, momentum, dampening, wd, nes
 
 
 # ------------------------------------------------------------------------ preprocessing
-def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype):
-    """u8 NHWC [B,H,W,3] -> normalized NHWC [B,oh,ow,cpad] (zero padded channels).
+def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype, pad=None):
+    """u8 NHWC [B,H,W,3] -> normalized NHWC [B,oh,ow,cpad] (zero padded channels), on a
+    zero-bordered canvas when pad = (top, bottom, left, right).
 
     mode 0: bilinear, no antialias  (train path: ToTensor -> Resize on tensor, main.py:62-65)
     mode 1: bicubic with antialias  (eval path: PIL resize, evaluation_pipeline.py:89)
@@ -349,6 +350,9 @@ def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype):
     x = _nhwc((x - m) / s)
     if cpad > 3:
         x = F.pad(x, (0, cpad - 3))
+    if pad:
+        t, b, l, r = pad
+        x = F.pad(x, (0, 0, l, r, t, b))
     return x.to(out_dtype)
 
 

@@ -577,6 +577,26 @@ def test_preprocess(gpu, mode, src, dst):
     assert float(out[..., 3:].float().abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("cpad,pad", [(4, (3, 3, 3, 3)), (4, (0, 0, 0, 1)), (8, (1, 2, 3, 4)),
+                                      (3, (2, 0, 0, 2))])
+def test_preprocess_canvas(gpu, mode, cpad, pad):
+    """Zero-bordered canvas output (pixel-pair stem layout): 8-B stores for 4 channels,
+    16-B for 8, scalar otherwise; border and padding channels exactly zero."""
+    img = torch.randint(0, 256, (2, 50, 60, 3), dtype=torch.uint8, device=gpu)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    out = C().preprocess(img, 40, 44, list(mean), list(std), mode, cpad, list(pad))
+    r = ref.preprocess(img, 40, 44, mean, std, mode, cpad, torch.float32, pad)
+    t, b, l, rr = pad
+    assert out.shape == (2, 40 + t + b, 44 + l + rr, cpad)
+    assert float((out.float() - r).abs().max()) < 0.05
+    if cpad > 3:
+        assert float(out[..., 3:].float().abs().max()) == 0.0
+    inner = torch.zeros_like(out, dtype=torch.bool)
+    inner[:, t:t + 40, l:l + 44] = True
+    assert float(out.float().masked_fill(inner, 0).abs().max()) == 0.0
+
+
 def test_dropout(gpu):
     x = torch.ones(1 << 16, device=gpu, dtype=torch.bfloat16)
     y, m = C().dropout_fwd(x, 0.5, 7, 1)

@@ -193,3 +193,61 @@ def test_grad_join_order_independent(order):
     r1 = Fn._dgrad_joined(ref, j, dz, calls[1][0], (10, 10), calls[1][1], None)
     assert j.partial is None
     assert torch.allclose(r1, exp, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("k,s,p,hw", [(7, 2, 3, (32, 32)), (7, 2, 3, (33, 35)), (7, 2, 0, (31, 30)),
+                                      (3, 2, 0, (29, 31)), (4, 2, 1, (20, 22))])
+def test_pixel_pair_stem_matches_conv2d(k, s, p, hw):
+    """Pixel-pair stem (4-channel canvas viewed as 8-channel pixel pairs, stride-1 conv
+    with a ceil(S/2)-wide kernel) == the image conv, forward and weight gradient, from
+    both a raw 3-channel image and the pre-padded canvas of input_spec."""
+    from mpi_pytorch_amd.models.layers import Conv2d
+    from mpi_pytorch_amd.parallel import ParamArena
+    from mpi_pytorch_amd.ops import functional as Fn
+    from mpi_pytorch_amd.ops import ref
+    torch.manual_seed(0)
+    conv = Conv2d(3, 16, k, s, p, bias=False)
+    assert conv.pair
+    ParamArena(torch.nn.ModuleList([conv]), "cpu")
+    w = conv.state_dict()["weight"]  # OIHW [16, 3, k, k]
+    H, W = hw
+    x = torch.randn(2, H, W, 3)
+    y_ref = F.conv2d(x.permute(0, 3, 1, 2), w, stride=s, padding=p)
+    # raw image path (converted by fit_input)
+    conv.weight.grad.zero_()
+    y = Fn.conv_act(x, conv)
+    assert torch.allclose(y.permute(0, 3, 1, 2), y_ref, atol=1e-4, rtol=1e-4)
+    # canvas path: what the preprocess kernel writes
+    spec = conv.input_spec(hw)
+    t, b, l, r = spec["pad"]
+    canvas = F.pad(F.pad(x, (0, 1)), (0, 0, l, r, t, b))
+    y2 = Fn.conv_act(canvas, conv)
+    assert torch.equal(y2, y)
+    # weight gradient through the pair layout, exported back to OIHW
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(False)
+    wr = w.clone().requires_grad_(True)
+    (F.conv2d(xr, wr, stride=s, padding=p) * g.permute(0, 3, 1, 2)).sum().backward()
+    gw = conv._exp(conv.weight.grad)
+    assert torch.allclose(gw, wr.grad, atol=1e-3, rtol=1e-3)
+    # the stored padding (4th channel; column past an odd kernel) holds exactly zero grad
+    full = conv.weight.grad.view(16, k, conv.sp, 2, 4)
+    assert float(full[..., 3].abs().max()) == 0.0
+    if k % 2:
+        assert float(full[:, :, -1, 1].abs().max()) == 0.0
+    # preprocess writes the same canvas
+    img = torch.randint(0, 256, (2, H, W, 3), dtype=torch.uint8)
+    a = ref.preprocess(img, H, W, [0.5] * 3, [0.25] * 3, 0, 4, torch.float32, spec["pad"])
+    b_ = F.pad(F.pad(ref.preprocess(img, H, W, [0.5] * 3, [0.25] * 3, 0, 3, torch.float32),
+                     (0, 1)), (0, 0, l, r, t, b))
+    assert torch.equal(a, b_)
+
+
+def test_pixel_pair_stem_state_dict_roundtrip():
+    from mpi_pytorch_amd.models.layers import Conv2d
+    conv = Conv2d(3, 8, 7, 2, 3, bias=False)
+    w = torch.randn(8, 3, 7, 7)
+    conv.load_state_dict({"weight": w})
+    assert torch.equal(conv.state_dict()["weight"], w)
+    assert tuple(conv.weight.shape) == (8, 7, 4, 8)
