@@ -105,6 +105,13 @@ void igemm_set_engine(int engine);
 void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
 void igemm_set_dma_uni(int on);  // LDS-DMA uniform-tap fast path (default on)
 bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path on)
+// conv_halo.hip: halo-staged direct 3x3 / stride-1 conv (forward and stride-1 dgrad with
+// a K-contiguous B); run_rows / the fused-reduction dgrad take it when conv3_halo_ok
+bool conv3_halo_ok(const IGemmArgs& a);
+int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
+constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
+void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
+bool igemm_halo_enabled();
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

@@ -1,0 +1,468 @@
+// Halo-staged direct 3x3 / stride-1 convolution for gfx950 (MI355X / CDNA4): the forward
+// and the stride-1 dgrad of every 3x3 "same" conv (ResNet-18 has 13
+// such convs = 26 of its 34 rows-GEMM launches per step).
+//
+// Why a second engine: the implicit GEMM (igemm_dma.hip) gathers a fresh A tile for every
+// tap, so each input pixel crosses L2 -> LDS nine times and the weight tile once per
+// 128-row M-tile: 21 (64-channel) to 32 (128-channel) MAC per staged byte.  The measured
+// L2 -> LDS gather rate is ~30 B/clk/CU (MI355X_MICROARCH.md "Indexed rows") against 2048
+// bf16 MAC/clk/CU of MFMA, so those layers ran at 16-25 % of the matrix peak
+// (profiles/conv_kernels_tuned_b256.txt).  Here a block stages, per 32-channel chunk, the
+// input rows its 256 output pixels touch plus a one-pixel halo ONCE, and runs all nine taps
+// out of LDS: 67-77 MAC per staged byte, and 185 when the whole weight tile stays resident.
+//
+//  * LDS halo image: "slots" of W+2 pixels (zero column left and right), one input row per
+//    slot, one zero slot between consecutive images, so every tap is a uniform pixel offset
+//    dh*(W+2)+dw and no lane ever tests a border.  Slot s of a tile whose first output row
+//    is (img0, oh0) holds input row v = s + oh0 - 1 of the image sequence with period H+1
+//    (row H of each period = the zero separator).
+//  * Pixel rows are 64 B (32 bf16 channels, four 16-B chunks).  Chunk c of row r sits at
+//    position c ^ (2 * ((r >> 2) & 1)): a fragment read (ds_read_b128, lane l: row l%16,
+//    chunk l/16) of ANY 16 consecutive rows - the taps shift halo rows by arbitrary
+//    amounts - touches every bank once per lane group (brute-force checked for all 64
+//    alignments; the engine's aligned-row swizzle kc_off conflicts 2-way off alignment).
+//    The weight image [tap][64 cols][32 k] uses the same rows and swizzle.
+//  * Staging is buffer_load_dwordx4 ... lds: the swizzle moves to the source (lane on
+//    chunk position q of row r fetches chunk q ^ (2 * ((r>>2)&1))), border / out-of-tensor lanes
+//    get an offset past num_records and the hardware returns zeros, the chunk step moves the
+//    descriptor base (scalar), so a DMA costs no VALU in the loop.
+//  * Persistent blocks (one 4-wave block per CU, 146 KiB LDS): work items (tile, chunk) run
+//    through a 2-stage ring, item k+1's DMAs overlap item k's 144 MFMAs per wave and the
+//    epilogue of the previous tile; XCD x owns a contiguous share of the tile list.
+//  * WRES (64-wide outputs, <= 64 input channels, e.g. ResNet layer1): the 64 x 9 x C weight
+//    tile is loaded once per block and only the halo streams.
+//  * Epilogue = the rows engine's (igemm_common.h): bias, ReLU, BN statistics slab, fused
+//    BN-backward reduction, accumulate (GradJoin).
+#include <algorithm>
+#include <cstdlib>
+#include "igemm_common.h"
+
+namespace mpa {
+
+constexpr int HB_BM = 256, HB_BN = 64, HB_NW = 4;
+constexpr int HB_HIW = 9;                       // halo DMA instructions per wave per chunk
+constexpr int HB_HPX = 16 * HB_NW * HB_HIW;     // 576 halo pixels per chunk
+constexpr int HB_HBYTES = HB_HPX * 64;          // 36 KiB
+constexpr int HB_WIW = 9;                       // weight DMA instructions per wave per chunk
+constexpr int HB_WBYTES = 9 * HB_BN * 64;       // 36 KiB: [tap][64 cols][32 k]
+constexpr int HB_RED = HB_NW * HB_BN * 2 * 4;   // epilogue cross-wave statistics
+constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED;  // 149,504 B
+
+struct HaloPlan {
+  int toff[9];          // halo pixel offset of tap t: dh * (W + 2) + dw, dh/dw in {-1,0,1}
+  int btoff[9];         // byte offset of tap t's weight row segment: bt[t] * aC * 2
+  uint32_t mag_w, mag_w2, mag_h1, mag_hw;  // floor(2^32 / d) + 1: exact n / d for n*d < 2^32
+  int tiles_m, tiles_total, cc;
+  uint32_t a_bytes, b_bytes;
+};
+
+__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t mag) { return __umulhi(n, mag); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void halo_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
+  return __builtin_bit_cast(bf16x8, *LDS_PTR(const u32x4, lds_byte));
+}
+
+// Epilogue of one 256 x 64 tile (lane: 4 consecutive channels n = n0 + 16 jn + 4 (lane/16)
+// of pixel m = m0 + 64 wave + 16 i + lane%16).  Leaner than the rows engine's: N % 64 == 0
+// (no column guards), dense [M][ldc] output with 32-bit offsets, per-column operands held in
+// registers for the block's whole life (its column tile never changes), and the BN
+// statistics accumulated in registers across ALL of the block's tiles (ss/sq), reduced and
+// written once per block by halo_stats_flush - the per-tile shuffle tree and slab write of
+// rows_epilogue cost more VALU than the tile's 288-1152 MFMAs per wave.
+__device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, f32x4 (&acc)[4][4], int m0,
+                                              int n0, int wave, int lane, const f32x4 (&colb)[4],
+                                              const f32x4 (&cols)[4], float (&ss)[4][4],
+                                              float (&sq)[4][4]) {
+  const int nl = (lane >> 4) * 4;
+  bf16_t* const out = (bf16_t*)p.C;
+  const bool stats = p.stats != nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wave * 64 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+    const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
+    uint2 zz[4], yy[4], oo[4];
+    if (p.ep_bnred) {
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) {
+        zz[jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
+        yy[jn] = p.ep_y ? *(const uint2*)(p.ep_y + orow + jn * 16) : make_uint2(0x3f803f80u, 0x3f803f80u);
+      }
+    } else if (p.beta) {
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) oo[jn] = *(const uint2*)(out + orow + jn * 16);
+    }
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      float v[4];
+      if (p.ep_bnred) {
+        // dy (bf16-rounded) masked by ReLU(y) > 0; reduction (sum g, sum g * xhat)
+        const uint32_t yw[4] = {yy[jn].x << 16, yy[jn].x & 0xffff0000u, yy[jn].y << 16,
+                                yy[jn].y & 0xffff0000u};
+        const float zr[4] = {__uint_as_float(zz[jn].x << 16), __uint_as_float(zz[jn].x & 0xffff0000u),
+                             __uint_as_float(zz[jn].y << 16), __uint_as_float(zz[jn].y & 0xffff0000u)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = bf2f(f2bf(acc[i][jn][r]));
+          v[r] = (__uint_as_float(yw[r]) > 0.f) ? d : 0.f;
+          ss[jn][r] += v[r];
+          sq[jn][r] += v[r] * (zr[r] - colb[jn][r]) * cols[jn][r];
+        }
+      } else {
+        float old[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.beta) {
+          old[0] = __uint_as_float(oo[jn].x << 16); old[1] = __uint_as_float(oo[jn].x & 0xffff0000u);
+          old[2] = __uint_as_float(oo[jn].y << 16); old[3] = __uint_as_float(oo[jn].y & 0xffff0000u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[i][jn][r] + colb[jn][r] + old[r];
+          v[r] = p.relu ? fmaxf(t, 0.f) : t;
+        }
+      }
+      const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+      *(uint2*)(out + orow + jn * 16) = make_uint2(lo, hi);
+      if (stats && !p.ep_bnred) {
+        // shifted statistics of the bf16-rounded values BN will read
+        const float rv[4] = {__uint_as_float(lo << 16) - cols[jn][0],
+                             __uint_as_float(lo & 0xffff0000u) - cols[jn][1],
+                             __uint_as_float(hi << 16) - cols[jn][2],
+                             __uint_as_float(hi & 0xffff0000u) - cols[jn][3]};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ss[jn][r] += rv[r];
+          sq[jn][r] += rv[r] * rv[r];
+        }
+      }
+    }
+  }
+}
+
+// Block-level statistics: reduce the per-lane sums of the block's tiles and write slab row
+// blockIdx.x ([2][N]: the block's 64 columns, zeros elsewhere, so every row is complete);
+// block 0 zeroes the final-sum vector the slab reduction accumulates into.
+__device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)[4][4],
+                                                 float (&sq)[4][4], char* red, int n0, int wave,
+                                                 int tid) {
+  const int lane = tid & 63, nl = (lane >> 4) * 4;
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = ss[jn][r], b = sq[jn][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+      }
+      ss[jn][r] = a;
+      sq[jn][r] = b;
+    }
+  float* rd = (float*)red;
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rd[(wave * 64 + jn * 16 + nl + r) * 2] = ss[jn][r];
+        rd[(wave * 64 + jn * 16 + nl + r) * 2 + 1] = sq[jn][r];
+      }
+  }
+  __syncthreads();
+  float* row = p.stats + (size_t)blockIdx.x * 2 * p.N;
+  for (int c = tid; c < p.N; c += 256) {
+    float a = 0.f, b = 0.f;
+    if (c >= n0 && c < n0 + 64) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        a += rd[(w * 64 + c - n0) * 2];
+        b += rd[(w * 64 + c - n0) * 2 + 1];
+      }
+    }
+    row[c] = a;
+    row[p.N + c] = b;
+    if (blockIdx.x == 0) {
+      p.stats_sums[c] = 0.f;
+      p.stats_sums[p.N + c] = 0.f;
+    }
+  }
+}
+
+template <bool WRES>
+__global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
+  __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
+  char* const hal = smem;
+  char* const wst = smem + 2 * HB_HBYTES;
+  char* const red = smem + 2 * HB_HBYTES + 2 * HB_WBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.aH, W = p.aW, HW = H * W, W2 = W + 2, aC = p.aC;
+  const int nimg = p.M / HW;
+  const int jq = lane >> 4, l15 = lane & 15;
+
+  // persistent tile list: XCD x = blockIdx % 8 owns tiles [x*T/8, (x+1)*T/8); the host
+  // makes G8 a multiple of tiles_n, so a block's tiles all share one column tile nt
+  const int T = h.tiles_total;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, G8 = gridDim.x >> 3;
+  const int tbeg = (int)((int64_t)xcd * T / 8), tend = (int)((int64_t)(xcd + 1) * T / 8);
+  const int ntiles = tbeg + loc < tend ? (tend - tbeg - loc + G8 - 1) / G8 : 0;
+  const int CC = h.cc;
+  const int nitems = ntiles * CC;
+  const int nt = (tbeg + loc) % p.tiles_n;
+  const int n0 = nt * HB_BN;
+
+  // per-column epilogue operands of the block's 64 columns: bias (or BN mean) and stats
+  // shift (or BN rstd)
+  f32x4 colb[4], cols[4];
+  {
+    const bool bnred = p.ep_bnred != 0;
+    const float* bsrc = bnred ? p.ep_mean : p.bias;
+    const float* ssrc = bnred ? p.ep_rstd : p.stats_shift;
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      const int n = n0 + jn * 16 + jq * 4;
+      colb[jn] = bsrc ? *(const f32x4*)(bsrc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      cols[jn] = ssrc ? *(const f32x4*)(ssrc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float ss[4][4], sq[4][4];
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { ss[jn][r] = 0.f; sq[jn][r] = 0.f; }
+
+  // ---- halo lanes: tile-independent (slot, column, logical chunk) of each DMA lane
+  uint32_t hsc[HB_HIW];  // slot | (col + 1) << 10 | chunk << 18
+#pragma unroll
+  for (int j = 0; j < HB_HIW; ++j) {
+    const uint32_t hp = 16 * (wave * HB_HIW + j) + (lane >> 2);
+    const uint32_t s = udiv(hp, h.mag_w2);
+    const uint32_t colp = hp - s * W2;
+    const uint32_t lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
+    hsc[j] = s | (colp << 10) | (lc << 18);
+  }
+  // ---- weight lanes: row r = 16 q + lane/4 of the [tap][64][32] image, tap = q / 4; the
+  // block's column tile is fixed, so the offsets are too
+  uint32_t wv[HB_WIW];
+#pragma unroll
+  for (int j = 0; j < HB_WIW; ++j) {
+    const int q = wave * HB_WIW + j;
+    const int r = 16 * q + (lane >> 2);
+    const int n = r & 63;
+    const int lc = (lane & 3) ^ (((r >> 2) & 1) << 1);
+    wv[j] = (n0 + n < p.N) ? (uint32_t)(n0 + n) * p.ldb * 2 + h.btoff[q >> 2] + lc * 16
+                           : 0x80000000u;
+  }
+  uint32_t hv[HB_HIW];
+  auto tile_of = [&](int tk) { return tbeg + loc + tk * G8; };
+  auto prep_tile = [&](int tile) {  // DMA source offsets of a tile's halo
+    const int mt = tile / p.tiles_n;
+    const int m0 = mt * HB_BM;
+    const int img0 = m0 / HW;
+    const int oh0 = (m0 - img0 * HW) / W;
+#pragma unroll
+    for (int j = 0; j < HB_HIW; ++j) {
+      const int s = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
+      const int v = s + oh0 - 1;                                     // >= -1
+      const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;  // floor(v / (H+1))
+      const int row = v - d * (H + 1);
+      const int img = img0 + d;
+      const bool ok = row < H && (unsigned)col < (unsigned)W && img < nimg;
+      hv[j] = ok ? ((((uint32_t)img * H + row) * W + col) * aC) * 2 + (hsc[j] >> 18) * 16
+                 : 0x80000000u;
+    }
+  };
+  auto issue = [&](int cc, int stage) {
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
+    char* hdst = hal + stage * HB_HBYTES + wave * HB_HIW * 1024;
+#pragma unroll
+    for (int j = 0; j < HB_HIW; ++j) buf_lds16(ra, hdst + j * 1024, hv[j]);
+    if constexpr (!WRES) {
+      const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+      char* wdst = wst + stage * HB_WBYTES + wave * HB_WIW * 1024;
+#pragma unroll
+      for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
+    }
+  };
+
+  if (nitems > 0) {
+    if constexpr (WRES) {  // whole weight tile (tiles_n == 1, CC <= 2) once per block
+      for (int cc = 0; cc < CC; ++cc) {
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+        char* wdst = wst + cc * HB_WBYTES + wave * HB_WIW * 1024;
+#pragma unroll
+        for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
+      }
+    }
+    prep_tile(tile_of(0));
+    issue(0, 0);
+  }
+
+  // B fragment byte offsets (tap 0, column group 0): row l15 of the [tap][64][32] image
+  const int boff = l15 * 64 + ((jq ^ ((l15 >> 1) & 2)) << 4);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int xb[4];  // 64 * halo pixel + 16 * chunk of this lane's output row, per row fragment
+  for (int k = 0; k < nitems; ++k) {
+    const int st = k & 1;
+    const int tk = k / CC, cc = k - tk * CC;
+    if (k + 1 < nitems) {
+      const int cc1 = cc + 1 == CC ? 0 : cc + 1;
+      if (cc1 == 0) prep_tile(tile_of(tk + 1));
+      issue(cc1, st ^ 1);
+      halo_wait_barrier<WRES ? HB_HIW : HB_HIW + HB_WIW>();
+    } else {
+      halo_wait_barrier<0>();
+    }
+    const int tile = tile_of(tk);
+    const int m0 = (tile / p.tiles_n) * HB_BM;
+    if (cc == 0) {
+      const int img0 = m0 / HW;
+      const int r0 = m0 - img0 * HW;
+      const int oh0 = r0 / W;
+      const int mlast = p.M - 1 - img0 * HW;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t n = (uint32_t)min(r0 + wave * 64 + i * 16 + l15, mlast);
+        const uint32_t di = udiv(n, h.mag_hw);
+        const uint32_t rem = n - di * HW;
+        const uint32_t oh = udiv(rem, h.mag_w);
+        const uint32_t ow = rem - oh * W;
+        xb[i] = ((((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1) << 6) + (jq << 4);
+      }
+    }
+    // A: X = 64 * pixel + 16 * chunk (+ stage); the swizzle flips bit 5 by pixel bit 2
+    // (= X bit 8): 3 VALU per fragment and tap.  B: per-lane base + immediate offsets.
+    const int hbase = st * HB_HBYTES;
+    const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
+    bf16x8 af[2][4], bfr[2][4];
+    auto load = [&](int t, int b) {
+      const int add = hbase + 64 * h.toff[t];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int x = xb[i] + add;
+        af[b][i] = frag16(hal + (x ^ ((x >> 3) & 32)));
+      }
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) bfr[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) load(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn)
+          acc[i][jn] = mfma16(bfr[t & 1][jn], af[t & 1][i], acc[i][jn]);
+    }
+    if (cc == CC - 1) {
+      halo_epilogue(p, acc, m0, n0, wave, lane, colb, cols, ss, sq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // stage st is free for item k + 2
+  }
+  if (p.stats) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
+}
+
+// ------------------------------------------------------------------------------ host
+static bool g_halo = [] {
+  const char* e = getenv("MPA_HALO");
+  return !(e && e[0] == '0');
+}();
+void igemm_set_halo(int on) { g_halo = on != 0; }
+bool igemm_halo_enabled() { return g_halo; }
+
+static uint32_t magic(uint32_t d) { return (uint32_t)((1ull << 32) / d + 1); }
+
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+bool conv3_halo_ok(const IGemmArgs& a) {
+  if (!g_halo || a.nphase > 0 || a.stap || a.T != 9 || a.Uh != 1 || a.Uw != 1) return false;
+  if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.N % HB_BN != 0 || a.M <= 0)
+    return false;
+  // dense [M][ldc] output (stride-1 geometry), 32-bit element offsets in the epilogue
+  if (a.dH != a.oH || a.dW != a.oW || a.Uoh != 1 || a.Uow != 1 || a.Poh != 0 || a.Pow != 0)
+    return false;
+  if ((int64_t)a.M * a.ldc >= (1ll << 31) || a.ldc < a.N) return false;
+  if (a.Ktot != 9 * a.aC) return false;
+  for (int t = 0; t < 9; ++t) {
+    const int dh = a.Oh + a.taps.dh[t], dw = a.Ow + a.taps.dw[t];
+    if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return false;
+  }
+  const int64_t HW = (int64_t)a.aH * a.aW;
+  if (a.M % HW != 0 || HW + HB_BM >= 65536 || a.aW + 2 > 255) return false;
+  if ((int64_t)a.M * a.aC * 2 >= (1ll << 31)) return false;
+  if ((int64_t)a.N * a.ldb * 2 >= (1ll << 31)) return false;
+  // halo slots of any 256-pixel tile: rows touched + 2 halo rows + image separators
+  const int64_t rows = (HB_BM - 1 + a.aW - 1) / a.aW + 1;
+  const int64_t seps = (HB_BM - 1) / HW + 1;
+  return (rows + 2 + seps) * (a.aW + 2) <= HB_HPX;
+}
+
+// Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
+// returns the number of statistics-slab rows written (one per block, <= HALO_MAX_ROWS).
+int conv3_halo(IGemmArgs a, hipStream_t s) {
+  HaloPlan h{};
+  const int W2 = a.aW + 2;
+  for (int t = 0; t < 9; ++t) {
+    h.toff[t] = (a.Oh + a.taps.dh[t]) * W2 + (a.Ow + a.taps.dw[t]);
+    h.btoff[t] = a.taps.bt[t] * a.aC * 2;
+  }
+  h.mag_w = magic(a.aW);
+  h.mag_w2 = magic(W2);
+  h.mag_h1 = magic(a.aH + 1);
+  h.mag_hw = magic(a.aH * a.aW);
+  h.cc = a.aC / 32;
+  h.tiles_m = (a.M + HB_BM - 1) / HB_BM;
+  a.tiles_n = (a.N + HB_BN - 1) / HB_BN;
+  h.tiles_total = h.tiles_m * a.tiles_n;
+  a.tiles_total = h.tiles_total;
+  h.a_bytes = (uint32_t)((int64_t)a.M * a.aC * 2);
+  h.b_bytes = (uint32_t)((int64_t)a.N * a.ldb * 2);
+  // persistent grid: G8 blocks per XCD, a multiple of tiles_n (fixed column tile per block)
+  int g8 = std::min(std::min(num_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
+  g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
+  const int grid = 8 * g8;
+  if (a.tiles_n == 1 && h.cc <= 2)
+    hipLaunchKernelGGL(conv3_halo_kernel<true>, dim3(grid), dim3(256), 0, s, a, h);
+  else
+    hipLaunchKernelGGL(conv3_halo_kernel<false>, dim3(grid), dim3(256), 0, s, a, h);
+  return grid;
+}
+
+}  // namespace mpa

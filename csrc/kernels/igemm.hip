@@ -627,13 +627,24 @@ int64_t igemm_ws_floats(int M, int N, int Ktot) {
 
 // statistics slab rows: one per 128-row M-tile (the smallest BM of any plan) or per
 // splitk_finalize block row (<= 64), then the [2][N] sums
-static int64_t slab_rows_max(int M) { return std::max((M + 127) / 128, 64); }
+static int64_t slab_rows_max(int M) {
+  return std::max<int64_t>((M + 127) / 128, std::max(64, HALO_MAX_ROWS));
+}
 
 int64_t igemm_slab_floats(int M, int N) { return slab_rows_max(M) * 2 * N + 2 * N; }
 
 static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
   int BM, BN, splits;
   const bool dma = use_dma(vw);
+  if (dma && bkc && conv3_halo_ok(a)) {  // 3x3 / stride 1: halo-staged direct conv
+    float* stats = a.stats;
+    float* sums = stats ? slab + slab_rows_max(a.M) * 2 * a.N : nullptr;
+    a.stats = stats ? slab : nullptr;
+    a.stats_sums = sums;
+    const int rows = conv3_halo(a, s);
+    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s);
+    return;
+  }
   rows_plan(a, BM, BN, splits, ws != nullptr, dma);
   const int tiles_m = (a.M + BM - 1) / BM;
   void* final_out = a.C;
@@ -684,7 +695,8 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc) {
 
 // dgrad + fused BN-backward reduction (LDS-DMA engine only: one launch, dense slab rows)
 int64_t igemm_bnred_slab_floats(int M, int N, int nphase) {
-  const int64_t rows = (int64_t)((M + 127) / 128 + 1) * std::max(nphase, 1);
+  const int64_t rows = std::max<int64_t>((int64_t)((M + 127) / 128 + 1) * std::max(nphase, 1),
+                                         HALO_MAX_ROWS);
   return rows * 2 * N;
 }
 
@@ -722,6 +734,11 @@ void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* s
   a.stats = slab;
   a.stats_sums = sums;
   int BM, BN, rows;
+  if (a.nphase == 0 && bkc && conv3_halo_ok(a)) {
+    rows = conv3_halo(a, s);
+    slab_reduce(slab, rows, 2 * a.N, sums, false, s);
+    return;
+  }
   if (a.nphase > 0) {
     rows = plan_phases(a, BM, BN);
   } else {

@@ -50,17 +50,30 @@ def _pair(v):
     return v if isinstance(v, tuple) else (v, v)
 
 
-@pytest.fixture(params=[(2, 1), (2, 0), (0, 1)], ids=["dma", "dma-generic", "reg"])
+@pytest.fixture(autouse=True)
+def _halo_off(gpu):
+    """The halo-staged 3x3 kernel (conv_halo.hip) sums K in a different order than the
+    implicit-GEMM engines; it runs only where a test enables it (engine "dma-halo",
+    test_conv_halo_*), so the bitwise cross-engine checks compare like with like."""
+    C().igemm_set_halo(0)
+    yield
+    C().igemm_set_halo(1)
+
+
+@pytest.fixture(params=[(2, 1, 1), (2, 1, 0), (2, 0, 0), (0, 1, 0)],
+                ids=["dma-halo", "dma", "dma-generic", "reg"])
 def engine(request, gpu):
-    """Run a GEMM test on the LDS-DMA engine (uniform-tap fast path and generic gather)
-    and on the register-staged engine."""
+    """Run a GEMM test on the LDS-DMA engine (with and without the halo-staged 3x3/s1
+    kernel; uniform-tap fast path and generic gather) and on the register-staged engine."""
     prev = C().igemm_engine()
-    eng, uni = request.param
+    eng, uni, halo = request.param
     C().igemm_set_engine(eng)
     C().igemm_set_dma_uni(uni)
+    C().igemm_set_halo(halo)
     yield eng
     C().igemm_set_engine(prev)
     C().igemm_set_dma_uni(1)
+    C().igemm_set_halo(0)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -121,7 +134,10 @@ def test_conv_dgrad_accumulate(gpu, engine, case):
         acc2 = acc0.clone()
         C().conv_dgrad(dy, w, H, W, st, st, ph, pw, wt, acc2)
         torch.cuda.synchronize()
-        assert torch.equal(acc2, out)
+        if C().igemm_halo_enabled():  # 3x3/s1 from wt runs on the halo kernel: other K order
+            assert rel(acc2, out) < 1e-2
+        else:
+            assert torch.equal(acc2, out)
 
 
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0])
@@ -140,7 +156,10 @@ def test_conv_dgrad_transposed_weight(gpu, engine, case):
     dx = C().conv_dgrad(dy, w, H, W, st, st, ph, pw)
     dxt = C().conv_dgrad(dy, w, H, W, st, st, ph, pw, wt)
     torch.cuda.synchronize()
-    assert torch.equal(dx, dxt), rel(dxt, dx)
+    if C().igemm_halo_enabled():
+        assert rel(dxt, dx) < 1e-2
+    else:
+        assert torch.equal(dx, dxt), rel(dxt, dx)
 
 
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 3, 1, 1), (2, 14, 14, 64, 128, 3, 3, 2, 1),
@@ -175,6 +194,90 @@ def test_conv_dgrad_fused_bn_reduction(gpu, case):
     dz, _ = C().bn_bwd_apply(g, z, e, mean, rstd, gamma, dg, db, sums, True, False)
     dzr, _ = ref.bn_bwd(dx, z, y, mean, rstd, gamma, dg2, db2, True)
     assert rel(dz, dzr) < 3e-2 and rel(dg, dg2) < 2e-2 and rel(db, db2) < 2e-2
+
+
+HALO_CASES = [
+    # N, H, W, C, K: 3x3 / stride 1 / pad 1
+    (2, 56, 56, 64, 64),     # ResNet layer1: resident weights (N = 64, C <= 64)
+    (3, 28, 28, 128, 128),   # layer2: two N-tiles, streamed weights
+    (5, 14, 14, 256, 256),   # layer3: 256-pixel tiles cross image borders
+    (7, 7, 7, 512, 512),     # layer4: a tile spans 6 images (separator slots)
+    (3, 9, 11, 96, 128),     # odd W, 3 chunks, two N-tiles, partial last M-tile
+    (1, 5, 3, 32, 64),       # single chunk, tiny image, one partial M-tile
+    (2, 35, 35, 64, 96),     # Inception-style odd spatial size
+]
+
+
+def _halo_pair(fn):
+    """(halo kernel result, implicit-GEMM result) of fn()."""
+    C().igemm_set_halo(1)
+    a = fn()
+    C().igemm_set_halo(0)
+    b = fn()
+    torch.cuda.synchronize()
+    return a, b
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_fwd(gpu, case):
+    """Halo-staged 3x3/s1 forward (bias, ReLU, shifted BN statistics) == implicit GEMM and
+    the fp32 oracle."""
+    torch.manual_seed(21)
+    N, H, W, Cc, K = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * Cc))
+    b = torch.randn(K, device=gpu)
+    shift = torch.randn(K, device=gpu) * 0.1
+
+    def run():
+        st = torch.zeros(2, K, device=gpu)
+        return C().conv_fwd(x, w, b, 1, 1, 1, 1, True, st, shift), st
+
+    (y, st), (y0, st0) = _halo_pair(run)
+    str_ = torch.zeros(2, K, device=gpu)
+    yr = ref.conv_fwd(x, w, b, 1, 1, 1, 1, True, str_, shift)
+    assert rel(y, y0) < 1e-2 and rel(st, st0) < 1e-3
+    assert rel(y, yr) < 2e-2 and rel(st, str_) < 2e-2
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_dgrad(gpu, case):
+    """Stride-1 dgrad from the transposed weight on the halo kernel: plain, accumulating
+    (GradJoin) and with the fused BN-backward reduction, against the oracle."""
+    torch.manual_seed(22)
+    N, H, W, Cc, K = case
+    dy = bf(N, H, W, K, dev=gpu)
+    w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * K))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+    acc0 = bf(N, H, W, Cc, dev=gpu)
+    dx, dx0 = _halo_pair(lambda: C().conv_dgrad(dy, w, H, W, 1, 1, 1, 1, wt))
+    dxr = ref.conv_dgrad(dy, w, H, W, 1, 1, 1, 1)
+    assert rel(dx, dx0) < 1e-2 and rel(dx, dxr) < 2e-2
+    acc, _ = _halo_pair(lambda: C().conv_dgrad(dy, w, H, W, 1, 1, 1, 1, wt, acc0.clone()))
+    assert rel(acc, acc0.float() + dxr.float()) < 2e-2
+    z = bf(N, H, W, Cc, dev=gpu, scale=2.0)
+    mean = torch.randn(Cc, device=gpu) * 0.3
+    rstd = torch.rand(Cc, device=gpu) + 0.5
+    y = torch.relu(z.float() - 0.2).to(torch.bfloat16)
+    (g, sums), (g0, sums0) = _halo_pair(
+        lambda: C().conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, wt, z, y, mean, rstd))
+    gr, sr = ref.conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, None, z, y, mean, rstd)
+    assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
+    assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+
+
+def test_conv_halo_repeatable(gpu):
+    """Persistent 2-stage ring: repeated launches are bitwise identical (race screen)."""
+    torch.manual_seed(23)
+    x = bf(16, 28, 28, 128, dev=gpu)
+    w = bf(128, 3, 3, 128, dev=gpu, scale=1.0 / math.sqrt(9 * 128))
+    e = torch.empty(0, device=gpu)
+    C().igemm_set_halo(1)
+    outs = [C().conv_fwd(x, w, e, 1, 1, 1, 1, False, torch.zeros(2, 128, device=gpu), e)
+            for _ in range(4)]
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 def test_transpose_krsc_and_linear_dgrad_transposed(gpu):

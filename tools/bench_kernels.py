@@ -4,7 +4,7 @@ shapes at a given batch, reported as TFLOP/s.
     python tools/bench_kernels.py [batch] [iters]          engines 0 (register) and 1/2 (DMA)
     python tools/bench_kernels.py [batch] [iters] sweep    every tile on the DMA engine
 
-MPA_BENCH_ENGINES=0,1,2 selects engines; MPA_IGEMM_OCC=2|3|4 the register engine's
+MPA_BENCH_ENGINES=0,1,1h,2 selects engines ("1h": halo 3x3/s1 kernel on); MPA_IGEMM_OCC=2|3|4 the register engine's
 occupancy target.  Sweep rows print each tile's time (us) with its split count forced to
 auto; the `auto` column is what the planner picks."""
 import os
@@ -82,10 +82,14 @@ if SWEEP:
         C.igemm_force_tile(0, 0, 0)
     sys.exit(0)
 
-ENGINES = [int(e) for e in os.environ.get("MPA_BENCH_ENGINES", "0,1,2").split(",")]
-for eng in ENGINES:
+# "1h": engine 1 with the halo-staged 3x3/s1 kernel (conv_halo.hip) on; plain numbers off
+ENGINES = os.environ.get("MPA_BENCH_ENGINES", "0,1,1h,2").split(",")
+for spec in ENGINES:
+    eng = int(spec.rstrip("h"))
     C.igemm_set_engine(eng)
-    print("== engine %d (%s)" % (eng, ["register", "dma rows", "dma all"][eng]))
+    C.igemm_set_halo(1 if spec.endswith("h") else 0)
+    print("== engine %s (%s%s)" % (spec, ["register", "dma rows", "dma all"][eng],
+                                   " + halo 3x3/s1" if spec.endswith("h") else ""))
     print("occ=%s batch=%d" % (os.environ.get("MPA_IGEMM_OCC", "3"), B))
     tot = [0.0, 0.0, 0.0]
     for name, H, Ci, Co, R, st, pd in SHAPES:

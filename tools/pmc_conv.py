@@ -22,9 +22,10 @@ for name, H, Ci, Co, R, st, pd in LAYERS:
     dw = torch.zeros(Co, R, R, Ci, device=dev)
     e = torch.empty(0, device=dev)
     stats = torch.empty(2, Co, device=dev)
+    wt = w.permute(3, 1, 2, 0).reshape(Ci, R * R, Co).contiguous()  # as training runs dgrad
     for _ in range(3):
         C.conv_fwd(x, w, e, st, st, pd, pd, False, stats, e)
-        C.conv_dgrad(dy, w, H, H, st, st, pd, pd)
+        C.conv_dgrad(dy, w, H, H, st, st, pd, pd, wt)
         C.conv_wgrad(dy, x, dw, st, st, pd, pd)
     torch.cuda.synchronize()
 print("done")
