@@ -35,6 +35,7 @@
 //    BN-backward reduction, accumulate (GradJoin).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include "igemm_common.h"
 
 namespace mpa {
@@ -77,78 +78,95 @@ __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
   return __builtin_bit_cast(bf16x8, *LDS_PTR(const u32x4, lds_byte));
 }
 
-// Epilogue of one 256 x 64 tile (lane: 4 consecutive channels n = n0 + 16 jn + 4 (lane/16)
-// of pixel m = m0 + 64 wave + 16 i + lane%16).  Leaner than the rows engine's: N % 64 == 0
-// (no column guards), dense [M][ldc] output with 32-bit offsets, per-column operands held in
-// registers for the block's whole life (its column tile never changes), and the BN
-// statistics accumulated in registers across ALL of the block's tiles (ss/sq), reduced and
-// written once per block by halo_stats_flush - the per-tile shuffle tree and slab write of
-// rows_epilogue cost more VALU than the tile's 288-1152 MFMAs per wave.
-__device__ __forceinline__ void halo_epilogue(const IGemmArgs& p, f32x4 (&acc)[4][4], int m0,
-                                              int n0, int wave, int lane, const f32x4 (&colb)[4],
-                                              const f32x4 (&cols)[4], float (&ss)[4][4],
-                                              float (&sq)[4][4]) {
-  const int nl = (lane >> 4) * 4;
-  bf16_t* const out = (bf16_t*)p.C;
-  const bool stats = p.stats != nullptr;
+// Epilogue flavours (compile-time, so the fused epilogue below is one straight-line block)
+enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16 };
+
+// Per-tile operands the epilogue reads from memory (accumulate: the old output; fused
+// BN-backward reduction: z and y), loaded right after the tile's last MFMA chunk so they
+// are in registers long before the epilogue runs - a load issued behind the next item's
+// LDS-DMAs would make the in-order vmcnt wait for those DMAs too.
+struct EpiIn {
+  uint2 a[4][4], b[4][4];
+};
+
+template <int EPI>
+__device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m0, int n0,
+                                            int wave, int lane) {
+  if constexpr (!(EPI & (EP_BETA | EP_BNRED))) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wave * 64 + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-    const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
-    uint2 zz[4], yy[4], oo[4];
-    if (p.ep_bnred) {
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) in.a[i][jn] = in.b[i][jn] = make_uint2(0u, 0u);
+  } else {
+    const int nl = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(m0 + wave * 64 + i * 16 + (lane & 15), p.M - 1);  // rows >= M: unused
+      const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
 #pragma unroll
       for (int jn = 0; jn < 4; ++jn) {
-        zz[jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
-        yy[jn] = p.ep_y ? *(const uint2*)(p.ep_y + orow + jn * 16) : make_uint2(0x3f803f80u, 0x3f803f80u);
+        if constexpr (EPI & EP_BNRED) {
+          in.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
+          in.b[i][jn] = p.ep_y ? *(const uint2*)(p.ep_y + orow + jn * 16)
+                               : make_uint2(0x3f803f80u, 0x3f803f80u);
+        } else {
+          in.a[i][jn] = *(const uint2*)((const bf16_t*)p.C + orow + jn * 16);
+        }
       }
-    } else if (p.beta) {
-#pragma unroll
-      for (int jn = 0; jn < 4; ++jn) oo[jn] = *(const uint2*)(out + orow + jn * 16);
     }
+  }
+}
+
+__device__ __forceinline__ float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// Epilogue of one 256 x 64 tile (lane: 4 consecutive channels n = n0 + 16 jn + 4 (lane/16)
+// of pixel m = m0 + 64 wave + 16 i + lane%16).  N % 64 == 0 (no column guards), dense
+// [M][ldc] output with 32-bit offsets, per-column operands in registers for the block's
+// whole life (its column tile never changes), and the BN statistics accumulated in
+// registers across ALL of the block's tiles (ss/sq), reduced and written once per block by
+// halo_stats_flush.  epi_frag handles fragment (i, jn); the fused form calls it between the
+// next tile's taps (branch-free), the MASKED form after the block's last tile.
+template <int EPI, bool FULL>
+__device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, uint2 ia, uint2 ib,
+                                         bool ok, int jn, uint32_t orow, const f32x4& cb,
+                                         const f32x4& cs, float (&ssj)[4], float (&sqj)[4]) {
+  bf16_t* const out = (bf16_t*)p.C;
+  float v[4];
+  if constexpr (EPI & EP_BNRED) {
+    // dy (bf16-rounded) masked by ReLU(y) > 0; reduction (sum g, sum g * xhat)
+    const uint2 z = ia, y = ib;
+    const float zr[4] = {lo_f(z.x), hi_f(z.x), lo_f(z.y), hi_f(z.y)};
+    const float yr[4] = {lo_f(y.x), hi_f(y.x), lo_f(y.y), hi_f(y.y)};
 #pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      float v[4];
-      if (p.ep_bnred) {
-        // dy (bf16-rounded) masked by ReLU(y) > 0; reduction (sum g, sum g * xhat)
-        const uint32_t yw[4] = {yy[jn].x << 16, yy[jn].x & 0xffff0000u, yy[jn].y << 16,
-                                yy[jn].y & 0xffff0000u};
-        const float zr[4] = {__uint_as_float(zz[jn].x << 16), __uint_as_float(zz[jn].x & 0xffff0000u),
-                             __uint_as_float(zz[jn].y << 16), __uint_as_float(zz[jn].y & 0xffff0000u)};
+    for (int r = 0; r < 4; ++r) {
+      const float d = bf2f(f2bf(acc[r]));
+      v[r] = ((FULL || ok) && yr[r] > 0.f) ? d : 0.f;
+      ssj[r] += v[r];
+      sqj[r] += v[r] * (zr[r] - cb[r]) * cs[r];
+    }
+  } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = bf2f(f2bf(acc[i][jn][r]));
-          v[r] = (__uint_as_float(yw[r]) > 0.f) ? d : 0.f;
-          ss[jn][r] += v[r];
-          sq[jn][r] += v[r] * (zr[r] - colb[jn][r]) * cols[jn][r];
-        }
-      } else {
-        float old[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.beta) {
-          old[0] = __uint_as_float(oo[jn].x << 16); old[1] = __uint_as_float(oo[jn].x & 0xffff0000u);
-          old[2] = __uint_as_float(oo[jn].y << 16); old[3] = __uint_as_float(oo[jn].y & 0xffff0000u);
-        }
+    for (int r = 0; r < 4; ++r) v[r] = (EPI & EP_BIAS) ? acc[r] + cb[r] : acc[r];
+    if constexpr (EPI & EP_BETA) {
+      const uint2 o = ia;
+      v[0] += lo_f(o.x); v[1] += hi_f(o.x); v[2] += lo_f(o.y); v[3] += hi_f(o.y);
+    }
+    if constexpr (EPI & EP_RELU) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = acc[i][jn][r] + colb[jn][r] + old[r];
-          v[r] = p.relu ? fmaxf(t, 0.f) : t;
-        }
-      }
-      const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-      *(uint2*)(out + orow + jn * 16) = make_uint2(lo, hi);
-      if (stats && !p.ep_bnred) {
-        // shifted statistics of the bf16-rounded values BN will read
-        const float rv[4] = {__uint_as_float(lo << 16) - cols[jn][0],
-                             __uint_as_float(lo & 0xffff0000u) - cols[jn][1],
-                             __uint_as_float(hi << 16) - cols[jn][2],
-                             __uint_as_float(hi & 0xffff0000u) - cols[jn][3]};
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+  }
+  const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+  if (FULL || ok) *(uint2*)(out + orow + jn * 16) = make_uint2(lo, hi);
+  if constexpr ((EPI & EP_STATS) && !(EPI & EP_BNRED)) {
+    // shifted statistics of the bf16-rounded values BN will read
+    float rv[4] = {lo_f(lo) - cs[0], hi_f(lo) - cs[1], lo_f(hi) - cs[2], hi_f(hi) - cs[3]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          ss[jn][r] += rv[r];
-          sq[jn][r] += rv[r] * rv[r];
-        }
-      }
+    for (int r = 0; r < 4; ++r) {
+      if (!FULL) rv[r] = ok ? rv[r] : 0.f;
+      ssj[r] += rv[r];
+      sqj[r] += rv[r] * rv[r];
     }
   }
 }
@@ -203,7 +221,7 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
   }
 }
 
-template <bool WRES>
+template <bool WRES, int EPI, bool FULL>
 __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
   char* const hal = smem;
@@ -231,9 +249,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // shift (or BN rstd)
   f32x4 colb[4], cols[4];
   {
-    const bool bnred = p.ep_bnred != 0;
-    const float* bsrc = bnred ? p.ep_mean : p.bias;
-    const float* ssrc = bnred ? p.ep_rstd : p.stats_shift;
+    const float* bsrc = (EPI & EP_BNRED) ? p.ep_mean : p.bias;
+    const float* ssrc = (EPI & EP_BNRED) ? p.ep_rstd : p.stats_shift;
 #pragma unroll
     for (int jn = 0; jn < 4; ++jn) {
       const int n = n0 + jn * 16 + jq * 4;
@@ -271,9 +288,9 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   }
   uint32_t hv[HB_HIW];
   auto tile_of = [&](int tk) { return tbeg + loc + tk * G8; };
-  auto prep_tile = [&](int tile) {  // DMA source offsets of a tile's halo
-    const int mt = tile / p.tiles_n;
-    const int m0 = mt * HB_BM;
+  auto m0_of = [&](int tk) { return (tile_of(tk) / p.tiles_n) * HB_BM; };
+  auto prep_tile = [&](int tk) {  // DMA source offsets of a tile's halo
+    const int m0 = m0_of(tk);
     const int img0 = m0 / HW;
     const int oh0 = (m0 - img0 * HW) / W;
 #pragma unroll
@@ -310,83 +327,169 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
         for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
       }
     }
-    prep_tile(tile_of(0));
+    prep_tile(0);
     issue(0, 0);
   }
 
   // B fragment byte offsets (tap 0, column group 0): row l15 of the [tap][64][32] image
   const int boff = l15 * 64 + ((jq ^ ((l15 >> 1) & 2)) << 4);
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   int xb[4];  // 64 * halo pixel + 16 * chunk of this lane's output row, per row fragment
-  for (int k = 0; k < nitems; ++k) {
-    const int st = k & 1;
-    const int tk = k / CC, cc = k - tk * CC;
-    if (k + 1 < nitems) {
-      const int cc1 = cc + 1 == CC ? 0 : cc + 1;
-      if (cc1 == 0) prep_tile(tile_of(tk + 1));
-      issue(cc1, st ^ 1);
-      halo_wait_barrier<WRES ? HB_HIW : HB_HIW + HB_WIW>();
-    } else {
-      halo_wait_barrier<0>();
-    }
-    const int tile = tile_of(tk);
-    const int m0 = (tile / p.tiles_n) * HB_BM;
-    if (cc == 0) {
-      const int img0 = m0 / HW;
-      const int r0 = m0 - img0 * HW;
-      const int oh0 = r0 / W;
-      const int mlast = p.M - 1 - img0 * HW;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t n = (uint32_t)min(r0 + wave * 64 + i * 16 + l15, mlast);
-        const uint32_t di = udiv(n, h.mag_hw);
-        const uint32_t rem = n - di * HW;
-        const uint32_t oh = udiv(rem, h.mag_w);
-        const uint32_t ow = rem - oh * W;
-        xb[i] = ((((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1) << 6) + (jq << 4);
-      }
-    }
-    // A: X = 64 * pixel + 16 * chunk (+ stage); the swizzle flips bit 5 by pixel bit 2
-    // (= X bit 8): 3 VALU per fragment and tap.  B: per-lane base + immediate offsets.
+  EpiIn ein;
+  f32x4 acc[4][4];
+
+  // Epilogue of fragment (i, jn) of the tile at m0e (operands ia / ib from epi_preload).
+  auto epi_fr = [&](int i, int jn, int m0e, auto full) {
+    constexpr bool F = decltype(full)::value;
+    const int m = m0e + wave * 64 + i * 16 + l15;
+    const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
+    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb[jn],
+                     cols[jn], ss[jn], sq[jn]);
+  };
+
+  // One 32-channel chunk, all 9 taps, in 8 regions (column half hn, row fragment i): a
+  // region holds the 18 B fragments of its column half in registers (72 VGPRs) and runs
+  // 9 taps x 2 MFMAs for one row fragment.  Regions are fenced with sched_barrier (the
+  // scheduler would otherwise hoist every A read of the chunk and exceed 512 VGPRs); each
+  // prefetches the next region's first A fragment.  side(hn, i) runs inside the region, so
+  // its VALU fills the MFMA shadow: in a tile's FIRST chunk it is the previous tile's
+  // epilogue of exactly the two fragments this region is about to restart from zero.
+  // A: X = 64 * pixel + 16 * chunk (+ stage); the swizzle flips bit 5 by pixel bit 2 (= X
+  // bit 8): 3 VALU per fragment.
+  auto mma_chunk = [&](int st, int cc, auto first, auto side) {
+    constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    bf16x8 af[2][4], bfr[2][4];
-    auto load = [&](int t, int b) {
-      const int add = hbase + 64 * h.toff[t];
+    auto load = [&](int i, int t) {
+      const int x = xb[i] + hbase + 64 * h.toff[t];
+      return frag16(hal + (x ^ ((x >> 3) & 32)));
+    };
+    if constexpr (!WRES) {
+      // deep-K layers (CC >= 4 chunks per tile): tap-outer, all 16 fragments per tap (the
+      // next tap's 8 reads in flight under 16 MFMAs); the epilogue runs after the tile
+      bf16x8 a2[2][4], b2[2][4];
+      auto ld = [&](int t, int b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a2[b][i] = load(i, t);
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn)
+            acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
+                                (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+      }
+      return;
+    }
+    bf16x8 af[2];
+    af[0] = load(0, 0);
+#pragma unroll
+    for (int hn = 0; hn < 2; ++hn) {
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 bfr[9][2];
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[t][j] = frag16(wimg + t * (HB_BN * 64) + (2 * hn + j) * 1024);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int x = xb[i] + add;
-        af[b][i] = frag16(hal + (x ^ ((x >> 3) & 32)));
+        if (i) __builtin_amdgcn_sched_barrier(0);
+        side(hn, i);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int b = (i * 9 + t) & 1;
+          if (t + 1 < 9) af[b ^ 1] = load(i, t + 1);
+          else if (i + 1 < 4) af[b ^ 1] = load(i + 1, 0);
+          else if (hn == 0) af[b ^ 1] = load(0, 0);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int jn = 2 * hn + j;
+            acc[i][jn] = mfma16(bfr[t][j], af[b],
+                                (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+          }
+        }
       }
-#pragma unroll
-      for (int jn = 0; jn < 4; ++jn) bfr[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
-    };
-    load(0, 0);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) load(t + 1, (t + 1) & 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 4; ++jn)
-          acc[i][jn] = mfma16(bfr[t & 1][jn], af[t & 1][i], acc[i][jn]);
     }
-    if (cc == CC - 1) {
-      halo_epilogue(p, acc, m0, n0, wave, lane, colb, cols, ss, sq);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // One tile: CC items through the 2-stage ring.  The previous tile's epilogue runs inside
+  // this tile's first chunk (above); its operands are preloaded at the top of the previous
+  // tile's last chunk, before that item's DMAs are issued (an in-order vmcnt wait for a
+  // load issued behind the DMAs would wait for them too).
+  auto run_tile = [&](int tk, int prev_m0) {
+    const int m0 = m0_of(tk);
+    for (int cc = 0; cc < CC; ++cc) {
+      const int k = tk * CC + cc;
+      const int st = k & 1;
+      if (WRES && cc == 0 && prev_m0 >= 0 && CC == 1) {
+        // single-chunk tiles: the previous tile's operands are consumed in THIS item, so
+        // the preload for this tile happens after it (below)
+      } else if (cc == CC - 1) {
+        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
+      }
+      if (k + 1 < nitems) {
+        const int cc1 = cc + 1 == CC ? 0 : cc + 1;
+        if (cc1 == 0) prep_tile(tk + 1);
+        issue(cc1, st ^ 1);
+        halo_wait_barrier<WRES ? HB_HIW : HB_HIW + HB_WIW>();
+      } else {
+        halo_wait_barrier<0>();
+      }
+      if (cc == 0) {
+        const int img0 = m0 / HW;
+        const int r0 = m0 - img0 * HW;
+        const int oh0 = r0 / W;
+        const int mlast = p.M - 1 - img0 * HW;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t n = (uint32_t)min(r0 + wave * 64 + i * 16 + l15, mlast);
+          const uint32_t di = udiv(n, h.mag_hw);
+          const uint32_t rem = n - di * HW;
+          const uint32_t oh = udiv(rem, h.mag_w);
+          const uint32_t ow = rem - oh * W;
+          xb[i] = ((((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1) << 6) + (jq << 4);
+        }
+        if (WRES && prev_m0 >= 0) {
+          mma_chunk(st, 0, std::true_type{}, [&](int hn, int i) {
+            epi_fr(i, 2 * hn, prev_m0, std::true_type{});  // previous tile: always full
+            epi_fr(i, 2 * hn + 1, prev_m0, std::true_type{});
+          });
+        } else {
+          mma_chunk(st, 0, std::true_type{}, [](int, int) {});
+        }
+      } else {
+        mma_chunk(st, cc, std::false_type{}, [](int, int) {});
+      }
+      if (WRES && cc == 0 && prev_m0 >= 0 && CC == 1) {
+        // (the item's global loads were waited above; these complete before the next wait)
+        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
+      }
+      if (!WRES && cc == CC - 1 && tk + 1 < ntiles) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{});
+      }
+      __syncthreads();  // stage st is free for item k + 2
     }
-    __syncthreads();  // stage st is free for item k + 2
+  };
+
+  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, tk > 0 ? m0_of(tk - 1) : -1);
+  if (ntiles > 0) {
+    const int m0l = m0_of(ntiles - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
   }
-  if (p.stats) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
+  if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
 }
 
 // ------------------------------------------------------------------------------ host
@@ -411,6 +514,22 @@ static int num_cus() {
   return n;
 }
 
+// epilogue flavour of a launch; -1: not instantiated (the implicit GEMM runs it)
+static int halo_epi(const IGemmArgs& a) {
+  int e = 0;
+  if (a.ep_bnred) return (a.beta || a.relu || a.bias) ? -1 : EP_BNRED;
+  if (a.relu) e |= EP_RELU;
+  if (a.beta) e |= EP_BETA;
+  if (a.stats) e |= EP_STATS;
+  if (a.bias) e |= EP_BIAS;
+  switch (e) {
+    case 0: case EP_BETA: case EP_STATS: case EP_BIAS | EP_RELU: case EP_BIAS | EP_STATS:
+      return e;
+    default:
+      return -1;
+  }
+}
+
 bool conv3_halo_ok(const IGemmArgs& a) {
   if (!g_halo || a.nphase > 0 || a.stap || a.T != 9 || a.Uh != 1 || a.Uw != 1) return false;
   if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.N % HB_BN != 0 || a.M <= 0)
@@ -419,6 +538,7 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   if (a.dH != a.oH || a.dW != a.oW || a.Uoh != 1 || a.Uow != 1 || a.Poh != 0 || a.Pow != 0)
     return false;
   if ((int64_t)a.M * a.ldc >= (1ll << 31) || a.ldc < a.N) return false;
+  if (halo_epi(a) < 0) return false;  // an epilogue flavour without an instantiation
   if (a.Ktot != 9 * a.aC) return false;
   for (int t = 0; t < 9; ++t) {
     const int dh = a.Oh + a.taps.dh[t], dw = a.Ow + a.taps.dw[t];
@@ -432,6 +552,20 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   const int64_t rows = (HB_BM - 1 + a.aW - 1) / a.aW + 1;
   const int64_t seps = (HB_BM - 1) / HW + 1;
   return (rows + 2 + seps) * (a.aW + 2) <= HB_HPX;
+}
+
+template <int EPI>
+static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
+                        hipStream_t s) {
+  const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
+  if (wres && full)
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true>), dim3(grid), dim3(256), 0, s, a, h);
+  else if (wres)
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false>), dim3(grid), dim3(256), 0, s, a, h);
+  else if (full)
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true>), dim3(grid), dim3(256), 0, s, a, h);
+  else
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false>), dim3(grid), dim3(256), 0, s, a, h);
 }
 
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
@@ -458,10 +592,15 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   int g8 = std::min(std::min(num_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
-  if (a.tiles_n == 1 && h.cc <= 2)
-    hipLaunchKernelGGL(conv3_halo_kernel<true>, dim3(grid), dim3(256), 0, s, a, h);
-  else
-    hipLaunchKernelGGL(conv3_halo_kernel<false>, dim3(grid), dim3(256), 0, s, a, h);
+  const bool wres = a.tiles_n == 1 && h.cc <= 2;
+  switch (halo_epi(a)) {
+    case 0: launch_halo<0>(wres, grid, a, h, s); break;
+    case EP_BETA: launch_halo<EP_BETA>(wres, grid, a, h, s); break;
+    case EP_STATS: launch_halo<EP_STATS>(wres, grid, a, h, s); break;
+    case EP_BIAS | EP_RELU: launch_halo<EP_BIAS | EP_RELU>(wres, grid, a, h, s); break;
+    case EP_BIAS | EP_STATS: launch_halo<EP_BIAS | EP_STATS>(wres, grid, a, h, s); break;
+    default: launch_halo<EP_BNRED>(wres, grid, a, h, s); break;
+  }
   return grid;
 }
 
