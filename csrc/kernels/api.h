@@ -111,6 +111,10 @@ bool conv3_halo_ok(const IGemmArgs& a);
 int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
+// halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z
+bool conv3_halo_wgrad_ok(const WGradArgs& a);
+int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
+int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);
 bool igemm_halo_enabled();
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)

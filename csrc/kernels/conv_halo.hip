@@ -492,6 +492,177 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
 }
 
+// ======================================================================================
+//  Halo-staged 3x3 / stride-1 weight gradient:
+//    dW[k][t = 3r+s][c] += sum_pix dy[pix][k] * x[pix + (r-1, s-1)][c]
+//  The implicit-GEMM wgrad gathers an im2col column panel per (tap, channel) tile, i.e.
+//  every x pixel nine times.  Here a block owns a 64 (k) x 64 (c) x 9 (taps) output
+//  partition and streams 128-pixel tiles: the dy tile [128 px][64 k] and the x halo of
+//  those pixels (both 32-channel chunks of the partition) are staged once per tile, and the
+//  nine taps read shifted halo rows.  Reduction dim = pixels: both operands are read
+//  pixel-major with ds_read_b64_tr_b16 (dy image in the engine's mn_off<64> layout; halo
+//  rows 64 B with chunk c at position c ^ (2 * ((row >> 3) & 1)), so the 2 x 4 pixel rows
+//  one 32-lane half reads hit every bank once).  Wave w owns 16 channels (chunk w/2) for
+//  all 64 k and 9 taps: 36 accumulators of 16x16.  Partials go to a [Z][K][9C] slab
+//  (Z = blocks per partition), summed into the fp32 gradient arena by wgrad_reduce.
+// ======================================================================================
+constexpr int HW_BM = 128;                    // pixels per tile
+constexpr int HW_HIW = 7;                     // halo DMA instructions per wave per chunk
+constexpr int HW_HPX = 16 * 4 * HW_HIW;       // 448 halo pixels
+constexpr int HW_HBYTES = HW_HPX * 64;        // 28 KiB per chunk
+constexpr int HW_DBYTES = HW_BM * 64 * 2;     // 16 KiB: dy tile, 4 k-steps x [32 px][64 k]
+constexpr int HW_STAGE = HW_DBYTES + 2 * HW_HBYTES;  // 72 KiB
+constexpr int HW_LDS = 2 * HW_STAGE;                 // 147,456 B
+
+struct HaloWPlan {
+  int toff[9];
+  uint32_t mag_w, mag_w2, mag_h1, mag_hw;
+  int tiles_m, parts, kparts, Z;
+  uint32_t dy_bytes, x_bytes;
+};
+
+__global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
+  __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.H, W = p.W, HW = H * W, W2 = W + 2, C = p.C, K = p.Kout;
+  const int M = p.Mpix, nimg = M / HW;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+
+  const int part = blockIdx.x % h.parts, z = blockIdx.x / h.parts;
+  const int k0 = (part % h.kparts) * 64, c0 = (part / h.kparts) * 64;
+  const int ntiles = z < h.tiles_m ? (h.tiles_m - z + h.Z - 1) / h.Z : 0;
+
+  // ---- DMA lanes.  dy: instruction j of this wave = rows 8 (4 wave + j) + lane/8 of the
+  // tile (k-step image (row >> 5), mn_off<64> swizzle at the source)
+  uint32_t drow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wave + j) + (lane >> 3);
+    const int chunk = (lane & 7) ^ mn_swz<64>(row & 31);
+    drow[j] = ((uint32_t)row * K + k0 + chunk * 8) * 2;  // + pixel0 * K * 2 per tile
+  }
+  // halo: instruction j = pixels 16 (7 wave + j) + lane/4 of the image; chunk 1 of the
+  // partition is the same lanes with the descriptor base 64 B further
+  uint32_t hsc[HW_HIW];
+#pragma unroll
+  for (int j = 0; j < HW_HIW; ++j) {
+    const uint32_t hp = 16 * (wave * HW_HIW + j) + (lane >> 2);
+    const uint32_t sl = udiv(hp, h.mag_w2);
+    const uint32_t colp = hp - sl * W2;
+    const uint32_t lc = (lane & 3) ^ (((hp >> 3) & 1) << 1);
+    hsc[j] = sl | (colp << 10) | (lc << 18);
+  }
+  uint32_t hv[HW_HIW], dv[4];
+  int hb[4][2];  // halo pixel of this lane's B rows (k-step ks, lo/hi)
+  auto prep = [&](int mt) {
+    const int m0 = mt * HW_BM;
+    const int img0 = m0 / HW;
+    const int r0 = m0 - img0 * HW;
+    const int oh0 = r0 / W;
+#pragma unroll
+    for (int j = 0; j < HW_HIW; ++j) {
+      const int sl = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
+      const int v = sl + oh0 - 1;
+      const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;
+      const int row = v - d * (H + 1);
+      const int img = img0 + d;
+      const bool ok = row < H && (unsigned)col < (unsigned)W && img < nimg;
+      hv[j] = ok ? ((((uint32_t)img * H + row) * W + col) * C + c0) * 2 + (hsc[j] >> 18) * 16
+                 : 0x80000000u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * (4 * wave + j) + (lane >> 3);
+      dv[j] = m0 + row < M ? drow[j] + (uint32_t)m0 * K * 2 : 0x80000000u;
+    }
+    const int mlast = M - 1 - img0 * HW;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint32_t n = (uint32_t)min(r0 + ks * 32 + 8 * g + 4 * e + q, mlast);
+        const uint32_t di = udiv(n, h.mag_hw);
+        const uint32_t rem = n - di * HW;
+        const uint32_t oh = udiv(rem, h.mag_w);
+        const uint32_t ow = rem - oh * W;
+        hb[ks][e] = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+      }
+  };
+  auto issue = [&](int stage) {
+    char* st = smem + stage * HW_STAGE;
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.dy, h.dy_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) buf_lds16(rd, st + (4 * wave + j) * 1024, dv[j]);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)p.x + ch * 64, h.x_bytes);
+      char* hd = st + HW_DBYTES + ch * HW_HBYTES + wave * HW_HIW * 1024;
+#pragma unroll
+      for (int j = 0; j < HW_HIW; ++j) buf_lds16(rx, hd + j * 1024, hv[j]);
+    }
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int km = 0; km < 4; ++km)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[km][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
+  const int hoff = HW_DBYTES + (wave >> 1) * HW_HBYTES;
+  const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
+  if (ntiles > 0) {
+    prep(z);
+    issue(0);
+  }
+  for (int k = 0; k < ntiles; ++k) {
+    const int st = k & 1;
+    halo_wait_barrier<0>();
+    int hbk[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) { hbk[ks][0] = hb[ks][0]; hbk[ks][1] = hb[ks][1]; }
+    if (k + 1 < ntiles) {  // next tile's DMA overlaps this tile's MFMAs
+      prep(z + (k + 1) * h.Z);
+      issue(st ^ 1);
+    }
+    const char* sbase = smem + st * HW_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sbase + ks * 4096, 16 * km, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int base = st * HW_STAGE + hoff + cbyte + 64 * h.toff[t];
+        const int x0 = hbk[ks][0] * 64 + base, x1 = hbk[ks][1] * 64 + base;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, smem + (x0 ^ ((x0 >> 4) & 32))));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, smem + (x1 ^ ((x1 >> 4) & 32))));
+        s16x8 r;
+        r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+        r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
+#pragma unroll
+        for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
+      }
+    }
+    __syncthreads();  // stage st is free for tile k + 2
+  }
+  // partial of this block -> slab z: dw[k][t][c] at k = k0 + 16 km + lane%16,
+  // c = c0 + 16 wave + 4 (lane/16) .. +3
+  const int64_t ncols = 9 * (int64_t)C;
+  float* dst = p.slab + (int64_t)z * K * ncols;
+#pragma unroll
+  for (int km = 0; km < 4; ++km) {
+    const int kk = k0 + 16 * km + li;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      *(f32x4*)(dst + (int64_t)kk * ncols + t * C + c0 + 16 * wave + 4 * g) = acc[km][t];
+  }
+}
+
 // ------------------------------------------------------------------------------ host
 static bool g_halo = [] {
   const char* e = getenv("MPA_HALO");
@@ -602,6 +773,49 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
     default: launch_halo<EP_BNRED>(wres, grid, a, h, s); break;
   }
   return grid;
+}
+
+// ------------------------------------------------------------------ halo wgrad host
+static bool halo_wgrad_geom(const WGradArgs& a) {
+  if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1)
+    return false;
+  if (a.P != a.H || a.Q != a.W || a.C % 64 != 0 || a.Kout % 64 != 0) return false;
+  const int64_t HW = (int64_t)a.H * a.W;
+  if (a.Mpix % HW != 0 || HW + HW_BM >= 65536 || a.W + 2 > 255) return false;
+  if ((int64_t)a.Mpix * a.C * 2 >= (1ll << 31) || (int64_t)a.Mpix * a.Kout * 2 >= (1ll << 31))
+    return false;
+  const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
+  const int64_t seps = (HW_BM - 1) / HW + 1;
+  return (rows + 2 + seps) * (a.W + 2) <= HW_HPX;
+}
+
+int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols) {
+  if (Ncols % 9 != 0 || (Ncols / 9) % 64 != 0 || Kout % 64 != 0) return 0;
+  return (int64_t)HALO_MAX_ROWS * 64 * 64 * 9;  // <= 256 blocks x one 64x9x64 partition
+}
+
+bool conv3_halo_wgrad_ok(const WGradArgs& a) {
+  return halo_wgrad_geom(a) && a.slab != nullptr;
+}
+
+// slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
+int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
+  HaloWPlan h{};
+  const int W2 = a.W + 2;
+  for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);
+  h.mag_w = magic(a.W);
+  h.mag_w2 = magic(W2);
+  h.mag_h1 = magic(a.H + 1);
+  h.mag_hw = magic(a.H * a.W);
+  h.tiles_m = (a.Mpix + HW_BM - 1) / HW_BM;
+  h.kparts = a.Kout / 64;
+  h.parts = h.kparts * (a.C / 64);
+  const int G = std::min(num_cus(), HALO_MAX_ROWS);
+  h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
+  h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
+  h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
+  hipLaunchKernelGGL(conv3_halo_wgrad_kernel, dim3(h.parts * h.Z), dim3(256), 0, s, a, h);
+  return h.Z;
 }
 
 }  // namespace mpa

@@ -266,6 +266,27 @@ def test_conv_halo_dgrad(gpu, case):
     assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
 
 
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_wgrad(gpu, case):
+    """Halo-staged 3x3/s1 weight gradient (slab partials + reduce, accumulating into dw)
+    == implicit-GEMM wgrad and the fp32 oracle."""
+    torch.manual_seed(24)
+    N, H, W, Cc, K = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    dy = bf(N, H, W, K, dev=gpu)
+    dw0 = torch.randn(K, 3, 3, Cc, device=gpu)
+
+    def run():
+        dw = dw0.clone()
+        C().conv_wgrad(dy, x, dw, 1, 1, 1, 1)
+        return dw
+
+    dw, dwi = _halo_pair(run)
+    dwr = dw0.clone()
+    ref.conv_wgrad(dy, x, dwr, 1, 1, 1, 1)
+    assert rel(dw, dwi) < 1e-3 and rel(dw - dw0, dwr - dw0) < 1e-2
+
+
 def test_conv_halo_repeatable(gpu):
     """Persistent 2-stage ring: repeated launches are bitwise identical (race screen)."""
     torch.manual_seed(23)

@@ -57,4 +57,5 @@ def check(N, H, W, BM=256, HPX=576):
 if __name__ == "__main__":
     for case in [(2, 56, 56), (3, 28, 28), (5, 14, 14), (7, 7, 7), (3, 9, 11), (1, 5, 3),
                  (2, 35, 35), (4, 1, 1), (3, 2, 2), (64, 7, 7), (2, 17, 17)]:
-        print(case, check(*case))
+        print(case, "fwd/dgrad (256-px tiles):", check(*case),
+              "| wgrad (128-px tiles):", check(*case, BM=128, HPX=448))
