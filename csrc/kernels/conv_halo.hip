@@ -69,9 +69,33 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, char* lds, u
                                            voff, 0, 0, 0);
 }
 
+// The same DMA as inline asm: the compiler does not see an LDS write, so it inserts no
+// vmcnt(0) before the following ds_read_b64_tr_b16 (whose intrinsic it cannot prove
+// disjoint from the DMA target - with the builtin, every DMA issued between transposed
+// reads was followed by a full wait).  Safe for the compiler's own vmcnt accounting: it
+// only undercounts outstanding ops, so its waits get stronger, never weaker; the kernel
+// waits for these DMAs itself (wait_all_barrier) before reading their stage.
+__device__ __forceinline__ void buf_lds16_asm(__amdgpu_buffer_rsrc_t r, const char* lds,
+                                              uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void halo_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// all of this wave's VMEM (LDS-DMAs, loads, stores) done, then the workgroup barrier; as a
+// builtin s_waitcnt (vmcnt 0, lgkmcnt 0) the compiler's wait insertion knows the loads are
+// complete, so it adds no vmcnt(0) later that would also wait for DMAs issued afterwards
+__device__ __forceinline__ void wait_all_barrier() {
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  __builtin_amdgcn_s_barrier();
 }
 
 __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
@@ -305,17 +329,20 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
                  : 0x80000000u;
     }
   };
-  auto issue = [&](int cc, int stage) {
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
-    char* hdst = hal + stage * HB_HBYTES + wave * HB_HIW * 1024;
-#pragma unroll
-    for (int j = 0; j < HB_HIW; ++j) buf_lds16(ra, hdst + j * 1024, hv[j]);
-    if constexpr (!WRES) {
+  // DMA instruction j (halo 0..8, then weights 9..17 unless resident) of item (cc, stage)
+  auto dma = [&](int cc, int stage, int j) {
+    if (j < HB_HIW) {
+      const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
+      buf_lds16(ra, hal + stage * HB_HBYTES + (wave * HB_HIW + j) * 1024, hv[j]);
+    } else if (!WRES && j < HB_HIW + HB_WIW) {
       const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
-      char* wdst = wst + stage * HB_WBYTES + wave * HB_WIW * 1024;
-#pragma unroll
-      for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
+      buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j - HB_HIW) * 1024,
+                wv[j - HB_HIW]);
     }
+  };
+  auto issue = [&](int cc, int stage) {
+#pragma unroll
+    for (int j = 0; j < HB_HIW + HB_WIW; ++j) dma(cc, stage, j);
   };
 
   if (nitems > 0) {
@@ -355,7 +382,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // epilogue of exactly the two fragments this region is about to restart from zero.
   // A: X = 64 * pixel + 16 * chunk (+ stage); the swizzle flips bit 5 by pixel bit 2 (= X
   // bit 8): 3 VALU per fragment.
-  auto mma_chunk = [&](int st, int cc, auto first, auto side) {
+  auto mma_chunk = [&](int st, int cc, auto first, auto side, auto nd) {
     constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
@@ -383,6 +410,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
           for (int jn = 0; jn < 4; ++jn)
             acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
                                 (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+        nd(2 * t);  // the next item's 18 DMAs, two per tap, in the MFMA shadow
+        nd(2 * t + 1);
       }
       return;
     }
@@ -401,6 +430,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       for (int i = 0; i < 4; ++i) {
         if (i) __builtin_amdgcn_sched_barrier(0);
         side(hn, i);
+        nd(4 * hn + i);  // the next item's 9 halo DMAs: one per region (+1 in the first)
+        if (hn == 0 && i == 0) nd(8);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
           const int b = (i * 9 + t) & 1;
@@ -434,14 +465,15 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       } else if (cc == CC - 1) {
         epi_preload<EPI>(p, ein, m0, n0, wave, lane);
       }
-      if (k + 1 < nitems) {
-        const int cc1 = cc + 1 == CC ? 0 : cc + 1;
-        if (cc1 == 0) prep_tile(tk + 1);
-        issue(cc1, st ^ 1);
-        halo_wait_barrier<WRES ? HB_HIW : HB_HIW + HB_WIW>();
-      } else {
-        halo_wait_barrier<0>();
-      }
+      // this item's DMAs were issued during the previous item's MFMAs; the next item's
+      // are issued during this one's (stage st ^ 1 was freed by the previous barrier)
+      wait_all_barrier();
+      const bool more = k + 1 < nitems;
+      const int cc1 = cc + 1 == CC ? 0 : cc + 1;
+      if (more && cc1 == 0) prep_tile(tk + 1);
+      auto nd = [&](int j) {
+        if (more) dma(cc1, st ^ 1, j);
+      };
       if (cc == 0) {
         const int img0 = m0 / HW;
         const int r0 = m0 - img0 * HW;
@@ -460,12 +492,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
           mma_chunk(st, 0, std::true_type{}, [&](int hn, int i) {
             epi_fr(i, 2 * hn, prev_m0, std::true_type{});  // previous tile: always full
             epi_fr(i, 2 * hn + 1, prev_m0, std::true_type{});
-          });
+          }, nd);
         } else {
-          mma_chunk(st, 0, std::true_type{}, [](int, int) {});
+          mma_chunk(st, 0, std::true_type{}, [](int, int) {}, nd);
         }
       } else {
-        mma_chunk(st, cc, std::false_type{}, [](int, int) {});
+        mma_chunk(st, cc, std::false_type{}, [](int, int) {}, nd);
       }
       if (WRES && cc == 0 && prev_m0 >= 0 && CC == 1) {
         // (the item's global loads were waited above; these complete before the next wait)
@@ -589,18 +621,20 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
         hb[ks][e] = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
       }
   };
-  auto issue = [&](int stage) {
+  // DMA instruction j of a tile: dy rows (0..3), halo chunk 0 (4..10), halo chunk 1 (11..17)
+  auto dmaw = [&](int stage, int j) {
     char* st = smem + stage * HW_STAGE;
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.dy, h.dy_bytes);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) buf_lds16(rd, st + (4 * wave + j) * 1024, dv[j]);
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch) {
+    if (j < 4) {
+      buf_lds16_asm(make_rsrc(p.dy, h.dy_bytes), st + (4 * wave + j) * 1024, dv[j]);
+    } else {
+      const int ch = (j - 4) / HW_HIW, jj = (j - 4) % HW_HIW;
       const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)p.x + ch * 64, h.x_bytes);
-      char* hd = st + HW_DBYTES + ch * HW_HBYTES + wave * HW_HIW * 1024;
-#pragma unroll
-      for (int j = 0; j < HW_HIW; ++j) buf_lds16(rx, hd + j * 1024, hv[j]);
+      buf_lds16_asm(rx, st + HW_DBYTES + ch * HW_HBYTES + (wave * HW_HIW + jj) * 1024, hv[jj]);
     }
+  };
+  auto issue = [&](int stage) {
+#pragma unroll
+    for (int j = 0; j < 4 + 2 * HW_HIW; ++j) dmaw(stage, j);
   };
 
   f32x4 acc[4][9];
@@ -618,14 +652,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   }
   for (int k = 0; k < ntiles; ++k) {
     const int st = k & 1;
-    halo_wait_barrier<0>();
+    wait_all_barrier();
     int hbk[4][2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) { hbk[ks][0] = hb[ks][0]; hbk[ks][1] = hb[ks][1]; }
-    if (k + 1 < ntiles) {  // next tile's DMA overlaps this tile's MFMAs
-      prep(z + (k + 1) * h.Z);
-      issue(st ^ 1);
-    }
+    const bool more = k + 1 < ntiles;
+    if (more) prep(z + (k + 1) * h.Z);  // next tile's 18 DMAs: one per 2 tap-steps below
     const char* sbase = smem + st * HW_STAGE;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -646,6 +678,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
         for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
+        if (more && ((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
       }
     }
     __syncthreads();  // stage st is free for tile k + 2
