@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256) void slab_stats_kernel(const float* __restrict
 void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sums, float* out,
                 hipStream_t s) {
   int rstep = 1, rows = S;
-  if (S > 64) {  // fold to <= 64 chunk heads: the finalize has only C/64 blocks
+  if (S > 256) {  // fold to <= 64 chunk heads (one launch up to 256 rows: halo-conv slabs)
     const int chunk = (S + 63) / 64;
     rows = (S + chunk - 1) / chunk;
     rstep = chunk;
