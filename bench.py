@@ -35,7 +35,8 @@ def main(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--batch", type=int, default=512,
+                   help="per-GPU batch (profiles/batch_sweep_r18.txt: 256 -> 29.5k, 512 -> 34.0k img/s)")
     p.add_argument("--model", default="resnet18")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--classes", type=int, default=64500)
