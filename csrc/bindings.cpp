@@ -361,7 +361,8 @@ Tensor bn_fwd_eval(Tensor x, Tensor gamma, Tensor beta, Tensor rmean, Tensor rva
 }
 
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd, Tensor gamma,
-                           Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g) {
+                           Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g,
+                           c10::optional<Tensor> zmask_beta) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
@@ -372,9 +373,11 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
   Tensor gout = want_g ? torch::empty_like(x) : Tensor();
   Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
+  const Tensor zb = (zmask_beta && zmask_beta->defined()) ? *zmask_beta : Tensor();
+  if (has(zb)) TORCH_CHECK(zb.numel() == C, "bn_bwd: zmask beta size");
   mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
               fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr, want_g ? bpm(gout) : nullptr,
-              ws.data_ptr<float>(), cur_stream());
+              ws.data_ptr<float>(), cur_stream(), fopt(zb));
   return {dx, gout};
 }
 
@@ -732,7 +735,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
         py::arg("res"), py::arg("relu"), py::arg("counter") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"),
+        py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

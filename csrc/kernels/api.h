@@ -137,9 +137,12 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s);
+// zmask_beta (y == null): the ReLU mask of y = relu(bn(x)) is recomputed from x with this
+// beta (no residual in the forward), so y is never read
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
-            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s);
+            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s,
+            const float* zmask_beta = nullptr);
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);

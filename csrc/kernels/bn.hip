@@ -174,7 +174,7 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
       float f[8];
       unpack8(xv[u], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[j] + sh[j];
+      for (int j = 0; j < 8; ++j) f[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
       if (res) {
         float g[8];
         unpack8(rv[u], g);
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     const float var = stats[C + c0 + j];
     const float rs = rsqrtf(var + eps);
     sc[j] = gamma[c0 + j] * rs;
-    sh[j] = beta[c0 + j] - mu * sc[j];
+    sh[j] = __builtin_fmaf(-mu, sc[j], beta[c0 + j]);
     if (blockIdx.x == 0 && cm.r0 == 0) {
       mean_out[c0 + j] = mu;
       rstd_out[c0 + j] = rs;
@@ -242,10 +242,28 @@ __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
 
 // ---------------------------------------------------------------------- backward
 // pass 1: ws[0:C] += sum(g), ws[C:2C] += sum(g * xhat), g = dy * (y > 0 if relu)
+// ReLU mask of y = relu(bn(x)) recomputed from x exactly as bn_fwd_train rounded it
+// (same fma affine, same bf16 rounding): the backward of a BN+ReLU whose output carries no
+// residual then never reads y - one activation-sized read less in each of its two passes
+__device__ __forceinline__ void bn_relu_coeffs(const float* gamma, const float* beta,
+                                               const float* mean, const float* rstd, int c0,
+                                               float* sc, float* sh) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = gamma[c0 + j] * rstd[c0 + j];
+    sh[j] = __builtin_fmaf(-mean[c0 + j], sc[j], beta[c0 + j]);
+  }
+}
+__device__ __forceinline__ bool bn_relu_live(float x, float sc, float sh) {
+  return bf2f(f2bf(__builtin_fmaf(x, sc, sh))) > 0.f;
+}
+
+// zmask (beta != null, y == null): ReLU mask from x via bn_relu_live
 template <int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ rstd, int M, int C,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int M, int C,
     float* __restrict__ slab, float* __restrict__ sums) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
@@ -258,9 +276,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) { sums[c0 + j] = 0.f; sums[C + c0 + j] = 0.f; }
     }
-    float mu[8], rs[8];
+    float mu[8], rs[8], msc[8], msh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+    const bool zmask = !y && beta;
+    if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
     sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
       uint4 dv[UNR], xr[UNR], yr[UNR];
 #pragma unroll
@@ -283,6 +303,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
           unpack8(yr[u], yv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+        } else if (zmask) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = bn_relu_live(xv[j], msc[j], msh[j]) ? g[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -309,8 +332,9 @@ template <int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ gamma, const float* __restrict__ ws, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, int M, int C, bf16_t* __restrict__ dx, bf16_t* __restrict__ gout) {
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ ws,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int M, int C,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ gout) {
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -330,6 +354,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
   }
   if (!dx && !gout) return;
+  const bool zmask = !y && beta;
+  float msc[8], msh[8];
+  if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
   sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
     uint4 dv[UNR], xr[UNR], yr[UNR];
 #pragma unroll
@@ -338,7 +365,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         const size_t off = (size_t)(r + u * st) * C + c0;
         dv[u] = *(const uint4*)(dy + off);
         if (y) yr[u] = *(const uint4*)(y + off);
-        if (dx) xr[u] = *(const uint4*)(x + off);
+        if (dx || zmask) xr[u] = *(const uint4*)(x + off);
       }
     }
 #pragma unroll
@@ -352,6 +379,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         unpack8(yr[u], yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+        if (gout) *(uint4*)(gout + off) = pack8(g);
+      } else if (zmask) {
+        float xv[8];
+        unpack8(xr[u], xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = bn_relu_live(xv[j], msc[j], msh[j]) ? g[j] : 0.f;
         if (gout) *(uint4*)(gout + off) = pack8(g);
       } else if (gout) {
         *(uint4*)(gout + off) = dv[u];
@@ -620,7 +653,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const float mu = stats[c0 + j], var = stats[C + c0 + j];
     const float rs = rsqrtf(var + eps);
     sc[j] = gamma[c0 + j] * rs;
-    sh[j] = beta[c0 + j] - mu * sc[j];
+    sh[j] = __builtin_fmaf(-mu, sc[j], beta[c0 + j]);
     if (blockIdx.x == 0 && cm.r0 == 0) {
       mean_out[c0 + j] = mu;
       rstd_out[c0 + j] = rs;
@@ -953,15 +986,15 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
-            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s) {
+            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials
   const dim3 gr = grid_for(M, C);
   float* slab = ws + 2 * C;
-  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, M, C, slab,
-                     ws);
+  const float* zb = y ? nullptr : zmask_beta;
+  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
   BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd,
-                     gamma, ws, dgamma, dbeta, M, C, dx, g);
+                     gamma, zb, ws, dgamma, dbeta, M, C, dx, g);
 }
 
 // apply pass only, with the reduction sums [sum g | sum g*xhat] already in `sums` (e.g.
@@ -969,8 +1002,8 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s) {
-  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, sums, dgamma,
-            dbeta, M, C, dx, g);
+  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
+            (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,

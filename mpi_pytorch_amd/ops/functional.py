@@ -202,6 +202,10 @@ class _ConvBNAct(torch.autograd.Function):
             dz, g = k.bn_bwd_apply(dy, z, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
                                    _sink(beta, dy), lo.sums, True, want_g)
             lo.sums = None
+        elif ctx.relu and not ctx.has_res and beta is not None:
+            # relu(bn(z)) without a residual: the mask is recomputed from z, y is not read
+            dz, g = k.bn_bwd(dy, z, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
+                             _sink(beta, dy), True, want_g, beta)
         else:
             dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
                              _sink(beta, dy), True, want_g)

@@ -132,12 +132,17 @@ def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
     return y.reshape(x.shape).to(x.dtype)
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True):
-    """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient)."""
+def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zmask_beta=None):
+    """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient).  With
+    ``zmask_beta`` and no ``y`` the mask of y = relu(bn(x)) is recomputed from x."""
     C = x.shape[-1]
     g = _f(dy).reshape(-1, C)
     if _opt(y) is not None:
         g = g * (_f(y).reshape(-1, C) > 0)
+    elif _opt(zmask_beta) is not None:
+        sc = gamma * rstd
+        t = (_f(x).reshape(-1, C) * sc + (zmask_beta - mean * sc)).to(torch.bfloat16).float()
+        g = g * (t > 0)
     M = g.shape[0]
     xhat = (_f(x).reshape(-1, C) - mean) * rstd
     sg = g.sum(0)

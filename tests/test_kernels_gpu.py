@@ -493,6 +493,27 @@ def test_bn(gpu, M, Cc, relu, res):
     assert rel(dg, dg2) < 1e-2 and rel(db, db2) < 1e-2
 
 
+@pytest.mark.parametrize("M,Cc", [(4096, 64), (1000, 136)])
+def test_bn_bwd_mask_from_z(gpu, M, Cc):
+    """relu(bn(z)) backward with the mask recomputed from z (no y read) == the y-masked
+    backward, bit for bit: the recomputation replays bn_fwd_train's fma and rounding."""
+    torch.manual_seed(14)
+    x = (bf(M, Cc, dev=gpu, scale=2.0) + 0.3).to(torch.bfloat16)
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu)
+    e = torch.empty(0, device=gpu)
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    y, mean, rstd = C().bn_fwd_train(x, e, g, b, rm, rv, 0.1, 1e-5, e, True, e)
+    dy = bf(M, Cc, dev=gpu)
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    dx, gg = C().bn_bwd(dy, x, y, mean, rstd, g, dg, db, True, True)
+    dxz, ggz = C().bn_bwd(dy, x, e, mean, rstd, g, dg2, db2, True, True, b)
+    torch.cuda.synchronize()
+    assert torch.equal(gg, ggz) and torch.equal(dx, dxz)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+
+
 def test_bn_stats_from_conv(gpu):
     """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
     torch.manual_seed(5)
