@@ -509,7 +509,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
 #pragma unroll
           for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{});
       }
-      __syncthreads();  // stage st is free for item k + 2
+      // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
+      // after its top barrier, which every wave passes only once done reading stage st)
     }
   };
 
@@ -681,7 +682,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
         if (more && ((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
       }
     }
-    __syncthreads();  // stage st is free for tile k + 2
+    // (no barrier: tile k + 2's DMAs into stage st follow tile k + 1's top barrier)
   }
   // partial of this block -> slab z: dw[k][t][c] at k = k0 + 16 km + lane%16,
   // c = c0 + 16 wave + 4 (lane/16) .. +3
