@@ -549,6 +549,7 @@ constexpr int HW_LDS = 2 * HW_STAGE;                 // 147,456 B
 
 struct HaloWPlan {
   int toff[9];
+  int w2;  // halo row pitch in pixels: W + 2 rounded up to 16 (see the B-address note)
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;
   int tiles_m, parts, kparts, Z;
   uint32_t dy_bytes, x_bytes;
@@ -558,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = p.H, W = p.W, HW = H * W, W2 = W + 2, C = p.C, K = p.Kout;
+  const int H = p.H, W = p.W, HW = H * W, W2 = h.w2, C = p.C, K = p.Kout;
   const int M = p.Mpix, nimg = M / HW;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
 
@@ -587,7 +588,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     hsc[j] = sl | (colp << 10) | (lc << 18);
   }
   uint32_t hv[HW_HIW], dv[4];
-  int hb[4][2];  // halo pixel of this lane's B rows (k-step ks, lo/hi)
+  // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
+  const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
+  // B-row addresses per (k-step, lo/hi, column tap dw): the swizzle bit is pixel bit 3,
+  // and the row pitch W2 is a multiple of 16, so a tap's row offset dh * W2 never changes
+  // it - the swizzled address of pixel (hp + dh*W2 + dw) is hbw[dw] + dh*W2*64
+  int hbw[4][2][3];
   auto prep = [&](int mt) {
     const int m0 = mt * HW_BM;
     const int img0 = m0 / HW;
@@ -619,7 +625,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
         const uint32_t rem = n - di * HW;
         const uint32_t oh = udiv(rem, h.mag_w);
         const uint32_t ow = rem - oh * W;
-        hb[ks][e] = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+        const int hp = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const int x = (hp + d - 1) * 64 + cbyte;
+          hbw[ks][e][d] = x ^ ((x >> 4) & 32);
+        }
       }
   };
   // DMA instruction j of a tile: dy rows (0..3), halo chunk 0 (4..10), halo chunk 1 (11..17)
@@ -644,9 +655,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[km][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
   const int hoff = HW_DBYTES + (wave >> 1) * HW_HBYTES;
-  const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
   if (ntiles > 0) {
     prep(z);
     issue(0);
@@ -654,9 +663,13 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   for (int k = 0; k < ntiles; ++k) {
     const int st = k & 1;
     wait_all_barrier();
-    int hbk[4][2];
+    int hbk[4][2][3];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) { hbk[ks][0] = hb[ks][0]; hbk[ks][1] = hb[ks][1]; }
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) hbk[ks][e][d] = hbw[ks][e][d];
     const bool more = k + 1 < ntiles;
     if (more) prep(z + (k + 1) * h.Z);  // next tile's 18 DMAs: one per 2 tap-steps below
     const char* sbase = smem + st * HW_STAGE;
@@ -667,12 +680,11 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sbase + ks * 4096, 16 * km, lane);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int base = st * HW_STAGE + hoff + cbyte + 64 * h.toff[t];
-        const int x0 = hbk[ks][0] * 64 + base, x1 = hbk[ks][1] * 64 + base;
+        const int base = st * HW_STAGE + hoff + (t / 3 - 1) * W2 * 64;  // wave-uniform
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + (x0 ^ ((x0 >> 4) & 32))));
+            LDS_PTR(s16x4, smem + base + hbk[ks][0][t % 3]));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + (x1 ^ ((x1 >> 4) & 32))));
+            LDS_PTR(s16x4, smem + base + hbk[ks][1][t % 3]));
         s16x8 r;
         r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
         r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -810,6 +822,8 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ halo wgrad host
+static int halo_wgrad_pitch(int W) { return (W + 2 + 15) / 16 * 16; }
+
 static bool halo_wgrad_geom(const WGradArgs& a) {
   if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1)
     return false;
@@ -820,7 +834,7 @@ static bool halo_wgrad_geom(const WGradArgs& a) {
     return false;
   const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
   const int64_t seps = (HW_BM - 1) / HW + 1;
-  return (rows + 2 + seps) * (a.W + 2) <= HW_HPX;
+  return (rows + 2 + seps) * halo_wgrad_pitch(a.W) <= HW_HPX;
 }
 
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols) {
@@ -835,7 +849,8 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
 // slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   HaloWPlan h{};
-  const int W2 = a.W + 2;
+  const int W2 = halo_wgrad_pitch(a.W);
+  h.w2 = W2;
   for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);
   h.mag_w = magic(a.W);
   h.mag_w2 = magic(W2);

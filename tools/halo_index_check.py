@@ -14,8 +14,8 @@ def udiv(n, m):
     return (n * m) >> 32
 
 
-def check(N, H, W, BM=256, HPX=576):
-    HW, W2 = H * W, W + 2
+def check(N, H, W, BM=256, HPX=576, pitch=None):
+    HW, W2 = H * W, (pitch(W) if pitch else W + 2)
     M = N * HW
     rows = (BM - 1 + W - 1) // W + 1
     seps = (BM - 1) // HW + 1
@@ -58,4 +58,5 @@ if __name__ == "__main__":
     for case in [(2, 56, 56), (3, 28, 28), (5, 14, 14), (7, 7, 7), (3, 9, 11), (1, 5, 3),
                  (2, 35, 35), (4, 1, 1), (3, 2, 2), (64, 7, 7), (2, 17, 17)]:
         print(case, "fwd/dgrad (256-px tiles):", check(*case),
-              "| wgrad (128-px tiles):", check(*case, BM=128, HPX=448))
+              "| wgrad (128-px tiles, pitch W+2 -> x16):",
+              check(*case, BM=128, HPX=448, pitch=lambda w: (w + 2 + 15) // 16 * 16))
