@@ -50,8 +50,9 @@ constexpr int HB_RED = HB_NW * HB_BN * 2 * 4;   // epilogue cross-wave statistic
 constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED;  // 149,504 B
 
 struct HaloPlan {
-  int toff[9];          // halo pixel offset of tap t: dh * (W + 2) + dw, dh/dw in {-1,0,1}
-  int btoff[9];         // byte offset of tap t's weight row segment: bt[t] * aC * 2
+  int w2;               // halo row pitch P: W + 1 (one shared zero column) rounded up to 8
+  int btoff[9];         // tap t = (dh + 1) * 3 + (dw + 1): byte offset bt * aC * 2 of its
+                        // weight row segment (the host orders any 3x3 tap table this way)
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;  // floor(2^32 / d) + 1: exact n / d for n*d < 2^32
   int tiles_m, tiles_total, cc;
   uint32_t a_bytes, b_bytes;
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = p.aH, W = p.aW, HW = H * W, W2 = W + 2, aC = p.aC;
+  const int H = p.aH, W = p.aW, HW = H * W, W2 = h.w2, aC = p.aC;
   const int nimg = p.M / HW;
   const int jq = lane >> 4, l15 = lane & 15;
 
@@ -360,7 +361,11 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
 
   // B fragment byte offsets (tap 0, column group 0): row l15 of the [tap][64][32] image
   const int boff = l15 * 64 + ((jq ^ ((l15 >> 1) & 2)) << 4);
-  int xb[4];  // 64 * halo pixel + 16 * chunk of this lane's output row, per row fragment
+  // Swizzled LDS byte address of this lane's A row in each row fragment for column tap
+  // dw = d - 1: X = 64 * (pixel + dw) + 16 * chunk, chunk position flipped by pixel bit 2
+  // (X bit 8).  The pitch is a multiple of 8 pixels, so a row tap dh adds dh*P*64 without
+  // touching bits 0..8: a tap's address is xbw[i][dw + 1] + dh*P*64 (+ stage) - 1 VALU.
+  int xbw[4][3];
   EpiIn ein;
   f32x4 acc[4][4];
 
@@ -387,8 +392,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
     auto load = [&](int i, int t) {
-      const int x = xb[i] + hbase + 64 * h.toff[t];
-      return frag16(hal + (x ^ ((x >> 3) & 32)));
+      return frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
     };
     if constexpr (!WRES) {
       // deep-K layers (CC >= 4 chunks per tile): tap-outer, all 16 fragments per tap (the
@@ -486,7 +490,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
           const uint32_t rem = n - di * HW;
           const uint32_t oh = udiv(rem, h.mag_w);
           const uint32_t ow = rem - oh * W;
-          xb[i] = ((((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1) << 6) + (jq << 4);
+          const int hp = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+#pragma unroll
+          for (int d = 0; d < 3; ++d) {
+            const int x = ((hp + d - 1) << 6) + (jq << 4);
+            xbw[i][d] = x ^ ((x >> 3) & 32);
+          }
         }
         if (WRES && prev_m0 >= 0) {
           mma_chunk(st, 0, std::true_type{}, [&](int hn, int i) {
@@ -731,6 +740,10 @@ static int num_cus() {
   return n;
 }
 
+// halo row pitch: W pixels + one zero column shared by consecutive rows (a row's right
+// border is the next row's left border), rounded up to 8 pixels
+static int halo_pitch(int W) { return (W + 1 + 7) / 8 * 8; }
+
 // epilogue flavour of a launch; -1: not instantiated (the implicit GEMM runs it)
 static int halo_epi(const IGemmArgs& a) {
   int e = 0;
@@ -757,10 +770,13 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   if ((int64_t)a.M * a.ldc >= (1ll << 31) || a.ldc < a.N) return false;
   if (halo_epi(a) < 0) return false;  // an epilogue flavour without an instantiation
   if (a.Ktot != 9 * a.aC) return false;
+  int seen = 0;  // every (dh, dw) in {-1,0,1}^2 exactly once
   for (int t = 0; t < 9; ++t) {
     const int dh = a.Oh + a.taps.dh[t], dw = a.Ow + a.taps.dw[t];
     if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return false;
+    seen |= 1 << ((dh + 1) * 3 + dw + 1);
   }
+  if (seen != 511) return false;
   const int64_t HW = (int64_t)a.aH * a.aW;
   if (a.M % HW != 0 || HW + HB_BM >= 65536 || a.aW + 2 > 255) return false;
   if ((int64_t)a.M * a.aC * 2 >= (1ll << 31)) return false;
@@ -768,7 +784,9 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   // halo slots of any 256-pixel tile: rows touched + 2 halo rows + image separators
   const int64_t rows = (HB_BM - 1 + a.aW - 1) / a.aW + 1;
   const int64_t seps = (HB_BM - 1) / HW + 1;
-  return (rows + 2 + seps) * (a.aW + 2) <= HB_HPX;
+  // (+1: with P == W + 1 the last slot's right border is the next pixel)
+  const int P = halo_pitch(a.aW);
+  return (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
 }
 
 template <int EPI>
@@ -789,10 +807,11 @@ static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan&
 // returns the number of statistics-slab rows written (one per block, <= HALO_MAX_ROWS).
 int conv3_halo(IGemmArgs a, hipStream_t s) {
   HaloPlan h{};
-  const int W2 = a.aW + 2;
-  for (int t = 0; t < 9; ++t) {
-    h.toff[t] = (a.Oh + a.taps.dh[t]) * W2 + (a.Ow + a.taps.dw[t]);
-    h.btoff[t] = a.taps.bt[t] * a.aC * 2;
+  const int W2 = halo_pitch(a.aW);
+  h.w2 = W2;
+  for (int t = 0; t < 9; ++t) {  // raster (dh, dw) order, whatever order the table had
+    const int r = (a.Oh + a.taps.dh[t] + 1) * 3 + (a.Ow + a.taps.dw[t] + 1);
+    h.btoff[r] = a.taps.bt[t] * a.aC * 2;
   }
   h.mag_w = magic(a.aW);
   h.mag_w2 = magic(W2);

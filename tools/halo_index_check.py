@@ -19,7 +19,7 @@ def check(N, H, W, BM=256, HPX=576, pitch=None):
     M = N * HW
     rows = (BM - 1 + W - 1) // W + 1
     seps = (BM - 1) // HW + 1
-    if (rows + 2 + seps) * W2 > HPX:
+    if (rows + 2 + seps) * W2 + (1 if W2 == W + 1 else 0) > HPX:
         return "not eligible"
     mw2, mh1, mhw, mw = magic(W2), magic(H + 1), magic(HW), magic(W)
     for mt in range((M + BM - 1) // BM):
@@ -35,6 +35,7 @@ def check(N, H, W, BM=256, HPX=576, pitch=None):
             row = v - d * (H + 1)
             img = img0 + d
             lds[hp] = (img, row, col) if (row < H and 0 <= col < W and img < N) else None
+        lds[HPX] = "outside the halo image"
         r0 = m0 - img0 * HW
         mlast = M - 1 - img0 * HW
         for rel in range(BM):
@@ -57,6 +58,7 @@ def check(N, H, W, BM=256, HPX=576, pitch=None):
 if __name__ == "__main__":
     for case in [(2, 56, 56), (3, 28, 28), (5, 14, 14), (7, 7, 7), (3, 9, 11), (1, 5, 3),
                  (2, 35, 35), (4, 1, 1), (3, 2, 2), (64, 7, 7), (2, 17, 17)]:
-        print(case, "fwd/dgrad (256-px tiles):", check(*case),
+        print(case, "fwd/dgrad (256-px tiles, pitch W+1 -> x8):",
+              check(*case, pitch=lambda w: (w + 1 + 7) // 8 * 8),
               "| wgrad (128-px tiles, pitch W+2 -> x16):",
               check(*case, BM=128, HPX=448, pitch=lambda w: (w + 2 + 15) // 16 * 16))
