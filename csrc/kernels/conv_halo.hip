@@ -370,13 +370,14 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   f32x4 acc[4][4];
 
   // Epilogue of fragment (i, jn) of the tile at m0e (operands ia / ib from epi_preload).
-  auto epi_fr = [&](int i, int jn, int m0e, auto full) {
+  auto epi_fr = [&](int i, int jn, int m0e, auto full, const EpiIn& in) {
     constexpr bool F = decltype(full)::value;
     const int m = m0e + wave * 64 + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
-    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb[jn],
+    epi_frag<EPI, F>(p, acc[i][jn], in.a[i][jn], in.b[i][jn], m < p.M, jn, orow, colb[jn],
                      cols[jn], ss[jn], sq[jn]);
   };
+  EpiIn einp;  // resident-weight path: the previous tile's operands (fused epilogue)
 
   // One 32-channel chunk, all 9 taps, in 8 regions (column half hn, row fragment i): a
   // region holds the 18 B fragments of its column half in registers (72 VGPRs) and runs
@@ -454,24 +455,25 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // One tile: CC items through the 2-stage ring.  The previous tile's epilogue runs inside
-  // this tile's first chunk (above); its operands are preloaded at the top of the previous
-  // tile's last chunk, before that item's DMAs are issued (an in-order vmcnt wait for a
-  // load issued behind the DMAs would wait for them too).
+  // One tile: CC items through the 2-stage ring.  Epilogue operands (accumulate: old
+  // output; fused BN reduction: z, y) are loaded right after an item's top wait, so they
+  // are in flight under that item's MFMAs and complete before the next wait - resident-
+  // weight tiles load at chunk 0 (the previous tile's set moves to einp for the fused
+  // epilogue of this chunk), deep-K tiles at chunk CC - 2.
   auto run_tile = [&](int tk, int prev_m0) {
     const int m0 = m0_of(tk);
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       const int st = k & 1;
-      if (WRES && cc == 0 && prev_m0 >= 0 && CC == 1) {
-        // single-chunk tiles: the previous tile's operands are consumed in THIS item, so
-        // the preload for this tile happens after it (below)
-      } else if (cc == CC - 1) {
-        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
-      }
       // this item's DMAs were issued during the previous item's MFMAs; the next item's
       // are issued during this one's (stage st ^ 1 was freed by the previous barrier)
       wait_all_barrier();
+      if (cc == (WRES ? 0 : max(CC - 2, 0))) {
+        if constexpr ((EPI & (EP_BETA | EP_BNRED)) != 0) {
+          if (WRES) einp = ein;
+        }
+        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
+      }
       const bool more = k + 1 < nitems;
       const int cc1 = cc + 1 == CC ? 0 : cc + 1;
       if (more && cc1 == 0) prep_tile(tk + 1);
@@ -499,8 +501,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
         }
         if (WRES && prev_m0 >= 0) {
           mma_chunk(st, 0, std::true_type{}, [&](int hn, int i) {
-            epi_fr(i, 2 * hn, prev_m0, std::true_type{});  // previous tile: always full
-            epi_fr(i, 2 * hn + 1, prev_m0, std::true_type{});
+            epi_fr(i, 2 * hn, prev_m0, std::true_type{}, einp);  // previous tile: full
+            epi_fr(i, 2 * hn + 1, prev_m0, std::true_type{}, einp);
           }, nd);
         } else {
           mma_chunk(st, 0, std::true_type{}, [](int, int) {}, nd);
@@ -508,15 +510,11 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       } else {
         mma_chunk(st, cc, std::false_type{}, [](int, int) {}, nd);
       }
-      if (WRES && cc == 0 && prev_m0 >= 0 && CC == 1) {
-        // (the item's global loads were waited above; these complete before the next wait)
-        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
-      }
       if (!WRES && cc == CC - 1 && tk + 1 < ntiles) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{});
+          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{}, ein);
       }
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
       // after its top barrier, which every wave passes only once done reading stage st)
@@ -529,7 +527,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
+      for (int jn = 0; jn < 4; ++jn)
+        epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{}, ein);
   }
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
 }
