@@ -11,9 +11,10 @@
 // input rows its 256 output pixels touch plus a one-pixel halo ONCE, and runs all nine taps
 // out of LDS: 67-77 MAC per staged byte, and 185 when the whole weight tile stays resident.
 //
-//  * LDS halo image: "slots" of W+2 pixels (zero column left and right), one input row per
-//    slot, one zero slot between consecutive images, so every tap is a uniform pixel offset
-//    dh*(W+2)+dw and no lane ever tests a border.  Slot s of a tile whose first output row
+//  * LDS halo image: "slots" of P pixels, one input row per slot, P = W + 1 rounded up to
+//    8: a row's right border column is the next row's left border (one shared zero column),
+//    and one zero slot separates consecutive images, so every tap is a uniform pixel offset
+//    dh*P + dw and no lane ever tests a border.  Slot s of a tile whose first output row
 //    is (img0, oh0) holds input row v = s + oh0 - 1 of the image sequence with period H+1
 //    (row H of each period = the zero separator).
 //  * Pixel rows are 64 B (32 bf16 channels, four 16-B chunks).  Chunk c of row r sits at
@@ -21,18 +22,21 @@
 //    chunk l/16) of ANY 16 consecutive rows - the taps shift halo rows by arbitrary
 //    amounts - touches every bank once per lane group (brute-force checked for all 64
 //    alignments; the engine's aligned-row swizzle kc_off conflicts 2-way off alignment).
-//    The weight image [tap][64 cols][32 k] uses the same rows and swizzle.
+//    The weight image [tap][64 cols][32 k] uses the same rows and swizzle.  P % 8 == 0, so
+//    a row tap never moves the swizzle bit and A addresses are precomputed per column tap.
 //  * Staging is buffer_load_dwordx4 ... lds: the swizzle moves to the source (lane on
-//    chunk position q of row r fetches chunk q ^ (2 * ((r>>2)&1))), border / out-of-tensor lanes
-//    get an offset past num_records and the hardware returns zeros, the chunk step moves the
-//    descriptor base (scalar), so a DMA costs no VALU in the loop.
+//    chunk position q of row r fetches chunk q ^ (2 * ((r>>2)&1))), border / out-of-tensor
+//    lanes get an offset past num_records and the hardware returns zeros, the chunk step
+//    moves the descriptor base (scalar), so a DMA costs no VALU.  The next item's DMAs are
+//    issued inside the current item's MFMA stream (an LDS-DMA costs its wave 60-180
+//    cycles of issue; as a burst in front of the wait they stalled every item).
 //  * Persistent blocks (one 4-wave block per CU, 146 KiB LDS): work items (tile, chunk) run
-//    through a 2-stage ring, item k+1's DMAs overlap item k's 144 MFMAs per wave and the
-//    epilogue of the previous tile; XCD x owns a contiguous share of the tile list.
+//    through a 2-stage ring; XCD x owns a contiguous share of the tile list.
 //  * WRES (64-wide outputs, <= 64 input channels, e.g. ResNet layer1): the 64 x 9 x C weight
 //    tile is loaded once per block and only the halo streams.
-//  * Epilogue = the rows engine's (igemm_common.h): bias, ReLU, BN statistics slab, fused
-//    BN-backward reduction, accumulate (GradJoin).
+//  * Lean epilogue (bias, ReLU, BN statistics, fused BN-backward reduction, accumulate for
+//    GradJoin) after each tile; BN statistics accumulate in registers across all of a
+//    block's tiles and are written once per block.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -369,98 +373,53 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   EpiIn ein;
   f32x4 acc[4][4];
 
-  // Epilogue of fragment (i, jn) of the tile at m0e (operands ia / ib from epi_preload).
-  auto epi_fr = [&](int i, int jn, int m0e, auto full, const EpiIn& in) {
+  // Epilogue of fragment (i, jn) of the tile at m0e (operands from epi_preload).
+  auto epi_fr = [&](int i, int jn, int m0e, auto full) {
     constexpr bool F = decltype(full)::value;
     const int m = m0e + wave * 64 + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
-    epi_frag<EPI, F>(p, acc[i][jn], in.a[i][jn], in.b[i][jn], m < p.M, jn, orow, colb[jn],
+    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb[jn],
                      cols[jn], ss[jn], sq[jn]);
   };
-  EpiIn einp;  // resident-weight path: the previous tile's operands (fused epilogue)
 
-  // One 32-channel chunk, all 9 taps, in 8 regions (column half hn, row fragment i): a
-  // region holds the 18 B fragments of its column half in registers (72 VGPRs) and runs
-  // 9 taps x 2 MFMAs for one row fragment.  Regions are fenced with sched_barrier (the
-  // scheduler would otherwise hoist every A read of the chunk and exceed 512 VGPRs); each
-  // prefetches the next region's first A fragment.  side(hn, i) runs inside the region, so
-  // its VALU fills the MFMA shadow: in a tile's FIRST chunk it is the previous tile's
-  // epilogue of exactly the two fragments this region is about to restart from zero.
-  // A: X = 64 * pixel + 16 * chunk (+ stage); the swizzle flips bit 5 by pixel bit 2 (= X
-  // bit 8): 3 VALU per fragment.
-  auto mma_chunk = [&](int st, int cc, auto first, auto side, auto nd) {
+  // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + 4 B fragments (the next
+  // tap's 8 reads in flight under this tap's 16 MFMAs) and two of the next item's 18
+  // LDS-DMAs in the MFMA shadow.  FIRST: the tile's first chunk (accumulators start at 0).
+  // (Measured: a row-major body that held the chunk's B fragments in registers and ran the
+  // previous tile's epilogue interleaved with the next tile's MFMAs was 10-15 % slower once
+  // the DMA issue moved into the MFMA stream and the A addresses were precomputed.)
+  auto mma_chunk = [&](int st, int cc, auto first, auto nd) {
     constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    auto load = [&](int i, int t) {
-      return frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
+    bf16x8 a2[2][4], b2[2][4];
+    auto ld = [&](int t, int b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
-    if constexpr (!WRES) {
-      // deep-K layers (CC >= 4 chunks per tile): tap-outer, all 16 fragments per tap (the
-      // next tap's 8 reads in flight under 16 MFMAs); the epilogue runs after the tile
-      bf16x8 a2[2][4], b2[2][4];
-      auto ld = [&](int t, int b) {
+    ld(0, 0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a2[b][i] = load(i, t);
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
-        for (int jn = 0; jn < 4; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
-      };
-      ld(0, 0);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jn = 0; jn < 4; ++jn)
-            acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
-                                (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
-        nd(2 * t);  // the next item's 18 DMAs, two per tap, in the MFMA shadow
-        nd(2 * t + 1);
-      }
-      return;
+        for (int jn = 0; jn < 4; ++jn)
+          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
+                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+      nd(2 * t);
+      nd(2 * t + 1);
     }
-    bf16x8 af[2];
-    af[0] = load(0, 0);
-#pragma unroll
-    for (int hn = 0; hn < 2; ++hn) {
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 bfr[9][2];
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bfr[t][j] = frag16(wimg + t * (HB_BN * 64) + (2 * hn + j) * 1024);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i) __builtin_amdgcn_sched_barrier(0);
-        side(hn, i);
-        nd(4 * hn + i);  // the next item's 9 halo DMAs: one per region (+1 in the first)
-        if (hn == 0 && i == 0) nd(8);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int b = (i * 9 + t) & 1;
-          if (t + 1 < 9) af[b ^ 1] = load(i, t + 1);
-          else if (i + 1 < 4) af[b ^ 1] = load(i + 1, 0);
-          else if (hn == 0) af[b ^ 1] = load(0, 0);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int jn = 2 * hn + j;
-            acc[i][jn] = mfma16(bfr[t][j], af[b],
-                                (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
   };
 
-  // One tile: CC items through the 2-stage ring.  Epilogue operands (accumulate: old
-  // output; fused BN reduction: z, y) are loaded right after an item's top wait, so they
-  // are in flight under that item's MFMAs and complete before the next wait - resident-
-  // weight tiles load at chunk 0 (the previous tile's set moves to einp for the fused
-  // epilogue of this chunk), deep-K tiles at chunk CC - 2.
-  auto run_tile = [&](int tk, int prev_m0) {
+  // One tile: CC items through the 2-stage ring, then its epilogue.  The epilogue operands
+  // (accumulate: old output; fused BN reduction: z, y) are loaded right after the top wait
+  // of the tile's second-to-last item, so they are in flight under its MFMAs (a load issued
+  // in front of a wait would be waited for with the DMAs).
+  auto run_tile = [&](int tk) {
     const int m0 = m0_of(tk);
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
@@ -468,12 +427,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       // this item's DMAs were issued during the previous item's MFMAs; the next item's
       // are issued during this one's (stage st ^ 1 was freed by the previous barrier)
       wait_all_barrier();
-      if (cc == (WRES ? 0 : max(CC - 2, 0))) {
-        if constexpr ((EPI & (EP_BETA | EP_BNRED)) != 0) {
-          if (WRES) einp = ein;
-        }
-        epi_preload<EPI>(p, ein, m0, n0, wave, lane);
-      }
+      if (cc == max(CC - 2, 0)) epi_preload<EPI>(p, ein, m0, n0, wave, lane);
       const bool more = k + 1 < nitems;
       const int cc1 = cc + 1 == CC ? 0 : cc + 1;
       if (more && cc1 == 0) prep_tile(tk + 1);
@@ -499,36 +453,28 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
             xbw[i][d] = x ^ ((x >> 3) & 32);
           }
         }
-        if (WRES && prev_m0 >= 0) {
-          mma_chunk(st, 0, std::true_type{}, [&](int hn, int i) {
-            epi_fr(i, 2 * hn, prev_m0, std::true_type{}, einp);  // previous tile: full
-            epi_fr(i, 2 * hn + 1, prev_m0, std::true_type{}, einp);
-          }, nd);
-        } else {
-          mma_chunk(st, 0, std::true_type{}, [](int, int) {}, nd);
-        }
+        mma_chunk(st, 0, std::true_type{}, nd);
       } else {
-        mma_chunk(st, cc, std::false_type{}, [](int, int) {}, nd);
+        mma_chunk(st, cc, std::false_type{}, nd);
       }
-      if (!WRES && cc == CC - 1 && tk + 1 < ntiles) {
+      if (cc == CC - 1 && tk + 1 < ntiles) {  // full tile (only the last can end past M)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{}, ein);
+          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{});
       }
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
       // after its top barrier, which every wave passes only once done reading stage st)
     }
   };
 
-  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, tk > 0 ? m0_of(tk - 1) : -1);
+  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk);
   if (ntiles > 0) {
     const int m0l = m0_of(ntiles - 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn)
-        epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{}, ein);
+      for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
   }
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
 }
