@@ -712,6 +712,65 @@ Tensor dropout_bwd(Tensor dy, Tensor mask, double p) {
   return dx;
 }
 
+// ----------------------------------------------------------------------- channel concat
+Tensor concat_channels(std::vector<Tensor> xs) {
+  TORCH_CHECK(!xs.empty(), "concat_channels: no inputs");
+  const Tensor& x0 = xs[0];
+  TORCH_CHECK(x0.dim() >= 2, "concat_channels: inputs must be [..., C]");
+  const int64_t pixels = x0.numel() / x0.size(-1);
+  std::vector<const mpa::bf16_raw*> ptrs;
+  std::vector<int> chans;
+  int64_t ctot = 0;
+  for (const Tensor& x : xs) {
+    CHECK_ACT(x);
+    TORCH_CHECK(x.dim() == x0.dim() && x.get_device() == x0.get_device(),
+                "concat_channels: rank/device mismatch");
+    for (int d = 0; d + 1 < x.dim(); ++d)
+      TORCH_CHECK(x.size(d) == x0.size(d), "concat_channels: leading dims differ");
+    TORCH_CHECK(x.size(-1) % 8 == 0, "concat_channels: channels must be a multiple of 8");
+    ptrs.push_back(bp(x));
+    chans.push_back((int)x.size(-1));
+    ctot += x.size(-1);
+  }
+  TORCH_CHECK(pixels * (ctot / 8) < (int64_t(1) << 31), "concat_channels: too large");
+  const c10::OptionalDeviceGuard g(device_of(x0));
+  std::vector<int64_t> shape(x0.sizes().begin(), x0.sizes().end());
+  shape.back() = ctot;
+  Tensor y = torch::empty(shape, x0.options());
+  if (pixels > 0)
+    mpa::concat_channels(ptrs.data(), chans.data(), (int)xs.size(), (int)pixels, (int)ctot,
+                         bpm(y), cur_stream());
+  return y;
+}
+
+std::vector<Tensor> split_channels(Tensor dy, std::vector<int64_t> sizes) {
+  CHECK_ACT(dy);
+  TORCH_CHECK(dy.dim() >= 2 && !sizes.empty(), "split_channels: dy must be [..., C]");
+  int64_t ctot = 0;
+  for (int64_t c : sizes) {
+    TORCH_CHECK(c > 0 && c % 8 == 0, "split_channels: channels must be a multiple of 8");
+    ctot += c;
+  }
+  TORCH_CHECK(ctot == dy.size(-1), "split_channels: sizes do not sum to C");
+  const int64_t pixels = dy.numel() / ctot;
+  TORCH_CHECK(pixels * (ctot / 8) < (int64_t(1) << 31), "split_channels: too large");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  std::vector<Tensor> out;
+  std::vector<mpa::bf16_raw*> ptrs;
+  std::vector<int> chans;
+  std::vector<int64_t> shape(dy.sizes().begin(), dy.sizes().end());
+  for (int64_t c : sizes) {
+    shape.back() = c;
+    out.push_back(torch::empty(shape, dy.options()));
+    ptrs.push_back(bpm(out.back()));
+    chans.push_back((int)c);
+  }
+  if (pixels > 0)
+    mpa::split_channels(bp(dy), chans.data(), (int)sizes.size(), (int)pixels, (int)ctot,
+                        ptrs.data(), cur_stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -765,5 +824,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad") = std::vector<int64_t>{});
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
+  m.def("concat_channels", &concat_channels);
+  m.def("split_channels", &split_channels);
   mpa_runtime::register_bindings(m);
 }

@@ -180,6 +180,13 @@ void adaptive_avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, 
 void adaptive_avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q,
                           bf16_raw* dx, hipStream_t s);
 
+// concat.hip (NHWC channel concat / split; every segment's channels % 8 == 0)
+constexpr int CAT_MAXSEG = 32;
+void concat_channels(const bf16_raw* const* xs, const int* chans, int nseg, int pixels,
+                     int ctotal, bf16_raw* y, hipStream_t s);
+void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, int ctotal,
+                    bf16_raw* const* dxs, hipStream_t s);
+
 // loss.hip
 // logits rows have stride ld >= NC (padded heads); ce_bwd writes dlogits with stride ld and
 // zeros in columns NC..ld-1

@@ -25,7 +25,7 @@ class _DenseLayer(nn.Module):
         self.conv2 = Conv2d(bn_size * growth_rate, growth_rate, 3, 1, 1, bias=False)
 
     def forward(self, feats):
-        x = feats[0] if len(feats) == 1 else torch.cat(feats, dim=-1)
+        x = feats[0] if len(feats) == 1 else Fn.cat_channels(feats)
         x = self.norm1(x, relu=True)
         x = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True)
         return self.conv2(x)
@@ -43,7 +43,7 @@ class _DenseBlock(nn.ModuleDict):
         feats = [x]
         for layer in self.values():
             feats.append(layer(feats))
-        return torch.cat(feats, dim=-1)
+        return Fn.cat_channels(feats)
 
 
 class _Transition(nn.Sequential):

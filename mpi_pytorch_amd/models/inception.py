@@ -40,7 +40,7 @@ def _max3s2(x):
 
 
 def _cat(xs):
-    return torch.cat(xs, dim=-1)
+    return Fn.cat_channels(xs)
 
 
 class InceptionA(nn.Module):

@@ -26,7 +26,7 @@ class Fire(nn.Module):
 
     def forward(self, x):
         s = self.squeeze(x, relu=True)
-        return torch.cat([self.expand1x1(s, relu=True), self.expand3x3(s, relu=True)], dim=-1)
+        return Fn.cat_channels([self.expand1x1(s, relu=True), self.expand3x3(s, relu=True)])
 
 
 class SqueezeNet(nn.Module):

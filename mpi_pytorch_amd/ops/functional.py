@@ -507,6 +507,29 @@ def adaptive_avg_pool2d(x, out_hw):
     return K(x).adaptive_avgpool_fwd(x, oh, ow)
 
 
+# ======================================================================== channel concat
+class _Concat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        ctx.sizes = [x.shape[-1] for x in xs]
+        return K(xs[0]).concat_channels(list(xs))
+
+    @staticmethod
+    def backward(ctx, dy):
+        return tuple(K(dy).split_channels(dy.contiguous(), ctx.sizes))
+
+
+def cat_channels(xs):
+    """NHWC channel concat (torchvision's ``torch.cat(dim=1)`` on NCHW) [K13]: one native
+    strided-copy kernel forward, the matching split kernel backward."""
+    xs = [x.contiguous() for x in xs]
+    if len(xs) == 1:
+        return xs[0]
+    if torch.is_grad_enabled() and any(x.requires_grad for x in xs):
+        return _Concat.apply(*xs)
+    return K(xs[0]).concat_channels(xs)
+
+
 # =============================================================================== dropout
 class DropoutRNG:
     """Per-device counter so every dropout call draws a fresh mask (graph-safe: the seed

@@ -374,5 +374,13 @@ def dropout_bwd(dy, mask, p):
     return (_f(dy) * mask.float() / (1 - p)).to(dy.dtype)
 
 
+def concat_channels(xs):
+    return torch.cat(list(xs), dim=-1)
+
+
+def split_channels(dy, sizes):
+    return [t.contiguous() for t in torch.split(dy, list(sizes), dim=-1)]
+
+
 def relu_fwd(x):
     return torch.relu(x)

@@ -752,3 +752,25 @@ def test_dropout(gpu):
     assert not torch.equal(m, m2)
     dx = C().dropout_bwd(torch.ones_like(x), m, 0.5)
     assert torch.allclose(dx.float(), m.float() * 2.0)
+
+
+@pytest.mark.parametrize("chans", [[64, 32], [256] + [32] * 24 + [32] * 9, [96, 64, 8, 192]])
+def test_concat_split_channels(gpu, chans):
+    """Native NHWC channel concat / split (concat.hip) against torch.cat / torch.split;
+    34 segments exercise the multi-launch path (CAT_MAXSEG = 32)."""
+    xs = [bf(3, 7, 5, c, dev=gpu) for c in chans]
+    y = C().concat_channels(xs)
+    assert torch.equal(y, ref.concat_channels(xs))
+    dy = bf(3, 7, 5, sum(chans), dev=gpu)
+    for a, b in zip(C().split_channels(dy, chans), ref.split_channels(dy, chans)):
+        assert a.is_contiguous() and torch.equal(a, b)
+
+
+def test_cat_channels_autograd(gpu):
+    from mpi_pytorch_amd.ops import functional as Fn
+    xs = [bf(2, 4, 4, c, dev=gpu).requires_grad_() for c in (16, 24)]
+    y = Fn.cat_channels(xs)
+    g = bf(*y.shape, dev=gpu)
+    y.backward(g)
+    assert torch.equal(y.detach(), torch.cat([x.detach() for x in xs], -1))
+    assert torch.equal(xs[0].grad, g[..., :16]) and torch.equal(xs[1].grad, g[..., 16:])
