@@ -43,7 +43,7 @@ def main(argv=None):
     p.add_argument("--optimizer", default="adam")
     p.add_argument("--lr", type=float, default=4e-4)
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"])
-    p.add_argument("--bucket-mb", type=float, default=64.0)
+    p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--comm-dtype", default="fp32")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")

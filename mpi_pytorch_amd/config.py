@@ -63,7 +63,7 @@ class Config:
     optimizer: str = "adam"                # adam | sgd
     momentum: float = 0.9
     weight_decay: float = 0.0
-    bucket_mb: float = 64.0                # gradient all-reduce bucket size (MiB)
+    bucket_mb: float = 16.0                # gradient all-reduce bucket size (MiB)
     grad_comm_dtype: str = "fp32"          # fp32 | bf16 (wire dtype of the gradient all-reduce)
     overlap_comm: bool = True              # launch bucket all-reduce during backward
     resume_epoch: bool = True              # honour saved epoch (reference restarts at 0: main.py:142)

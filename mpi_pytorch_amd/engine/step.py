@@ -31,7 +31,7 @@ from ..parallel import ParamArena, GradBucketer, sync_params, World
 
 
 def build_model(name: str, num_classes: int, feature_extract: bool, device: torch.device,
-                world: World, use_pretrained: bool = False, bucket_mb: float = 64.0,
+                world: World, use_pretrained: bool = False, bucket_mb: float = 16.0,
                 overlap: bool = True, comm_dtype: str = "fp32"):
     model, input_size = initialize_model(name, num_classes, feature_extract, use_pretrained)
     model = model.to(device)
@@ -131,7 +131,7 @@ class TrainStep:
 
 def build_training(name: str, num_classes: int, device, world: World, lr: float,
                    optimizer: str = "adam", momentum: float = 0.9, weight_decay: float = 0.0,
-                   feature_extract: bool = False, bucket_mb: float = 64.0, overlap: bool = True,
+                   feature_extract: bool = False, bucket_mb: float = 16.0, overlap: bool = True,
                    comm_dtype: str = "fp32"):
     model, input_size = build_model(name, num_classes, feature_extract, device, world,
                                     bucket_mb=bucket_mb, overlap=overlap, comm_dtype=comm_dtype)

@@ -6,7 +6,11 @@ Replaces the reference's per-parameter, blocking, post-backward loop
 Design for MI355X / RCCL over xGMI:
 
 * Buckets are cut from the flat fp32 gradient arena (:mod:`.arena`) at parameter
-  boundaries, ``bucket_mb`` each (a parameter larger than a bucket gets its own).  Since
+  boundaries, ``bucket_mb`` each (a parameter larger than a bucket gets its own).  The
+  default 16 MiB is sized for the exposed tail: the LAST bucket (layer2..stem) can only
+  start when backward ends, so it is kept small (ResNet-18 @64,500: 126 + 9 + 9.5 + 16 +
+  8.4 MiB), while 8-16 MiB messages still run near RCCL's large-message ring bandwidth
+  on one xGMI link per ring hop.  Since
   the arena is in reverse registration order, bucket 0 holds the classifier head, whose
   gradient is produced first; its all-reduce runs under the whole conv backward.
 * Each backward kernel calls ``arena.notify(p)`` after its weight-gradient launch.  When a
@@ -30,7 +34,7 @@ from .arena import ParamArena
 
 
 class GradBucketer:
-    def __init__(self, arena: ParamArena, world_size: int, bucket_mb: float = 64.0,
+    def __init__(self, arena: ParamArena, world_size: int, bucket_mb: float = 16.0,
                  overlap: bool = True, comm_dtype: str = "fp32", group=None):
         self.arena = arena
         self.world_size = world_size
@@ -45,7 +49,9 @@ class GradBucketer:
         end = 0
         for p in arena.trainable:
             o, e = arena.slice_of(p)
-            if cur and (e - start) > cap:
+            # close the bucket when p would overflow it - unless it is still tiny (the
+            # classifier bias ahead of the 126 MiB head weight): no sub-MiB collective
+            if cur and (e - start) > cap and (end - start) >= cap // 8:
                 self.buckets.append(cur)
                 self.ranges.append((start, end))
                 cur, start = [], o
