@@ -433,7 +433,8 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t kh, int6
 std::vector<Tensor> bn_relu_maxpool_fwd(Tensor z, Tensor stats, Tensor gamma, Tensor beta,
                                         Tensor rmean, Tensor rvar, double momentum, double eps,
                                         int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
-                                        int64_t pw, bool ceil, c10::optional<Tensor> counter) {
+                                        int64_t pw, bool ceil, c10::optional<Tensor> counter,
+                                        c10::optional<Tensor> zsel_out) {
   CHECK_ACT(z);
   TORCH_CHECK(kh * kw <= 256, "bn_relu_maxpool: window too large for uint8 argmax");
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
@@ -444,21 +445,33 @@ std::vector<Tensor> bn_relu_maxpool_fwd(Tensor z, Tensor stats, Tensor gamma, Te
   Tensor idx = empty_like_shape(z, {N, P, Q, C}, torch::kUInt8);
   Tensor mean = torch::empty({C}, z.options().dtype(torch::kFloat32));
   Tensor rstd = torch::empty({C}, z.options().dtype(torch::kFloat32));
+  mpa::bf16_raw* zsel = nullptr;
+  if (zsel_out && zsel_out->defined()) {
+    CHECK_ACT(*zsel_out);
+    TORCH_CHECK(zsel_out->sizes() == y.sizes(), "bn_relu_maxpool: zsel_out must be [N,P,Q,C]");
+    zsel = bpm(*zsel_out);
+  }
   mpa::bn_relu_maxpool_fwd(bp(z), fopt(stats), fopt(gamma), fopt(beta), fopt_mut(rmean),
                            fopt_mut(rvar), (float)momentum, (float)eps, N, H, W, C, P, Q, kh, kw,
                            sh, sw, ph, pw, bpm(y), idx.data_ptr<uint8_t>(), mean.data_ptr<float>(),
                            rstd.data_ptr<float>(),
                            (counter && counter->defined() && counter->numel() == 1)
                                ? counter->data_ptr<int64_t>() : nullptr,
-                           cur_stream());
+                           cur_stream(), zsel);
   return {y, idx, mean, rstd};
 }
 
 Tensor maxpool_bn_bwd(Tensor dp, Tensor idx, Tensor z, Tensor mean, Tensor rstd, Tensor gamma,
                       Tensor beta, Tensor dgamma, Tensor dbeta, int64_t kh, int64_t kw, int64_t sh,
-                      int64_t sw, int64_t ph, int64_t pw) {
+                      int64_t sw, int64_t ph, int64_t pw, c10::optional<Tensor> zsel) {
   CHECK_ACT(dp);
   CHECK_ACT(z);
+  const mpa::bf16_raw* zs = nullptr;
+  if (zsel && zsel->defined()) {
+    CHECK_ACT(*zsel);
+    TORCH_CHECK(zsel->sizes() == dp.sizes(), "maxpool_bn_bwd: zsel must match dp");
+    zs = bp(*zsel);
+  }
   const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
   const int P = dp.size(1), Q = dp.size(2);
   TORCH_CHECK(dp.size(0) == N && dp.size(3) == C && idx.sizes() == dp.sizes() && C % 8 == 0,
@@ -469,7 +482,7 @@ Tensor maxpool_bn_bwd(Tensor dp, Tensor idx, Tensor z, Tensor mean, Tensor rstd,
                            z.options().dtype(torch::kFloat32));
   mpa::maxpool_bn_bwd(bp(dp), idx.data_ptr<uint8_t>(), bp(z), fopt(mean), fopt(rstd), fopt(gamma),
                       fopt(beta), fopt_mut(dgamma), fopt_mut(dbeta), N, H, W, C, P, Q, kh, kw, sh,
-                      sw, ph, pw, bpm(dz), ws.data_ptr<float>(), cur_stream());
+                      sw, ph, pw, bpm(dz), ws.data_ptr<float>(), cur_stream(), zs);
   return dz;
 }
 
@@ -803,8 +816,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, py::arg("z"), py::arg("stats"),
         py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
-        py::arg("pw"), py::arg("ceil"), py::arg("counter") = py::none());
-  m.def("maxpool_bn_bwd", &maxpool_bn_bwd);
+        py::arg("pw"), py::arg("ceil"), py::arg("counter") = py::none(),
+        py::arg("zsel_out") = py::none());
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dp"), py::arg("idx"), py::arg("z"),
+        py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
+        py::arg("ph"), py::arg("pw"), py::arg("zsel") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("adaptive_avgpool_fwd", &adaptive_avgpool_fwd);

@@ -151,17 +151,20 @@ void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, 
 void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s);
 // fused BN(train) + ReLU + max-pool (stems): z [N][H][W][C] -> y [N][P][Q][C] + argmax idx;
 // backward: dp, idx, z -> dz (BN backward of the ReLU(BN) through the pool), ws of
-// maxpool_bn_ws_floats(N*H*W, C) floats; C % 8 == 0
+// maxpool_bn_ws_floats(N*H*W, C) floats; C % 8 == 0.  zsel (optional, [N][P][Q][C]): the raw
+// z at each window's argmax, written by the forward; with it the backward's reduction pass
+// reads only pooled-size tensors
 void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gamma,
                          const float* beta, float* rmean, float* rvar, float momentum, float eps,
                          int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
                          int ph, int pw, bf16_raw* y, uint8_t* idx, float* mean, float* rstd,
-                         int64_t* counter, hipStream_t s);
+                         int64_t* counter, hipStream_t s, bf16_raw* zsel = nullptr);
 int64_t maxpool_bn_ws_floats(int M, int C);
 void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, float* dgamma,
                     float* dbeta, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh,
-                    int sw, int ph, int pw, bf16_raw* dz, float* ws, hipStream_t s);
+                    int sw, int ph, int pw, bf16_raw* dz, float* ws, hipStream_t s,
+                    const bf16_raw* zsel = nullptr);
 
 // pool.hip  (NHWC)
 void maxpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, int kh, int kw,

@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, int C, PoolGeom g, bf16_t* __restrict__ y,
     uint8_t* __restrict__ idx, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter) {
+    unsigned long long* __restrict__ counter, bf16_t* __restrict__ zsel) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
@@ -668,10 +668,10 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const int t = r / g.Q;
     const int p = t % g.P;
     const int n = t / g.P;
-    float best[8];
+    float best[8], bz[8];
     int bi[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; bz[j] = 0.f; }
     if constexpr (K3S2) {
       // 3x3 / stride 2 / pad 1: all nine loads issued before any is consumed (out-of-range
       // taps read a clamped in-range pixel and are masked)
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float v = fmaxf(f[j] * sc[j] + sh[j], 0.f);
-            if (ok && v > best[j]) { best[j] = v; bi[j] = i * 3 + k; }
+            if (ok && v > best[j]) { best[j] = v; bi[j] = i * 3 + k; bz[j] = f[j]; }
           }
         }
     } else {
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float v = fmaxf(f[j] * sc[j] + sh[j], 0.f);
-            if (v > best[j]) { best[j] = v; bi[j] = i * g.kw + k; }
+            if (v > best[j]) { best[j] = v; bi[j] = i * g.kw + k; bz[j] = f[j]; }
           }
         }
       }
@@ -721,6 +721,58 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
     *(uint2*)(idx + o) = ib;
+    if (zsel) *(uint4*)(zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
+  }
+}
+
+// Backward reduction of the fused stem from POOLED tensors only: the pool gradient reaches
+// input pixel (n,h,w,c) only from windows whose argmax it is, and the ReLU mask there is
+// bn(z_argmax) > 0, so  sum_pixels g = sum_windows dp * [bn(zsel) > 0]  and
+// sum_pixels g * xhat = sum_windows dp * [bn(zsel) > 0] * xhat(zsel), with zsel the raw conv
+// output at each window's argmax (saved by the forward).  Reads dp + zsel (2 x pooled size)
+// instead of z + dp + idx (4 x + 1.5 x pooled size for a 3x3/s2 stem).
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_sel_reduce_kernel(
+    const bf16_t* __restrict__ dp, const bf16_t* __restrict__ zsel,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int C, int MP,
+    float* __restrict__ slab, float* __restrict__ sums) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; }
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sums[c0 + j] = 0.f; sums[C + c0 + j] = 0.f; }
+    }
+    float sc[8], sh[8], mu[8], rs[8];
+    bn_coeffs(mean, rstd, gamma, beta, c0, sc, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+#pragma unroll 2
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
+      const size_t o = (size_t)r * C + c0;
+      float d[8], zr[8];
+      unpack8(*(const uint4*)(dp + o), d);
+      unpack8(*(const uint4*)(zsel + o), zr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gr = (zr[j] * sc[j] + sh[j] > 0.f) ? d[j] : 0.f;
+        sg[j] += gr;
+        sgx[j] += gr * (zr[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  block_reduce8(sg, cm, red);
+  block_reduce8(sgx, cm, red);
+  if (cm.active && cm.r0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      slab[(size_t)blockIdx.x * 2 * C + cm.cc * 8 + j] = sg[j];
+      slab[(size_t)blockIdx.x * 2 * C + C + cm.cc * 8 + j] = sgx[j];
+    }
   }
 }
 
@@ -1038,13 +1090,13 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
                          const float* beta, float* rmean, float* rvar, float momentum, float eps,
                          int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
                          int ph, int pw, bf16_raw* y, uint8_t* idx, float* mean, float* rstd,
-                         int64_t* counter, hipStream_t s) {
+                         int64_t* counter, hipStream_t s, bf16_raw* zsel) {
   const PoolGeom g{N, H, W, P, Q, kh, kw, sh, sw, ph, pw};
   const bool k3 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1;
   hipLaunchKernelGGL(k3 ? bn_relu_maxpool_fwd_kernel<true> : bn_relu_maxpool_fwd_kernel<false>,
                      grid_for(N * P * Q, C, stem_grid(0)), dim3(256), 0, s, z, stats, gamma, beta,
                      rmean, rvar, momentum, eps, C, g, y, idx, mean, rstd,
-                     (unsigned long long*)counter);
+                     (unsigned long long*)counter, zsel);
 }
 
 int64_t maxpool_bn_ws_floats(int M, int C) {
@@ -1054,26 +1106,39 @@ int64_t maxpool_bn_ws_floats(int M, int C) {
 void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, float* dgamma,
                     float* dbeta, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh,
-                    int sw, int ph, int pw, bf16_raw* dz, float* ws, hipStream_t s) {
+                    int sw, int ph, int pw, bf16_raw* dz, float* ws, hipStream_t s,
+                    const bf16_raw* zsel) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials (as bn_bwd)
   const PoolGeom g{N, H, W, P, Q, kh, kw, sh, sw, ph, pw};
   const int M = N * H * W;
   float* slab = ws + 2 * C;
+  bool reduced = false;
+  if (zsel) {
+    const dim3 gr = grid_for(N * P * Q, C, stem_grid(1));
+    hipLaunchKernelGGL(maxpool_bn_bwd_sel_reduce_kernel, gr, dim3(256), 0, s, dp, zsel, mean,
+                       rstd, gamma, beta, C, N * P * Q, slab, ws);
+    slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+    reduced = true;
+  }
   if (pool_k3s2p1_even(g)) {
     const int cells = N * P * Q;
-    const dim3 gr = grid_for(cells, C, stem_grid(1));
-    hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<false>, gr, dim3(256), 0, s, dp, idx, z, mean,
-                       rstd, gamma, beta, nullptr, nullptr, nullptr, C, g, slab, ws, nullptr);
-    slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+    if (!reduced) {
+      const dim3 gr = grid_for(cells, C, stem_grid(1));
+      hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<false>, gr, dim3(256), 0, s, dp, idx, z, mean,
+                         rstd, gamma, beta, nullptr, nullptr, nullptr, C, g, slab, ws, nullptr);
+      slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+    }
     hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<true>, grid_for(cells, C, stem_grid(2)),
                        dim3(256), 0, s, dp, idx, z, mean, rstd, gamma, beta, ws, dgamma, dbeta, C,
                        g, nullptr, nullptr, dz);
     return;
   }
-  const dim3 gr = grid_for(M, C, stem_grid(1));
-  hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, gr, dim3(256), 0, s, dp, idx, z, mean, rstd,
-                     gamma, beta, C, g, slab, ws);
-  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+  if (!reduced) {
+    const dim3 gr = grid_for(M, C, stem_grid(1));
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, gr, dim3(256), 0, s, dp, idx, z, mean, rstd,
+                       gamma, beta, C, g, slab, ws);
+    slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+  }
   hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, grid_for(M, C, stem_grid(2)), dim3(256), 0, s, dp, idx, z,
                      mean, rstd, gamma, beta, ws, dgamma, dbeta, C, g, dz);
 }

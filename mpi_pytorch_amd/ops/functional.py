@@ -33,6 +33,7 @@ from ..parallel.arena import weight_of, weight_t_of, grad_sink, grad_done
 _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
 _NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
+_NO_ZSEL = os.environ.get("MPA_NO_ZSEL", "0") == "1"  # A/B: stem backward reduce from full z
 
 
 def K(t: torch.Tensor):
@@ -254,6 +255,14 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
                          _or_empty(residual, x), relu)
 
 
+def _pool_out(n: int, k: int, s: int, p: int, ceil: bool) -> int:
+    """Pooled extent, ATen's rule (a ceil-mode window must start inside the padded input)."""
+    o = (n + 2 * p - k + (s - 1 if ceil else 0)) // s + 1
+    if ceil and (o - 1) * s >= n + p:
+        o -= 1
+    return o
+
+
 class _ConvBNReLUPool(torch.autograd.Function):
     """maxpool(relu(bn(conv(x)))) -- the ResNet / DenseNet stem -- with BN, ReLU and the
     pool fused into one pass over the conv output z (forward) and the pool's gradient
@@ -269,25 +278,33 @@ class _ConvBNReLUPool(torch.autograd.Function):
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
         z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
                        _empty(x) if _NO_SHIFT else bn.running_mean)
+        # zsel: raw z at each window's argmax, so the backward's reduction pass reads only
+        # pooled-size tensors (maxpool_bn_bwd_sel_reduce_kernel)
+        zsel = None
+        if not _NO_ZSEL:
+            N, H, W, C_ = z.shape
+            zsel = torch.empty(N, _pool_out(H, cfg[0], cfg[2], cfg[4], cfg[6]),
+                               _pool_out(W, cfg[1], cfg[3], cfg[5], cfg[6]), C_,
+                               device=z.device, dtype=z.dtype)
         y, idx, mean, rstd = k.bn_relu_maxpool_fwd(z, stats, gamma, beta, bn.running_mean,
                                                    bn.running_var, bn.momentum_value(), bn.eps,
-                                                   *cfg, bn.num_batches_tracked)
+                                                   *cfg, bn.num_batches_tracked, zsel_out=zsel)
         ctx.conv = conv
         ctx.cfg = cfg
         ctx.bias = b
         ctx.params = (w, gamma, beta)
         ctx.in_hw = (x.shape[1], x.shape[2])
-        ctx.save_for_backward(x, z, idx, mean, rstd)
+        ctx.save_for_backward(x, z, idx, mean, rstd, zsel)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, z, idx, mean, rstd = ctx.saved_tensors
+        x, z, idx, mean, rstd, zsel = ctx.saved_tensors
         w, gamma, beta = ctx.params
         conv = ctx.conv
         k = K(dy)
         dz = k.maxpool_bn_bwd(dy.contiguous(), idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
-                              _sink(beta, dy), *ctx.cfg[:6])
+                              _sink(beta, dy), *ctx.cfg[:6], zsel=zsel)
         _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:

@@ -219,14 +219,20 @@ def maxpool_bwd(dy, idx, H, W, kh, kw, sh, sw, ph, pw, ceil):
 
 
 def bn_relu_maxpool_fwd(z, stats, gamma, beta, rmean, rvar, momentum, eps, kh, kw, sh, sw, ph,
-                        pw, ceil, counter=None):
+                        pw, ceil, counter=None, zsel_out=None):
     y, mean, rstd = bn_fwd_train(z, stats, gamma, beta, rmean, rvar, momentum, eps, None, True,
                                  counter)
     p, idx = maxpool_fwd(y, kh, kw, sh, sw, ph, pw, ceil)
+    if zsel_out is not None:  # raw z at each window's argmax
+        N, H, W, C = z.shape
+        flat = _nchw(idx).reshape(N, C, -1).long()  # ATen's flat h * W + w argmax
+        zs = _nchw(z).reshape(N, C, -1).gather(2, flat)
+        zsel_out.copy_(_nhwc(zs.reshape(N, C, p.shape[1], p.shape[2])))
     return p, idx, mean, rstd
 
 
-def maxpool_bn_bwd(dp, idx, z, mean, rstd, gamma, beta, dgamma, dbeta, kh, kw, sh, sw, ph, pw):
+def maxpool_bn_bwd(dp, idx, z, mean, rstd, gamma, beta, dgamma, dbeta, kh, kw, sh, sw, ph, pw,
+                   zsel=None):
     N, H, W, C = z.shape
     g = maxpool_bwd(dp, idx, H, W, kh, kw, sh, sw, ph, pw, False)
     # ReLU mask recomputed from z: bn(z) > 0

@@ -614,6 +614,21 @@ def test_bn_relu_maxpool_fused(gpu, case):
     dzr = ref.maxpool_bn_bwd(dp, gi, z, mean, rstd, g, b, dg2, db2, kh, kw, sh, sw, ph, pw)
     assert rel(dz, dzr) < 2e-2
     assert rel(dg, dg2) < 1e-2 and rel(db, db2) < 1e-2
+    # pooled-only reduction: the forward's zsel (raw z at each argmax) is exactly z gathered
+    # at the argmax, and the backward through it matches the full-z reduction
+    zsel = torch.empty_like(y)
+    rm3, rv3 = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    y3, idx3, _, _ = C().bn_relu_maxpool_fwd(z, st, g, b, rm3, rv3, 0.1, 1e-5, kh, kw, sh, sw,
+                                             ph, pw, ceil, zsel_out=zsel)
+    assert torch.equal(y3, y) and torch.equal(idx3, idx)
+    zg = torch.gather(z.permute(0, 3, 1, 2).reshape(N, Cc, -1), 2,
+                      gi.permute(0, 3, 1, 2).reshape(N, Cc, -1).long())
+    assert torch.equal(zg.reshape(N, Cc, *y.shape[1:3]).permute(0, 2, 3, 1), zsel)
+    dg3, db3 = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dz3 = C().maxpool_bn_bwd(dp, idx, z, mean, rstd, g, b, dg3, db3, kh, kw, sh, sw, ph, pw,
+                             zsel=zsel)
+    assert rel(dz3, dz) < 1e-2 and rel(dz3, dzr) < 2e-2
+    assert rel(dg3, dg) < 1e-4 and rel(db3, db) < 1e-4
 
 
 @pytest.mark.parametrize("case", POOL_CASES + [(2, 35, 35, 64, 3, 3, 1, 1, 1, 1, False),
