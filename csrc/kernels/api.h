@@ -116,6 +116,11 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a);
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);
 bool igemm_halo_enabled();
+// conv_stem.hip: direct row-staged forward of the 7x7 pixel-pair stem (super-tap layout,
+// 64 output channels); run_rows takes it when conv_stem_ok.  Returns the slab rows written.
+bool conv_stem_ok(const IGemmArgs& a);
+int conv_stem(IGemmArgs a, hipStream_t s);
+void igemm_set_stem(int on);  // MPA_STEM_DIRECT=0 disables (A/B, tests)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)

@@ -636,6 +636,14 @@ int64_t igemm_slab_floats(int M, int N) { return slab_rows_max(M) * 2 * N + 2 * 
 static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
   int BM, BN, splits;
   const bool dma = use_dma(vw);
+  if (dma && bkc && conv_stem_ok(a)) {  // 7x7 pixel-pair stem: row-staged direct conv
+    float* stats = a.stats;
+    float* sums = stats ? slab + slab_rows_max(a.M) * 2 * a.N : nullptr;
+    a.stats = stats ? slab : nullptr;
+    const int rows = conv_stem(a, s);
+    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s);
+    return;
+  }
   if (dma && bkc && conv3_halo_ok(a)) {  // 3x3 / stride 1: halo-staged direct conv
     float* stats = a.stats;
     float* sums = stats ? slab + slab_rows_max(a.M) * 2 * a.N : nullptr;

@@ -789,3 +789,31 @@ def test_cat_channels_autograd(gpu):
     y.backward(g)
     assert torch.equal(y.detach(), torch.cat([x.detach() for x in xs], -1))
     assert torch.equal(xs[0].grad, g[..., :16]) and torch.equal(xs[1].grad, g[..., 16:])
+
+
+@pytest.mark.parametrize("N,P,Q", [(3, 13, 37), (2, 16, 112), (1, 112, 112)])
+def test_conv_stem_direct(gpu, N, P, Q):
+    """Direct row-staged pixel-pair stem (conv_stem.hip) vs the implicit-GEMM engine on the
+    same super-tap layout: same K order, so bitwise-equal outputs; BN statistics (shifted
+    sums, different summation order) to fp32 rounding; and the fp32 oracle.  P % 8 != 0 and
+    Q % 16 != 0 exercise the partial item / partial subtile paths."""
+    torch.manual_seed(5)
+    x = bf(N, 2 * (P - 1) + 7, Q + 3, 8, dev=gpu, scale=0.5)
+    w = bf(64, 7, 4, 8, dev=gpu, scale=0.05)
+    e = torch.empty(0, device=gpu)
+    shift = torch.randn(64, device=gpu) * 0.1
+    outs = []
+    for on in (1, 0):
+        C().igemm_set_stem(on)
+        st = torch.empty(2, 64, device=gpu)
+        y = C().conv_fwd(x, w, e, 2, 1, 0, 0, False, st, shift)
+        outs.append((y, st))
+    C().igemm_set_stem(1)
+    (y1, s1), (y0, s0) = outs
+    assert y1.shape == (N, P, Q, 64)
+    assert torch.equal(y1, y0)
+    assert rel(s1, s0) < 1e-4
+    yr = ref.conv_fwd(x, w, e, 2, 1, 0, 0, False, None, None)
+    assert rel(y1, yr) < 1e-2
+    yf = y1.float().reshape(-1, 64)
+    assert rel(s1[0], yf.mean(0)) < 1e-3 and rel(s1[1], yf.var(0, unbiased=False)) < 1e-3
