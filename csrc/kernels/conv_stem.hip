@@ -12,8 +12,9 @@
 // batch-512 pass against a 121 us write floor (tools/stem_sweep.py).
 //
 // Design (gfx950, 64-wide waves, 160 KB LDS per CU):
-//   * persistent blocks of 8 waves, one per CU (grid <= 256 = one statistics-slab row each);
-//     a work item is 8 output rows of one image (8 x Q pixels);
+//   * persistent blocks of 8 waves, one per CU (grid <= 256 = one statistics-slab row
+//     each; MPA_STEM_CFG=1: 4 waves, two per CU); a work item is 8 (4) output rows of one
+//     image;
 //   * the item's (8 - 1) * sh + 7 canvas rows are staged ONCE into LDS (16-B vectors, plain
 //     loads into registers issued before the current item's MFMAs, written after them), so
 //     every A fragment - row q + kchunk of canvas row 2 pr + dh - is one ds_read_b128;
@@ -33,12 +34,7 @@ namespace mpa {
 
 namespace {
 constexpr int STEM_R = 7;             // kernel rows (7x7 stem)
-constexpr int STEM_ROWS = 8;          // output rows per work item
-constexpr int STEM_NW = 8;            // waves per block
-constexpr int STEM_MAX_CROWS = (STEM_ROWS - 1) * 2 + STEM_R;  // canvas rows, sh <= 2
 constexpr int STEM_MAX_WP = 120;      // canvas pairs per row (image width <= 232)
-constexpr int STEM_LDS = STEM_MAX_CROWS * STEM_MAX_WP * 16;   // 40,320 B
-constexpr int STEM_PREF = (STEM_LDS / 16 + STEM_NW * 64 - 1) / (STEM_NW * 64);  // vec / thread
 }  // namespace
 
 struct StemPlan {
@@ -48,7 +44,13 @@ struct StemPlan {
   int qsub;         // 16-pixel subtiles per output row: ceil(Q / 16)
 };
 
-__global__ __launch_bounds__(STEM_NW * 64, 1) void conv_stem_kernel(IGemmArgs p, StemPlan h) {
+// STEM_NW waves per block, STEM_ROWS output rows per item, STEM_OCC waves per SIMD
+template <int STEM_NW, int STEM_ROWS, int STEM_OCC>
+__global__ __launch_bounds__(STEM_NW * 64, STEM_OCC) void conv_stem_kernel(IGemmArgs p,
+                                                                           StemPlan h) {
+  constexpr int STEM_MAX_CROWS = (STEM_ROWS - 1) * 2 + STEM_R;  // canvas rows, sh <= 2
+  constexpr int STEM_LDS = STEM_MAX_CROWS * STEM_MAX_WP * 16;
+  constexpr int STEM_PREF = (STEM_LDS / 16 + STEM_NW * 64 - 1) / (STEM_NW * 64);  // vec/thread
   __shared__ __attribute__((aligned(16))) char canvas[STEM_LDS];
   __shared__ float red[STEM_NW][2][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -59,6 +61,7 @@ __global__ __launch_bounds__(STEM_NW * 64, 1) void conv_stem_kernel(IGemmArgs p,
   const bf16_t* __restrict__ A = (const bf16_t*)p.A;
   bf16_t* __restrict__ out = (bf16_t*)p.C;
 
+  static_assert(STEM_PREF * STEM_NW * 64 * 16 >= STEM_LDS, "prefetch covers the stage");
   // weights: lane holds W[n = 16 nb + li][dh][pair kc][0..7] for every (dh, nb)
   bf16x8 wf[STEM_R][4];
 #pragma unroll
@@ -212,16 +215,31 @@ bool conv_stem_ok(const IGemmArgs& a) {
   return true;
 }
 
-int conv_stem(IGemmArgs a, hipStream_t s) {
+// block shape: 0 = 8 waves x 8-row items, one block per CU; 1 = 4 waves x 4-row items, two
+// blocks per CU (one block's barrier / LDS-commit phase overlaps the other's MFMAs).
+// Measured equal at batch 512 (37.96k vs 38.01k img/s), so the default is the simpler 0.
+static int g_stem_cfg = [] {
+  const char* e = getenv("MPA_STEM_CFG");
+  return e ? atoi(e) : 0;
+}();
+
+template <int NW, int ROWS, int OCC>
+static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
   StemPlan h{};
-  h.items_img = (a.oH + STEM_ROWS - 1) / STEM_ROWS;
+  h.items_img = (a.oH + ROWS - 1) / ROWS;
   const int nimg = a.M / (a.oH * a.oW);
   h.items = nimg * h.items_img;
-  h.crows = (STEM_ROWS - 1) * a.Uh + STEM_R;
+  h.crows = (ROWS - 1) * a.Uh + STEM_R;
   h.qsub = (a.oW + 15) / 16;
-  const int grid = std::max(1, std::min(h.items, HALO_MAX_ROWS));
-  hipLaunchKernelGGL(conv_stem_kernel, dim3(grid), dim3(STEM_NW * 64), 0, s, a, h);
+  const int grid = std::max(1, std::min(h.items, max_blocks));
+  hipLaunchKernelGGL((conv_stem_kernel<NW, ROWS, OCC>), dim3(grid), dim3(NW * 64), 0, s, a, h);
   return grid;
+}
+
+int conv_stem(IGemmArgs a, hipStream_t s) {
+  // one statistics-slab row per block: the caller's slab holds >= slab_rows_max(M) rows
+  if (g_stem_cfg == 1 && (a.M + 127) / 128 >= 512) return launch_stem<4, 4, 2>(a, 512, s);
+  return launch_stem<8, 8, 1>(a, HALO_MAX_ROWS, s);
 }
 
 }  // namespace mpa

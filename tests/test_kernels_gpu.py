@@ -791,7 +791,7 @@ def test_cat_channels_autograd(gpu):
     assert torch.equal(xs[0].grad, g[..., :16]) and torch.equal(xs[1].grad, g[..., 16:])
 
 
-@pytest.mark.parametrize("N,P,Q", [(3, 13, 37), (2, 16, 112), (1, 112, 112)])
+@pytest.mark.parametrize("N,P,Q", [(3, 13, 37), (2, 16, 112), (1, 112, 112), (8, 112, 112)])
 def test_conv_stem_direct(gpu, N, P, Q):
     """Direct row-staged pixel-pair stem (conv_stem.hip) vs the implicit-GEMM engine on the
     same super-tap layout: same K order, so bitwise-equal outputs; BN statistics (shifted
