@@ -834,7 +834,17 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
   const int tiles_m = (a.Kout + BM - 1) / BM;
   a.tiles_total = tiles_m * a.tiles_n;
   const int ktiles = (a.Mpix + BK - 1) / BK;
-  splits = std::max(1, (512 + a.tiles_total - 1) / a.tiles_total);
+  // stem-shaped reductions (64 output rows, 129..256 columns, >= 1M pixels): two 64x128
+  // column tiles x 1024 splits beat one 64x256 tile x 512 splits (tools/stem_sweep.py at
+  // batch 512: 457 vs 501 us)
+  const bool stem2 = big && BM == 64 && BN == 256 && !(g_force_bm && g_force_bn) &&
+                     a.Ncols > 128 && a.Ncols <= 256;
+  if (stem2) {
+    BN = 128;
+    a.tiles_n = (a.Ncols + BN - 1) / BN;
+    a.tiles_total = tiles_m * a.tiles_n;
+  }
+  splits = std::max(1, ((stem2 ? 2048 : 512) + a.tiles_total - 1) / a.tiles_total);
   splits = std::min(splits, std::max(1, ktiles / 16));
   if (g_force_splits > 0) splits = std::min(g_force_splits, std::max(ktiles, 1));
   const int64_t out = (int64_t)a.Kout * a.Ncols;

@@ -62,3 +62,5 @@ for bm, bn, sp in [(0, 0, 0), (64, 256, 256), (64, 256, 1024), (64, 256, 2048), 
     print("wgrad %-14s %7.1f us  %5.0f TF/s" % ("auto" if not bm else "%dx%d/s%d" % (bm, bn, sp),
                                                  t, flop / t * 1e-6))
 C.igemm_force_tile(0, 0, 0)
+t = timeit(lambda: C.conv_wgrad(dy, x, dw, 2, 1, 0, 0))
+print("wgrad auto (again, after the forced tiles)  %7.1f us  %5.0f TF/s" % (t, flop / t * 1e-6))
