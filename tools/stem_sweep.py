@@ -56,7 +56,7 @@ t = timeit(lambda: y.zero_())
 print("write-only reference: zero_() of the %.0f MB output  %7.1f us (%.2f TB/s)" % (
     y.numel() * 2 / 1e6, t, y.numel() * 2 / t * 1e-6))
 for bm, bn, sp in [(0, 0, 0), (64, 256, 256), (64, 256, 1024), (64, 256, 2048), (64, 128, 0),
-                   (64, 128, 1024), (128, 256, 0)]:
+                   (64, 128, 512), (64, 128, 1024), (64, 128, 1536), (64, 128, 2048), (128, 256, 0)]:
     C.igemm_force_tile(bm, bn, sp)
     t = timeit(lambda: C.conv_wgrad(dy, x, dw, 2, 1, 0, 0))
     print("wgrad %-14s %7.1f us  %5.0f TF/s" % ("auto" if not bm else "%dx%d/s%d" % (bm, bn, sp),
