@@ -810,8 +810,8 @@ static void wgrad_vw(const WGradArgs& a, int vwa, int vwb, int splits, hipStream
   }
 }
 
-// split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB
-// split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB
+// split over pixels: ~512 blocks (2 per CU), >= 16 K-steps per split, slab <= 64 MiB;
+// stem-shaped reductions (see wgrad_plan) target ~1024 blocks instead
 // big: the 8-wave 128x256 LDS-DMA tile (measured +20..40 % over the 4-wave tiles for
 // Kout >= 256 and for the stem's tiny-output / huge-pixel-count reduction)
 static bool wgrad_big(const WGradArgs& a, bool dma_ok) {
@@ -835,8 +835,9 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
   a.tiles_total = tiles_m * a.tiles_n;
   const int ktiles = (a.Mpix + BK - 1) / BK;
   // stem-shaped reductions (64 output rows, 129..256 columns, >= 1M pixels): two 64x128
-  // column tiles x 1024 splits beat one 64x256 tile x 512 splits (tools/stem_sweep.py at
-  // batch 512: 457 vs 501 us)
+  // column tiles x 512 splits instead of one 64x256 tile x 512 splits
+  // (profiles/stem_sweep_b512.txt, batch 512: 64x128/s512 439.4 us, 64x128/s1024 449.2 us,
+  // 64x256/s512 493.7 us). 512 splits keep the fp32 slab at 29 MB (1024: 58.7 MB).
   const bool stem2 = big && BM == 64 && BN == 256 && !(g_force_bm && g_force_bn) &&
                      a.Ncols > 128 && a.Ncols <= 256;
   if (stem2) {
@@ -844,7 +845,7 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
     a.tiles_n = (a.Ncols + BN - 1) / BN;
     a.tiles_total = tiles_m * a.tiles_n;
   }
-  splits = std::max(1, ((stem2 ? 2048 : 512) + a.tiles_total - 1) / a.tiles_total);
+  splits = std::max(1, ((stem2 ? 1024 : 512) + a.tiles_total - 1) / a.tiles_total);
   splits = std::min(splits, std::max(1, ktiles / 16));
   if (g_force_splits > 0) splits = std::min(g_force_splits, std::max(ktiles, 1));
   const int64_t out = (int64_t)a.Kout * a.Ncols;

@@ -817,3 +817,42 @@ def test_conv_stem_direct(gpu, N, P, Q):
     assert rel(y1, yr) < 1e-2
     yf = y1.float().reshape(-1, 64)
     assert rel(s1[0], yf.mean(0)) < 1e-3 and rel(s1[1], yf.var(0, unbiased=False)) < 1e-3
+
+
+def test_conv_stem_wgrad_plan(gpu):
+    """Pixel-pair stem weight gradient at a production pixel count (>= 1M output pixels):
+    the auto plan (two 64x128 column tiles, split slab through wgrad_reduce, the
+    incremental-pixel DMA kernel with anisotropic stride (2, 1)) vs the fp32 oracle, and vs
+    the forced 64x256 / 64x128 single-split tiles (same K order per output -> fp32
+    rounding only)."""
+    torch.manual_seed(7)
+    N, P, Q = 96, 112, 112
+    x = bf(N, 2 * (P - 1) + 7, Q + 3, 8, dev=gpu, scale=0.5)
+    dy = bf(N, P, Q, 64, dev=gpu, scale=0.1)
+    assert N * P * Q >= (1 << 20)
+
+    def run():
+        dw = torch.zeros(64, 7, 4, 8, device=gpu)
+        C().conv_wgrad(dy, x, dw, 2, 1, 0, 0)
+        return dw
+
+    prev = C().igemm_engine()
+    try:
+        C().igemm_set_engine(1)
+        C().igemm_force_tile(0, 0, 0)
+        auto = run()
+        forced = []
+        for bm, bn in ((64, 256), (64, 128)):
+            C().igemm_force_tile(bm, bn, 1)
+            forced.append(run())
+    finally:
+        C().igemm_force_tile(0, 0, 0)
+        C().igemm_set_engine(prev)
+    dwr = torch.zeros(64, 7, 4, 8, device=gpu)
+    ref.conv_wgrad(dy, x, dwr, 2, 1, 0, 0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(auto).all()
+    assert rel(auto, dwr) < 1e-2
+    for f in forced:
+        assert rel(f, auto) < 1e-4 and rel(f, dwr) < 1e-2
+    assert rel(forced[0], forced[1]) < 1e-5
