@@ -35,7 +35,8 @@ __device__ __forceinline__ ColMap colmap(int cpr) {
 }
 
 // Tuning knobs (tools/bench_bn.py): MPA_BN_GRID = target block count, MPA_BN_UNR = rows in
-// flight per thread (1, 2 or 4).
+// flight per thread (1, 2 or 4).  Default 2: in the batch-512 ResNet-18 step (gpu_ab.sh,
+// two alternating repeats) UNR 2 runs 13.47 ms/step against 13.63 (UNR 1) and 13.49 (UNR 4).
 static int bn_grid_target() {  // 0: size-based default
   static const int v = [] {
     const char* e = getenv("MPA_BN_GRID");
@@ -46,8 +47,8 @@ static int bn_grid_target() {  // 0: size-based default
 static int bn_unr() {
   static const int v = [] {
     const char* e = getenv("MPA_BN_UNR");
-    const int u = e ? atoi(e) : 1;
-    return (u == 2 || u == 4) ? u : 1;
+    const int u = e ? atoi(e) : 2;
+    return (u == 1 || u == 4) ? u : 2;
   }();
   return v;
 }

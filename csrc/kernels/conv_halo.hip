@@ -60,6 +60,7 @@ struct HaloPlan {
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;  // floor(2^32 / d) + 1: exact n / d for n*d < 2^32
   int tiles_m, tiles_total, cc;
   uint32_t a_bytes, b_bytes;
+  int dbg;              // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
 };
 
 __device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t mag) { return __umulhi(n, mag); }
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       const int cc1 = cc + 1 == CC ? 0 : cc + 1;
       if (more && cc1 == 0) prep_tile(tk + 1);
       auto nd = [&](int j) {
-        if (more) dma(cc1, st ^ 1, j);
+        if (more && !h.dbg) dma(cc1, st ^ 1, j);
       };
       if (cc == 0) {
         const int img0 = m0 / HW;
@@ -507,6 +508,7 @@ struct HaloWPlan {
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;
   int tiles_m, parts, kparts, Z;
   uint32_t dy_bytes, x_bytes;
+  int dbg;  // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
 };
 
 __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
@@ -645,7 +647,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
         for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
-        if (more && ((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
+        if (more && !h.dbg && ((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
       }
     }
     // (no barrier: tile k + 2's DMAs into stage st follow tile k + 1's top barrier)
@@ -669,6 +671,10 @@ static bool g_halo = [] {
   return !(e && e[0] == '0');
 }();
 void igemm_set_halo(int on) { g_halo = on != 0; }
+static const int g_halo_dbg = [] {
+  const char* e = getenv("MPA_HALO_DBG");
+  return e ? atoi(e) : 0;
+}();
 bool igemm_halo_enabled() { return g_halo; }
 
 static uint32_t magic(uint32_t d) { return (uint32_t)((1ull << 32) / d + 1); }
@@ -752,6 +758,7 @@ static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan&
 // returns the number of statistics-slab rows written (one per block, <= HALO_MAX_ROWS).
 int conv3_halo(IGemmArgs a, hipStream_t s) {
   HaloPlan h{};
+  h.dbg = g_halo_dbg & 1;
   const int W2 = halo_pitch(a.aW);
   h.w2 = W2;
   for (int t = 0; t < 9; ++t) {  // raster (dh, dw) order, whatever order the table had
@@ -813,6 +820,7 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
 // slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   HaloWPlan h{};
+  h.dbg = g_halo_dbg & 1;
   const int W2 = halo_wgrad_pitch(a.W);
   h.w2 = W2;
   for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);

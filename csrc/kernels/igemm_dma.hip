@@ -517,10 +517,14 @@ void igemm_wgrad_dma_kernel(WGradArgs p) {
             ok ? p.x + (((size_t)b_img[i] * p.H + ih) * p.W + iw) * p.C + b_c[i]
                : zp;
         glds16(src, bimg + jb * 1024);
-        int ow = b_ow[i] + BK, oh = b_oh[i], img = b_img[i];
-        while (ow >= p.Q) { ow -= p.Q; ++oh; }
-        while (oh >= p.P) { oh -= p.P; ++img; }
-        b_ow[i] = ow; b_oh[i] = oh; b_img[i] = img;
+        if (PQ == 1) {  // Linear (1x1 "image"): the pixel IS the image index
+          b_img[i] += BK;
+        } else {
+          int ow = b_ow[i] + BK, oh = b_oh[i], img = b_img[i];
+          while (ow >= p.Q) { ow -= p.Q; ++oh; }
+          while (oh >= p.P) { oh -= p.P; ++img; }
+          b_ow[i] = ow; b_oh[i] = oh; b_img[i] = img;
+        }
       }
     }
   };
