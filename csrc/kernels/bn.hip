@@ -87,6 +87,39 @@ __device__ __forceinline__ void sweep_rows(const ColMap& cm, int M, F&& body) {
   for (; r < M; r += stride) body(r, stride, 1);
 }
 
+// Software-pipelined row sweep for the kernels that STORE per row: the loads of the next
+// UNR rows are issued before the current rows are processed and stored.  On CDNA, loads
+// and stores share the in-order vmcnt, so in the plain sweep the wait for row i+1's loads
+// also waited for row i's stores - a full write round trip per iteration.  Here the wait
+// for the prefetched rows leaves the stores issued after them in flight.
+// load(r, regs[u]) fills the NT 16-B vectors of row r; proc(r, regs[u]) consumes them.
+template <int UNR, int NT, typename L, typename P>
+__device__ __forceinline__ void sweep_rows_pl(const ColMap& cm, int M, L&& load, P&& proc) {
+  const int stride = gridDim.x * cm.rpi;
+  int r = blockIdx.x * cm.rpi + cm.r0;
+  if (r >= M) return;
+  uint4 cur[UNR][NT], nxt[UNR][NT];
+#pragma unroll
+  for (int u = 0; u < UNR; ++u)
+    if (r + u * stride < M) load(r + u * stride, cur[u]);
+  for (;;) {
+    const int rn = r + UNR * stride;
+    const bool more = rn < M;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (rn + u * stride < M) load(rn + u * stride, nxt[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (r + u * stride < M) proc(r + u * stride, cur[u]);
+    if (!more) break;
+    for (int u = 0; u < UNR; ++u)
+      for (int t = 0; t < NT; ++t) cur[u][t] = nxt[u][t];
+    r = rn;
+  }
+}
+
 // block-reduce 8-channel partials held per thread; returns sums in threads with r0 == 0
 __device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float* red) {
   __syncthreads();
@@ -159,36 +192,30 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
                                               const bf16_t* __restrict__ x,
                                               const bf16_t* __restrict__ res, int relu,
                                               bf16_t* __restrict__ y) {
-  sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
-    uint4 xv[UNR], rv[UNR];
+  sweep_rows_pl<UNR, 2>(
+      cm, M,
+      [&](int r, uint4 (&v)[2]) {
+        const size_t off = (size_t)r * C + c0;
+        v[0] = *(const uint4*)(x + off);
+        if (res) v[1] = *(const uint4*)(res + off);
+      },
+      [&](int r, uint4 (&v)[2]) {
+        float f[8];
+        unpack8(v[0], f);
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (u < n) {
-        const size_t off = (size_t)(r + u * st) * C + c0;
-        xv[u] = *(const uint4*)(x + off);
-        if (res) rv[u] = *(const uint4*)(res + off);
-      }
-    }
+        for (int j = 0; j < 8; ++j) f[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
+        if (res) {
+          float g[8];
+          unpack8(v[1], g);
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (u >= n) break;
-      float f[8];
-      unpack8(xv[u], f);
+          for (int j = 0; j < 8; ++j) f[j] += g[j];
+        }
+        if (relu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = __builtin_fmaf(f[j], sc[j], sh[j]);
-      if (res) {
-        float g[8];
-        unpack8(rv[u], g);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += g[j];
-      }
-      if (relu) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-      }
-      *(uint4*)(y + (size_t)(r + u * st) * C + c0) = pack8(f);
-    }
-  });
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+        }
+        *(uint4*)(y + (size_t)r * C + c0) = pack8(f);
+      });
 }
 
 // ------------------------------------------------------------------- forward (train)
@@ -358,47 +385,42 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const bool zmask = !y && beta;
   float msc[8], msh[8];
   if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
-  sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
-    uint4 dv[UNR], xr[UNR], yr[UNR];
+  const bool need_x = dx || zmask;
+  sweep_rows_pl<UNR, 3>(
+      cm, M,
+      [&](int r, uint4 (&v)[3]) {
+        const size_t off = (size_t)r * C + c0;
+        v[0] = *(const uint4*)(dy + off);
+        if (y) v[2] = *(const uint4*)(y + off);
+        if (need_x) v[1] = *(const uint4*)(x + off);
+      },
+      [&](int r, uint4 (&v)[3]) {
+        const size_t off = (size_t)r * C + c0;
+        float g[8];
+        unpack8(v[0], g);
+        if (y) {
+          float yv[8];
+          unpack8(v[2], yv);
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (u < n) {
-        const size_t off = (size_t)(r + u * st) * C + c0;
-        dv[u] = *(const uint4*)(dy + off);
-        if (y) yr[u] = *(const uint4*)(y + off);
-        if (dx || zmask) xr[u] = *(const uint4*)(x + off);
-      }
-    }
+          for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+          if (gout) *(uint4*)(gout + off) = pack8(g);
+        } else if (zmask) {
+          float xv[8];
+          unpack8(v[1], xv);
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (u >= n) break;
-      const size_t off = (size_t)(r + u * st) * C + c0;
-      float g[8];
-      unpack8(dv[u], g);
-      if (y) {
-        float yv[8];
-        unpack8(yr[u], yv);
+          for (int j = 0; j < 8; ++j) g[j] = bn_relu_live(xv[j], msc[j], msh[j]) ? g[j] : 0.f;
+          if (gout) *(uint4*)(gout + off) = pack8(g);
+        } else if (gout) {
+          *(uint4*)(gout + off) = v[0];
+        }
+        if (dx) {
+          float xv[8];
+          unpack8(v[1], xv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-        if (gout) *(uint4*)(gout + off) = pack8(g);
-      } else if (zmask) {
-        float xv[8];
-        unpack8(xr[u], xv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = bn_relu_live(xv[j], msc[j], msh[j]) ? g[j] : 0.f;
-        if (gout) *(uint4*)(gout + off) = pack8(g);
-      } else if (gout) {
-        *(uint4*)(gout + off) = dv[u];
-      }
-      if (dx) {
-        float xv[8];
-        unpack8(xr[u], xv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
-        *(uint4*)(dx + off) = pack8(xv);
-      }
-    }
-  });
+          for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
+          *(uint4*)(dx + off) = pack8(xv);
+        }
+      });
 }
 
 // g = dy * (y > 0) ; dbias += colsum(g)
@@ -483,34 +505,44 @@ __global__ void relu_kernel(const bf16_t* __restrict__ x, int64_t n8, bf16_t* __
 // Cross-block reduction of per-block partial sums (replaces same-address fp32 atomics,
 // which serialise at the memory-side atomic unit when thousands of blocks target the
 // same 2*C words - MI355X_MICROARCH.md "Global float atomics", contention row).
-// out[w] += sum_s slab[s*W + w]; 64 columns x 4 slab groups per block.  Each thread keeps
-// four independent partial sums so four slab loads are in flight per iteration (the
-// kernels are latency-bound: a few hundred KiB, one dependent add chain per thread).
+// out[w] += sum_s slab[s*W + w]; 64 columns x SG slab-row groups per block.  Each thread
+// keeps eight independent partial sums, so eight slab loads are in flight per iteration:
+// these kernels are latency-bound (a few hundred KiB just written by other XCDs, one add
+// chain per thread), and with 16 row groups a 256-row slab takes two round trips instead
+// of sixteen (slab_stats ~10 us -> ~3 us per BN layer).
+constexpr int SG = 16;  // slab-row groups per block (blockDim = 64 * SG)
 __device__ __forceinline__ float slab_col_sum(const float* __restrict__ slab, size_t rstride,
                                               int s0, int S, int step) {
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int s_ = s0;
-  for (; s_ + 3 * step < S; s_ += 4 * step) {
-    a0 += slab[(size_t)s_ * rstride];
-    a1 += slab[(size_t)(s_ + step) * rstride];
-    a2 += slab[(size_t)(s_ + 2 * step) * rstride];
-    a3 += slab[(size_t)(s_ + 3 * step) * rstride];
+  for (; s_ + 7 * step < S; s_ += 8 * step) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += slab[(size_t)(s_ + u * step) * rstride];
   }
-  for (; s_ < S; s_ += step) a0 += slab[(size_t)s_ * rstride];
-  return (a0 + a1) + (a2 + a3);
+  for (; s_ < S; s_ += step) a[0] += slab[(size_t)s_ * rstride];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int S,
-                                                           int W, float* __restrict__ out) {
-  __shared__ float red[256];
+// fixed-order sum of the SG groups' partials of column (threadIdx.x & 63) held in red[]
+__device__ __forceinline__ float group_sum(const float* red, int t) {
+  float v = 0.f;
+#pragma unroll
+  for (int g = 0; g < SG; ++g) v += red[g * 64 + t];
+  return v;
+}
+
+__global__ __launch_bounds__(64 * SG) void slab_reduce_kernel(const float* __restrict__ slab,
+                                                               int S, int W,
+                                                               float* __restrict__ out) {
+  __shared__ float red[64 * SG];
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   float acc = 0.f;
-  if (w < W) acc = slab_col_sum(slab + w, W, blockIdx.y * 4 + g, S, gridDim.y * 4);
+  if (w < W) acc = slab_col_sum(slab + w, W, blockIdx.y * SG + g, S, gridDim.y * SG);
   red[threadIdx.x] = acc;
   __syncthreads();
   if (g == 0 && w < W) {
-    acc = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    acc = group_sum(red, threadIdx.x);
     if (gridDim.y == 1) out[w] += acc;
     else atomicAdd(out + w, acc);
   }
@@ -520,8 +552,9 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // when the reduction should start from 0; zero_out=true is only a fallback memset)
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s) {
   if (zero_out) (void)hipMemsetAsync(out, 0, sizeof(float) * W, s);
-  const int gy = std::max(1, std::min(32, (S + 63) / 64));
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 63) / 64, gy), dim3(256), 0, s, slab, S, W, out);
+  const int gy = std::max(1, std::min(32, (S + 255) / 256));
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 63) / 64, gy), dim3(64 * SG), 0, s, slab, S, W,
+                     out);
 }
 
 int64_t bn_ws_floats(int M, int C) {
@@ -553,43 +586,41 @@ void stats_finalize(const float* sums, const float* shift, int M, int C, float* 
 // the chunk's first row in place (deterministic, no atomics; every block owns its chunk),
 // then the finalize kernel reads the chunk heads.  Thread (g, c) sums rows g, g+4, ... of
 // columns c and C + c; the 4 groups combine through LDS in a fixed order.
-__global__ __launch_bounds__(256) void slab_fold_kernel(float* __restrict__ slab, int S, int W,
-                                                        int chunk) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(64 * SG) void slab_fold_kernel(float* __restrict__ slab, int S,
+                                                             int W, int chunk) {
+  __shared__ float red[64 * SG];
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   const int r0 = blockIdx.y * chunk;
   const int r1 = min(S, r0 + chunk);
   float acc = 0.f;
-  if (w < W) acc = slab_col_sum(slab + w, W, r0 + g, r1, 4);
+  if (w < W) acc = slab_col_sum(slab + w, W, r0 + g, r1, SG);
   red[threadIdx.x] = acc;
   __syncthreads();
-  if (g == 0 && w < W)
-    slab[(size_t)r0 * W + w] =
-        (red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192]);
+  if (g == 0 && w < W) slab[(size_t)r0 * W + w] = group_sum(red, threadIdx.x);
 }
 
-__global__ __launch_bounds__(256) void slab_stats_kernel(const float* __restrict__ slab, int S,
-                                                         int rstep, int C,
-                                                         const float* __restrict__ shift, int M,
-                                                         float* __restrict__ sums,
-                                                         float* __restrict__ out) {
-  __shared__ float red[2][256];
+__global__ __launch_bounds__(64 * SG) void slab_stats_kernel(const float* __restrict__ slab,
+                                                              int S, int rstep, int C,
+                                                              const float* __restrict__ shift,
+                                                              int M, float* __restrict__ sums,
+                                                              float* __restrict__ out) {
+  __shared__ float red[2][64 * SG];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   const size_t W = 2 * (size_t)C;
   float a = 0.f, b = 0.f;
   if (c < C) {
-    a = slab_col_sum(slab + c, W * rstep, g, S, 4);
-    b = slab_col_sum(slab + C + c, W * rstep, g, S, 4);
+    a = slab_col_sum(slab + c, W * rstep, g, S, SG);
+    b = slab_col_sum(slab + C + c, W * rstep, g, S, SG);
   }
   red[0][threadIdx.x] = a;
   red[1][threadIdx.x] = b;
   __syncthreads();
   if (g == 0 && c < C) {
     const int t = threadIdx.x;
-    a = (red[0][t] + red[0][t + 64]) + (red[0][t + 128] + red[0][t + 192]);
-    b = (red[1][t] + red[1][t + 64]) + (red[1][t + 128] + red[1][t + 192]);
+    a = group_sum(red[0], t);
+    b = group_sum(red[1], t);
     sums[c] = a;
     sums[C + c] = b;
     const float inv = 1.f / (float)M;
@@ -607,11 +638,11 @@ void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sum
     const int chunk = (S + 63) / 64;
     rows = (S + chunk - 1) / chunk;
     rstep = chunk;
-    hipLaunchKernelGGL(slab_fold_kernel, dim3((2 * C + 63) / 64, rows), dim3(256), 0, s, slab, S,
-                       2 * C, chunk);
+    hipLaunchKernelGGL(slab_fold_kernel, dim3((2 * C + 63) / 64, rows), dim3(64 * SG), 0, s, slab,
+                       S, 2 * C, chunk);
   }
-  hipLaunchKernelGGL(slab_stats_kernel, dim3((C + 63) / 64), dim3(256), 0, s, slab, rows, rstep,
-                     C, shift, M, sums, out);
+  hipLaunchKernelGGL(slab_stats_kernel, dim3((C + 63) / 64), dim3(64 * SG), 0, s, slab, rows,
+                     rstep, C, shift, M, sums, out);
 }
 
 // ----------------------------------------------- BN + ReLU + max-pool (network stems)
@@ -664,6 +695,16 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     }
   }
   const int MP = g.N * g.P * g.Q;
+  // pooled output r -> (n, p, q), writes of (best, argmax, z at argmax)
+  auto emit = [&](int r, const float* best, const int* bi, const float* bz) {
+    const size_t o = (size_t)r * C + c0;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 ib;
+    ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(uint2*)(idx + o) = ib;
+    if (zsel) *(uint4*)(zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
+  };
   for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
     const int q = r % g.Q;
     const int t = r / g.Q;
@@ -675,7 +716,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; bz[j] = 0.f; }
     if constexpr (K3S2) {
       // 3x3 / stride 2 / pad 1: all nine loads issued before any is consumed (out-of-range
-      // taps read a clamped in-range pixel and are masked)
+      // taps read a clamped in-range pixel and are masked).  (Prefetching the next
+      // output's nine loads ahead of this output's stores measured slower: 300 -> 384 us.)
       const int h0 = 2 * p - 1, w0 = 2 * q - 1;
       uint4 v9[9];
 #pragma unroll
@@ -716,13 +758,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
         }
       }
     }
-    const size_t o = (size_t)r * C + c0;
-    *(uint4*)(y + o) = pack8(best);
-    uint2 ib;
-    ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
-    ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
-    *(uint2*)(idx + o) = ib;
-    if (zsel) *(uint4*)(zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
+    emit(r, best, bi, bz);
   }
 }
 
@@ -932,39 +968,47 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
       for (int j = 0; j < 8; ++j) { zsums[c0 + j] = 0.f; zsums[C + c0 + j] = 0.f; }
     }
     const int cells = g.N * g.P * g.Q;
-#pragma unroll 1
-    for (int r = blockIdx.x * cm.rpi + cm.r0; r < cells; r += gridDim.x * cm.rpi) {
-      const int q = r % g.Q;
-      const int t = r / g.Q;
-      const int p = t % g.P;
-      const int n = t / g.P;
+    // pooled neighbours (dp, idx): [0]=(p,q) [1]=(p,q+1) [2]=(p+1,q) [3]=(p+1,q+1); out-of-
+    // range neighbours load (p,q) and are masked in proc.  Register image per cell: dp 0..3,
+    // idx pairs 4..5, z 6..9.  The next cell's loads are issued before this cell's dz stores
+    // (sweep_rows_pl: a load after a store would wait for the store in the in-order vmcnt).
+    auto load = [&](int r, uint4 (&v)[10]) {
+      const int q = r % g.Q, t = r / g.Q, p = t % g.P, n = t / g.P;
       const bool pn = p + 1 < g.P, qn = q + 1 < g.Q;
-      // pooled neighbours (dp, idx): [0]=(p,q) [1]=(p,q+1) [2]=(p+1,q) [3]=(p+1,q+1)
-      uint4 dv[4];
       uint2 iv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int pp = p + (u >> 1), qq = q + (u & 1);
         const bool ok = (!(u >> 1) || pn) && (!(u & 1) || qn);
         const size_t o = (((size_t)n * g.P + (ok ? pp : p)) * g.Q + (ok ? qq : q)) * C + c0;
-        dv[u] = *(const uint4*)(dp + o);
+        v[u] = *(const uint4*)(dp + o);
         iv[u] = *(const uint2*)(idx + o);
-        if (!ok) { dv[u] = make_uint4(0, 0, 0, 0); iv[u] = make_uint2(~0u, ~0u); }
       }
-      uint4 zv[4];
+      v[4] = make_uint4(iv[0].x, iv[0].y, iv[1].x, iv[1].y);
+      v[5] = make_uint4(iv[2].x, iv[2].y, iv[3].x, iv[3].y);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int h = 2 * p + (v >> 1), w = 2 * q + (v & 1);
-        zv[v] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const int h = 2 * p + (w4 >> 1), w = 2 * q + (w4 & 1);
+        v[6 + w4] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
       }
+    };
+    auto proc = [&](int r, uint4 (&v)[10]) {
+      const int q = r % g.Q, t = r / g.Q, p = t % g.P, n = t / g.P;
+      const bool pn = p + 1 < g.P, qn = q + 1 < g.Q;
+      uint2 iv[4] = {make_uint2(v[4].x, v[4].y), make_uint2(v[4].z, v[4].w),
+                     make_uint2(v[5].x, v[5].y), make_uint2(v[5].z, v[5].w)};
       float d[4][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) unpack8(dv[u], d[u]);
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = (!(u >> 1) || pn) && (!(u & 1) || qn);
+        if (!ok) iv[u] = make_uint2(~0u, ~0u);  // argmax 255 never matches a tap
+        unpack8(v[u], d[u]);
+      }
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int a0 = v >> 1, b0 = v & 1;  // input pixel (2p+a0, 2q+b0)
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const int a0 = w4 >> 1, b0 = w4 & 1;  // input pixel (2p+a0, 2q+b0)
         float zr[8], gr[8];
-        unpack8(zv[v], zr);
+        unpack8(v[6 + w4], zr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float acc = 0.f;
@@ -992,7 +1036,8 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
           }
         }
       }
-    }
+    };
+    sweep_rows_pl<1, 10>(cm, cells, load, proc);
   }
   if constexpr (!APPLY) {
     block_reduce8(sg, cm, red);

@@ -42,53 +42,145 @@ __device__ __forceinline__ void store_px(bf16_t* o, float c0, float c1, float c2
 
 // Output geometry: the resized image sits at (pad.top, pad.left) of a zero-bordered
 // [OH + top + bottom][OW + left + right] canvas (the pre-padded input of a pixel-pair
-// stem conv, models/layers.py); a thread per canvas pixel, border pixels write zeros.
-__device__ __forceinline__ bool canvas_px(int64_t t, const OutPad& pd, int OH, int OW, int& b,
-                                          int& oy, int& ox) {
-  const int owp = OW + pd.left + pd.right, ohp = OH + pd.top + pd.bottom;
-  const int px = (int)(t % owp);
-  const int64_t r = t / owp;
-  const int py = (int)(r % ohp);
-  b = (int)(r / ohp);
-  oy = py - pd.top;
-  ox = px - pd.left;
-  return (unsigned)oy < (unsigned)OH && (unsigned)ox < (unsigned)OW;
-}
+// stem conv, models/layers.py); border pixels are written as zeros.
+//
+// Bilinear (the training path, one launch per batch): a block owns PP_ROWS canvas rows of
+// one image (a work item; blocks stride over the items).  Phase 1 stages the two source
+// rows of every one of those rows' bilinear taps into LDS with independent 16-B (or dword,
+// or byte) loads - one memory round trip per block; phase 2 has lane i compute canvas
+// pixel i of each row from LDS and store 8 B (pixel-pair layout) or 16 B, consecutive
+// lanes -> consecutive pixels.  (A pixel-per-thread grid-stride version with 64-bit index
+// math and byte gathers from global memory streamed ~1.5 TB/s; a row-at-a-time LDS
+// version was round-trip bound.)  The taps are LDS reads on purpose: a global (or flat)
+// load after the previous pixel's store makes the in-order vmcnt wait for that store too,
+// so every pixel paid a full store round trip.  Source rows wider than PP_MAXW pixels
+// (STAGED = false) read their taps from global memory.
+constexpr int PP_ROWS = 8;
+constexpr int PP_MAXW = 1344;  // 2 x 8 staged rows x 1344 px x 3 B = 63 KiB of LDS
 
+// VEC: staging load width (16, 4 or 1 bytes; alignment of the source rows); CPAD: 4 or 8
+// output channels with one 8-B / 16-B store per pixel, 0 = any (scalar stores)
+template <bool STAGED, int VEC, int CPAD>
 __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
     const uint8_t* __restrict__ img, int B, int H, int W, int OH, int OW,
-    Norm3 nrm, int cpad, OutPad pd, bf16_t* __restrict__ out) {
+    Norm3 nrm, int cpad_rt, OutPad pd, bf16_t* __restrict__ out) {
+  const int cpad = CPAD ? CPAD : cpad_rt;
+  extern __shared__ __attribute__((aligned(16))) uint8_t srow[];  // [PP_ROWS][2][rb]
   const float* mean = nrm.mean;
   const float* stdv = nrm.std;
-  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
-  const float sh = (float)H / OH, sw = (float)W / OW;
-  const float m0 = mean[0], m1 = mean[1], m2 = mean[2];
   const float i0 = 1.f / (255.f * stdv[0]), i1 = 1.f / (255.f * stdv[1]), i2 = 1.f / (255.f * stdv[2]);
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    int b, oy, ox;
-    if (!canvas_px(t, pd, OH, OW, b, oy, ox)) {
-      store_px(out + t * cpad, 0.f, 0.f, 0.f, cpad);
-      continue;
-    }
-    float sy = fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
-    float sx = fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
-    int y0 = min((int)sy, H - 1), x0 = min((int)sx, W - 1);
-    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
-    const float ly = sy - y0, lx = sx - x0;
+  const float o0 = mean[0] / stdv[0], o1 = mean[1] / stdv[1], o2 = mean[2] / stdv[2];
+  const int ohp = OH + pd.top + pd.bottom, owp = OW + pd.left + pd.right;
+  const int ngroups = (ohp + PP_ROWS - 1) / PP_ROWS;  // row groups per image
+  const float sh = (float)H / OH, sw = (float)W / OW;
+  const int rb = W * 3;                     // source row bytes
+  const int rbp = (rb + 15) & ~15;          // staged row pitch
+  constexpr int vec = VEC;
+  const int per = rb / vec;  // vectors per source row
+  // work items (image, row group), strided over a grid of at most ~2k blocks: per-wave
+  // start-up (kernel arguments, the normalisation divides) is paid once per block
+  for (int item = blockIdx.x; item < B * ngroups; item += gridDim.x) {
+    const int b = item / ngroups;
+    const int row0 = (item - b * ngroups) * PP_ROWS;
+    const int nrows = min(PP_ROWS, ohp - row0);
     const uint8_t* base = img + (size_t)b * H * W * 3;
-    float c[3];
+    auto tap_rows = [&](int r, int& y0, int& y1, float& ly) {
+      const int oy = row0 + r - pd.top;
+      const float sy = fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
+      y0 = min((int)sy, H - 1);
+      y1 = min(y0 + 1, H - 1);
+      ly = sy - y0;
+    };
+    if constexpr (STAGED) {  // phase 1: every (row, tap) source row; 4 loads in flight per
+                             // thread before any LDS write (one round trip per batch)
+      __syncthreads();       // the previous item's readers are done with srow
+      const int total = nrows * 2 * per;
+      for (int j0 = threadIdx.x; j0 < total; j0 += 4 * blockDim.x) {
+        uint4 v[4];
+        int dsto[4];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      const float v00 = base[((size_t)y0 * W + x0) * 3 + ch];
-      const float v01 = base[((size_t)y0 * W + x1) * 3 + ch];
-      const float v10 = base[((size_t)y1 * W + x0) * 3 + ch];
-      const float v11 = base[((size_t)y1 * W + x1) * 3 + ch];
-      c[ch] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+        for (int k = 0; k < 4; ++k) {
+          const int i = j0 + k * blockDim.x;
+          dsto[k] = -1;
+          if (i >= total) continue;
+          const int rt = i / per, e = i - rt * per;  // rt = 2 * row + tap
+          const int oy = row0 + (rt >> 1) - pd.top;
+          if ((unsigned)oy >= (unsigned)OH) continue;  // border row: nothing to stage
+          int y0, y1;
+          float ly;
+          tap_rows(rt >> 1, y0, y1, ly);
+          const uint8_t* src = base + (size_t)((rt & 1) ? y1 : y0) * rb;
+          dsto[k] = rt * rbp + e * vec;
+          if constexpr (vec == 16) v[k] = ((const uint4*)src)[e];
+          else if constexpr (vec == 4) v[k].x = ((const uint32_t*)src)[e];
+          else v[k].x = src[e];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (dsto[k] < 0) continue;
+          if constexpr (vec == 16) *(uint4*)(srow + dsto[k]) = v[k];
+          else if constexpr (vec == 4) *(uint32_t*)(srow + dsto[k]) = v[k].x;
+          else srow[dsto[k]] = (uint8_t)v[k].x;
+        }
+      }
+      __syncthreads();
     }
-    store_px(out + t * cpad, c[0] * i0 - m0 / stdv[0], c[1] * i1 - m1 / stdv[1],
-             c[2] * i2 - m2 / stdv[2], cpad);
+    for (int r = 0; r < nrows; ++r) {  // phase 2
+      const int oy = row0 + r - pd.top;
+      bf16_t* orow = out + ((size_t)b * ohp + row0 + r) * owp * cpad;
+      const bool brow = (unsigned)oy >= (unsigned)OH;
+      int y0, y1;
+      float ly;
+      tap_rows(r, y0, y1, ly);
+      const uint8_t* t0;
+      const uint8_t* t1;
+      if constexpr (STAGED) {
+        t0 = srow + (2 * r) * rbp;
+        t1 = srow + (2 * r + 1) * rbp;
+      } else {
+        t0 = base + (size_t)y0 * rb;
+        t1 = base + (size_t)y1 * rb;
+      }
+      for (int px = threadIdx.x; px < owp; px += blockDim.x) {
+        const int ox = px - pd.left;
+        bf16_t* o = orow + (size_t)px * cpad;
+        if (brow || (unsigned)ox >= (unsigned)OW) {
+          store_px(o, 0.f, 0.f, 0.f, cpad);
+          continue;
+        }
+        const float sx = fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
+        const int x0 = min((int)sx, W - 1), x1 = min(x0 + 1, W - 1);
+        const float lx = sx - x0;
+        float c[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const float v00 = t0[x0 * 3 + ch], v01 = t0[x1 * 3 + ch];
+          const float v10 = t1[x0 * 3 + ch], v11 = t1[x1 * 3 + ch];
+          c[ch] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+        }
+        store_px(o, c[0] * i0 - o0, c[1] * i1 - o1, c[2] * i2 - o2, cpad);
+      }
+    }
   }
+}
+
+// Bicubic-AA (eval path): one block per canvas row (blockIdx.x = row, blockIdx.y =
+// image); the per-pixel filter windows dominate, not the indexing.
+struct CanvasRow {
+  int owp, oy;     // canvas row width; resized-image row (outside [0, OH): border row)
+  bool border;
+  bf16_t* out;     // first pixel of this canvas row
+};
+
+__device__ __forceinline__ CanvasRow canvas_row(const OutPad& pd, int OH, int OW, int cpad,
+                                                bf16_t* out) {
+  CanvasRow r;
+  const int ohp = OH + pd.top + pd.bottom;
+  r.owp = OW + pd.left + pd.right;
+  r.oy = (int)blockIdx.x - pd.top;
+  r.border = (unsigned)r.oy >= (unsigned)OH;
+  r.out = out + (((size_t)blockIdx.y * ohp + blockIdx.x) * r.owp) * cpad;
+  return r;
 }
 
 // antialiased bicubic: separable weights computed on the fly (support scales with the
@@ -106,14 +198,15 @@ __device__ __forceinline__ void aa_window(int i, int in, int out, int& xmin, int
 __global__ __launch_bounds__(256) void preprocess_bicubic_aa_kernel(
     const uint8_t* __restrict__ img, int B, int H, int W, int OH, int OW,
     Norm3 nrm, int cpad, OutPad pd, bf16_t* __restrict__ out) {
+  const CanvasRow cr = canvas_row(pd, OH, OW, cpad, out);
   const float* mean = nrm.mean;
   const float* stdv = nrm.std;
-  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    int b, oy, ox;
-    if (!canvas_px(t, pd, OH, OW, b, oy, ox)) {
-      store_px(out + t * cpad, 0.f, 0.f, 0.f, cpad);
+  const int oy = cr.oy;
+  for (int px = threadIdx.x; px < cr.owp; px += blockDim.x) {
+    const int ox = px - pd.left;
+    bf16_t* o = cr.out + (size_t)px * cpad;
+    if (cr.border || (unsigned)ox >= (unsigned)OW) {
+      store_px(o, 0.f, 0.f, 0.f, cpad);
       continue;
     }
     int ymin, ysize, xmin, xsize;
@@ -124,7 +217,7 @@ __global__ __launch_bounds__(256) void preprocess_bicubic_aa_kernel(
     for (int j = 0; j < ysize; ++j) wsy += cubic_w((j + ymin - cy + 0.5f) * isy);
     for (int j = 0; j < xsize; ++j) wsx += cubic_w((j + xmin - cx + 0.5f) * isx);
     const float ny = wsy != 0.f ? 1.f / wsy : 0.f, nx = wsx != 0.f ? 1.f / wsx : 0.f;
-    const uint8_t* base = img + (size_t)b * H * W * 3;
+    const uint8_t* base = img + (size_t)blockIdx.y * H * W * 3;
     float acc[3] = {0.f, 0.f, 0.f};
     for (int j = 0; j < ysize; ++j) {
       const float wy = cubic_w((j + ymin - cy + 0.5f) * isy) * ny;
@@ -141,7 +234,7 @@ __global__ __launch_bounds__(256) void preprocess_bicubic_aa_kernel(
       acc[1] += wy * row[1];
       acc[2] += wy * row[2];
     }
-    store_px(out + t * cpad, (acc[0] / 255.f - mean[0]) / stdv[0],
+    store_px(o, (acc[0] / 255.f - mean[0]) / stdv[0],
              (acc[1] / 255.f - mean[1]) / stdv[1], (acc[2] / 255.f - mean[2]) / stdv[2], cpad);
   }
 }
@@ -183,13 +276,35 @@ static int blocks_n(int64_t n) {
 
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
                 int cpad, OutPad pd, bf16_raw* out, hipStream_t s) {
-  const int64_t total = (int64_t)B * (OH + pd.top + pd.bottom) * (OW + pd.left + pd.right);
-  if (mode == 0)
-    hipLaunchKernelGGL(preprocess_bilinear_kernel, dim3(blocks_n(total)), dim3(256), 0, s, img, B,
-                       H, W, OH, OW, nrm, cpad, pd, out);
-  else
-    hipLaunchKernelGGL(preprocess_bicubic_aa_kernel, dim3(blocks_n(total)), dim3(256), 0, s, img,
-                       B, H, W, OH, OW, nrm, cpad, pd, out);
+  if (B <= 0) return;  // bicubic: gridDim.y = images (<= 65535)
+  const int ohp = OH + pd.top + pd.bottom, owp = OW + pd.left + pd.right;
+  if (mode == 0) {
+    const int items = B * ((ohp + PP_ROWS - 1) / PP_ROWS);
+    const dim3 grid(std::min(items, 2048));
+    const size_t lds = (size_t)PP_ROWS * 2 * ((W * 3 + 15) & ~15);
+    const int rb = W * 3;
+    const uintptr_t ia = (uintptr_t)img;
+    const int vec = (rb % 16 == 0 && ia % 16 == 0) ? 16 : (rb % 4 == 0 && ia % 4 == 0) ? 4 : 1;
+#define PP_LAUNCH(ST, V, CP, L)                                                                 \
+  hipLaunchKernelGGL((preprocess_bilinear_kernel<ST, V, CP>), grid, dim3(256), L, s, img, B, H, \
+                     W, OH, OW, nrm, cpad, pd, out)
+#define PP_CPAD(ST, V, L)                                      \
+  do {                                                         \
+    if (cpad == 4) PP_LAUNCH(ST, V, 4, L);                     \
+    else if (cpad == 8) PP_LAUNCH(ST, V, 8, L);                \
+    else PP_LAUNCH(ST, V, 0, L);                               \
+  } while (0)
+    if (W > PP_MAXW) PP_CPAD(false, 1, 0);
+    else if (vec == 16) PP_CPAD(true, 16, lds);
+    else if (vec == 4) PP_CPAD(true, 4, lds);
+    else PP_CPAD(true, 1, lds);
+#undef PP_CPAD
+#undef PP_LAUNCH
+  } else {
+    const dim3 block(owp >= 256 ? 256 : std::max(64, (owp + 63) / 64 * 64));
+    hipLaunchKernelGGL(preprocess_bicubic_aa_kernel, dim3(ohp, B), block, 0, s, img, B, H, W, OH,
+                       OW, nrm, cpad, pd, out);
+  }
 }
 
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,

@@ -726,7 +726,9 @@ def test_adam_sgd(gpu):
 
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("src,dst", [((64, 80), (32, 32)), ((224, 224), (224, 224)),
-                                     ((100, 60), (128, 128))])
+                                     ((100, 60), (128, 128)),
+                                     ((30, 61), (20, 40)),      # 3W % 4 != 0: byte staging
+                                     ((12, 1400), (8, 16))])    # W > 1344: unstaged taps
 def test_preprocess(gpu, mode, src, dst):
     img = torch.randint(0, 256, (2, src[0], src[1], 3), dtype=torch.uint8, device=gpu)
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
