@@ -112,6 +112,11 @@ int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
 // halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z
+// halo-staged pixel-pair stem weight gradient (conv_stem.hip): partials into a.slab
+// ([Z][64][224], <= stem_wgrad_ws_floats()); returns Z
+bool stem_wgrad_ok(const WGradArgs& a);
+int stem_wgrad(WGradArgs a, hipStream_t s);
+int64_t stem_wgrad_ws_floats();
 bool conv3_halo_wgrad_ok(const WGradArgs& a);
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);

@@ -63,47 +63,6 @@ struct HaloPlan {
   int dbg;              // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
 };
 
-__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t mag) { return __umulhi(n, mag); }
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-
-__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                           voff, 0, 0, 0);
-}
-
-// The same DMA as inline asm: the compiler does not see an LDS write, so it inserts no
-// vmcnt(0) before the following ds_read_b64_tr_b16 (whose intrinsic it cannot prove
-// disjoint from the DMA target - with the builtin, every DMA issued between transposed
-// reads was followed by a full wait).  Safe for the compiler's own vmcnt accounting: it
-// only undercounts outstanding ops, so its waits get stronger, never weaker; the kernel
-// waits for these DMAs itself (wait_all_barrier) before reading their stage.
-__device__ __forceinline__ void buf_lds16_asm(__amdgpu_buffer_rsrc_t r, const char* lds,
-                                              uint32_t voff) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :
-               : "s"(m0), "v"(voff), "s"(r)
-               : "memory", "m0");
-}
-
-template <int N>
-__device__ __forceinline__ void halo_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// all of this wave's VMEM (LDS-DMAs, loads, stores) done, then the workgroup barrier; as a
-// builtin s_waitcnt (vmcnt 0, lgkmcnt 0) the compiler's wait insertion knows the loads are
-// complete, so it adds no vmcnt(0) later that would also wait for DMAs issued afterwards
-__device__ __forceinline__ void wait_all_barrier() {
-  __builtin_amdgcn_s_waitcnt(0x0070);
-  __builtin_amdgcn_s_barrier();
-}
-
 __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
   return __builtin_bit_cast(bf16x8, *LDS_PTR(const u32x4, lds_byte));
 }

@@ -242,4 +242,202 @@ int conv_stem(IGemmArgs a, hipStream_t s) {
   return launch_stem<8, 8, 1>(a, HALO_MAX_ROWS, s);
 }
 
+// ======================================================================================
+//  Stem weight gradient, halo-staged (pixel-pair layout of the forward above):
+//    dW[k][r][s][c] += sum_pix dz[pix][k] * canvas[n][2 oh + r][ow + s][c]
+//  k < 64 output channels; (r < 7, s < 4 pair columns, c < 8) = 224 columns; the reduction
+//  runs over every output pixel (6.4 M at batch 512).  As an implicit GEMM (igemm_wgrad_dma_
+//  inc_kernel) every 16-B canvas vector was gathered once per (r, s) tap it feeds - 14x -
+//  and the kernel waited on those gathers 57 % of its wave time.  Here a block owns the
+//  whole 64 x 224 output and streams items of 2 output rows of one image:
+//    * the item's dz rows (2 Q pixels x 128 B, contiguous) and its 9 canvas rows (contiguous:
+//      the 7 x 4 windows of every output pixel of the item) are staged ONCE per item,
+//      register-staged: the next item's 16-B loads are issued at the top of the current
+//      item and written to the other LDS stage after its MFMAs (LDS-DMA pieces cost the
+//      issuing wave 60-180 cycles each; as DMAs the 45 per item were 37 % of the kernel);
+//    * both operands are pixel-major and read with ds_read_b64_tr_b16: dz through the
+//      engine's mn_off<64> image, the canvas straight from its rows - a lane's 8-B granule
+//      of column fragment j (tap row r = j/2, pair columns 2 (j%2) + {0,1}) for pixel
+//      (row, ow) sits at ((2 row + r) Wc + ow + s) * 16 + 8 * (channel half): a per-lane
+//      base plus a wave-uniform tap offset;
+//    * the KS K-steps of an item are unrolled at compile time and software-pipelined (the
+//      next K-step's fragments are read under this one's MFMAs);
+//    * wave w accumulates all 64 k x column fragments {w, w+4, w+8, w+12} (< 14) in
+//      registers for the block's whole life; one [64][224] fp32 partial per block goes to
+//      the slab that wgrad_reduce adds into the gradient arena.
+// ======================================================================================
+namespace {
+constexpr int SW_KS = 8;                             // <= 8 K-steps: 2 Q <= 256 pixels
+constexpr int SW_DZ = SW_KS * 4096;                  // [K-step][32 px][64 k] bf16, mn_off<64>
+constexpr int SW_CROWS = 9;                          // canvas rows per item: 2 (2-1) + 7
+constexpr int SW_CVV = SW_CROWS * STEM_MAX_WP;       // canvas 16-B vectors per item (<= 1080)
+constexpr int SW_CVPT = (SW_CVV + 255) / 256;        // canvas vectors per thread (5)
+constexpr int SW_STAGE = SW_DZ + SW_CVV * 16;
+constexpr int SW_LDS = 2 * SW_STAGE;                 // 100,096 B
+}  // namespace
+
+struct StemWPlan {
+  int items, items_img;  // items = N * ceil(P / 2)
+  int ks;                // K-steps per item: ceil(2 Q / 32) (= the kernel's KS)
+};
+
+template <int KS>
+__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h) {
+  __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W;
+  const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
+  const int nfr = wave < 2 ? 4 : 3;  // column fragments j = wave + 4 i < 14
+
+  // per-lane canvas byte offsets of the B granules (item independent): K-step ks, half e
+  // -> item pixel pl = 32 ks + 8 g + qd + 4 e -> (row, ow); pixels past 2 Q are clamped
+  // (their dz rows are zero)
+  int bb[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pl = min(32 * ks + 8 * g + qd + 4 * e, 2 * Q - 1);
+      const int prow = pl >= Q ? 1 : 0;
+      const int ow = pl - prow * Q;
+      bb[ks][e] = ((2 * prow) * Wc + ow + (pp >> 1)) * 16 + (pp & 1) * 8;
+    }
+  // this thread's staging slots: dz vector tid + 256 i (row = v >> 3, chunk = v & 7) and
+  // canvas vector tid + 256 i
+  int dzoff[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    const int v = tid + 256 * i, row = v >> 3, chunk = v & 7;
+    dzoff[i] = (row >> 5) * 4096 + mn_off<64>(row & 31, chunk * 8);
+  }
+  const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors]
+  const u32x4* const cvsrc = (const u32x4*)p.x;    // [n][Hc][Wc] pair vectors
+  u32x4 pdz[KS], pcv[SW_CVPT];
+  auto fetch = [&](int it) {  // item it's vectors into registers (zeros past its end)
+    const int n = it / h.items_img, oh0 = (it - n * h.items_img) * 2;
+    const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
+    const size_t cv0 = ((size_t)n * Hc + 2 * oh0) * Wc;
+    const int cvlim = min(SW_CROWS, Hc - 2 * oh0) * Wc;
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const int v = tid + 256 * i;
+      pdz[i] = (v >> 3) < nval ? dzsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
+                               : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < SW_CVPT; ++i) {
+      const int v = tid + 256 * i;
+      pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto commit = [&](int stage) {
+    char* st = smem + stage * SW_STAGE;
+#pragma unroll
+    for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
+#pragma unroll
+    for (int i = 0; i < SW_CVPT; ++i) {
+      const int v = tid + 256 * i;
+      if (v < SW_CVV) *LDS_PTR(u32x4, st + SW_DZ + v * 16) = pcv[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int km = 0; km < 4; ++km)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[km][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragments of K-step ks from stage st
+  auto load_frags = [&](const char* sdz, const char* scv, int ks, bf16x8 (&af)[4],
+                        bf16x8 (&bf)[4]) {
+#pragma unroll
+    for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sdz + ks * 4096, 16 * km, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = min(wave + 4 * i, 13);  // (i >= nfr: a duplicate read, never used)
+      const int toff = ((j >> 1) * Wc + 2 * (j & 1)) * 16;  // tap row r, pair column s0
+      const s16x4 lo =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][0] + toff));
+      const s16x4 hi =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][1] + toff));
+      s16x8 r;
+      r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+      r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+      bf[i] = __builtin_bit_cast(bf16x8, r);
+    }
+  };
+
+  const int G = gridDim.x;
+  int it = blockIdx.x;
+  if (it < h.items) {
+    fetch(it);
+    commit(0);
+  }
+  for (int k = 0; it < h.items; ++k, it += G) {
+    const int st = k & 1;
+    __syncthreads();  // item k's stage written; every wave is done with item k-1's stage
+    const bool more = it + G < h.items;
+    if (more) fetch(it + G);  // lands under this item's MFMAs
+    const char* sdz = smem + st * SW_STAGE;
+    const char* scv = sdz + SW_DZ;
+    bf16x8 af[2][4], bf[2][4];
+    load_frags(sdz, scv, 0, af[0], bf[0]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) load_frags(sdz, scv, ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+      // waves 2 and 3 own three fragments; their fourth (a duplicate of fragment 13) keeps
+      // the MFMA stream branch-free - those waves would idle at the item barrier anyway -
+      // and is never stored
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int km = 0; km < 4; ++km)
+          acc[km][i] = mfma16(bf[ks & 1][i], af[ks & 1][km], acc[km][i]);
+    }
+    if (more) commit(st ^ 1);
+  }
+  // partial of this block -> slab row blockIdx.x: dw[k][col], k = 16 km + lane % 16,
+  // col = 16 j + 4 (lane / 16) .. +3
+  float* dst = p.slab + (size_t)blockIdx.x * 64 * 224;
+#pragma unroll
+  for (int km = 0; km < 4; ++km)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nfr) break;
+      const int j = wave + 4 * i;
+      *(f32x4*)(dst + (16 * km + li) * 224 + 16 * j + 4 * g) = acc[km][i];
+    }
+}
+
+bool stem_wgrad_ok(const WGradArgs& a) {
+  if (!g_stem_on || a.R != STEM_R || a.S != 4 || a.C != 8 || a.sh != 2 || a.sw != 1 || a.ph != 0 ||
+      a.pw != 0 || a.Kout != 64 || a.Ncols != 224 || a.slab == nullptr)
+    return false;
+  if (a.P != (a.H - STEM_R) / 2 + 1 || a.Q != a.W - 3 || a.Q < 16 || 2 * a.Q > 32 * SW_KS ||
+      a.W > STEM_MAX_WP || a.Mpix % (a.P * a.Q) != 0)
+    return false;
+  return ((reinterpret_cast<uintptr_t>(a.dy) | reinterpret_cast<uintptr_t>(a.x) |
+           reinterpret_cast<uintptr_t>(a.slab)) & 15) == 0;
+}
+
+int64_t stem_wgrad_ws_floats() { return (int64_t)HALO_MAX_ROWS * 64 * 224; }
+
+// partials into a.slab ([Z][64][224]); returns Z
+int stem_wgrad(WGradArgs a, hipStream_t s) {
+  StemWPlan h{};
+  const int nimg = a.Mpix / (a.P * a.Q);
+  h.items_img = (a.P + 1) / 2;
+  h.items = nimg * h.items_img;
+  h.ks = (2 * a.Q + 31) / 32;
+  const int grid = std::max(1, std::min(h.items, HALO_MAX_ROWS));
+  switch (h.ks) {
+#define SW_CASE(K) \
+  case K: hipLaunchKernelGGL(stem_wgrad_kernel<K>, dim3(grid), dim3(256), 0, s, a, h); break;
+    SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
+#undef SW_CASE
+  }
+  return grid;
+}
+
 }  // namespace mpa

@@ -855,6 +855,7 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
 
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
   int64_t best = conv3_halo_wgrad_ws_floats(Kout, Ncols);
+  if (Kout == 64 && Ncols == 224) best = std::max(best, stem_wgrad_ws_floats());
   for (int dma = 0; dma < 3; ++dma) {  // register, DMA, DMA big tile
     WGradArgs a{};
     a.Kout = Kout; a.Ncols = Ncols; a.Mpix = Mpix;
@@ -870,6 +871,13 @@ void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   if (igemm_engine() >= 1 && conv3_halo_wgrad_ok(a)) {  // 3x3 / stride 1: halo-staged
     const int z = conv3_halo_wgrad(a, s);
     const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 64 == 0: float4 rows
+    const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw);
+    return;
+  }
+  if (igemm_engine() >= 1 && stem_wgrad_ok(a)) {  // pixel-pair 7x7 stem: halo-staged
+    const int z = stem_wgrad(a, s);
+    const int64_t n = (int64_t)a.Kout * a.Ncols;
     const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw);
     return;
