@@ -30,6 +30,32 @@ sys.path.insert(0, ROOT)
 BASELINE_IMG_S = 8.06  # reference FLOP-equivalent img/s at 224^2 (best, 4 ranks)
 
 
+def _emulate_comm(model, step, spec, dev):
+    """bench.py --emulate-comm: see the flag's help."""
+    from mpi_pytorch_amd.ops import _ext
+    parts = [float(v) for v in spec.split(":")]
+    blocks, us = int(parts[0]), parts[1]
+    lds = int(parts[2]) if len(parts) > 2 else 37664  # RCCL generic kernel's static LDS
+    side = torch.cuda.Stream(device=dev)
+    sink = torch.zeros(max(blocks, 1), device=dev)
+    head = model.fc.weight if hasattr(model, "fc") else None
+
+    def on_grad(p):
+        if p is head:
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                _ext.ext().comm_emulator(blocks, 512, lds, us, sink)
+
+    model._mpa_arena.add_listener(on_grad)
+    fin = step.bucketer.finish
+
+    def finish():
+        fin()
+        torch.cuda.current_stream(dev).wait_stream(side)
+
+    step.bucketer.finish = finish
+
+
 def main(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -49,6 +75,11 @@ def main(argv=None):
     p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")
     p.add_argument("--static-data", action="store_true",
                    help="debug: reuse one device batch (no data pipeline in the loop)")
+    p.add_argument("--emulate-comm", default="",
+                   help="diagnostics, BLOCKS:US[:LDS]: when the classifier gradient lands, occupy "
+                        "BLOCKS CUs for US microseconds on a side stream (a stand-in for the "
+                        "data-parallel all-reduce overlapping backward); the optimizer waits "
+                        "for it like for the real collective")
     args = p.parse_args(argv)
 
     from mpi_pytorch_amd.parallel import init_world, barrier, get_world
@@ -74,6 +105,8 @@ def main(argv=None):
     if args.static_data:
         xs, ys = data.next()
         data.next = lambda: (xs, ys)
+    if args.emulate_comm:
+        _emulate_comm(model, step, args.emulate_comm, dev)
     # eager by default: the step is GPU-bound (host runs ahead), graph replay buys nothing
     # measurable and needs a per-step sync for correctness (engine/step.py)
     use_graph = args.graph == "on"

@@ -599,6 +599,15 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
   mpa::igemm_wgrad(a, vec_width(Cout), (Cin % 8 == 0) ? 8 : 1, cur_stream());
 }
 
+void comm_emulator(int64_t blocks, int64_t threads, int64_t lds_bytes, double us, Tensor sink) {
+  CHECK_CUDA(sink);
+  CHECK_F32(sink);
+  TORCH_CHECK(sink.numel() >= blocks && threads <= 512 && lds_bytes <= 160 * 1024,
+              "comm_emulator: args");
+  const c10::OptionalDeviceGuard g(device_of(sink));
+  mpa::comm_emulator(blocks, threads, lds_bytes, us, sink.data_ptr<float>(), cur_stream());
+}
+
 // ------------------------------------------------------------------------ loss / acc
 // logits: [B][NC] bf16 with unit column stride; rows may be padded (stride(0) >= NC, a
 // view of a classifier's padded output)
@@ -812,6 +821,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none());
   m.def("relu_fwd", &relu_fwd);
+  m.def("comm_emulator", &comm_emulator, "diagnostics: occupy CUs like a concurrent collective");
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, py::arg("z"), py::arg("stats"),

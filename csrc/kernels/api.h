@@ -238,4 +238,7 @@ void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t 
 void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,
                  hipStream_t s);
 
+// diag.hip: stand-in for a concurrent RCCL collective (bench.py --emulate-comm)
+void comm_emulator(int blocks, int threads, int lds_bytes, double us, float* sink, hipStream_t s);
+
 }  // namespace mpa

@@ -1,0 +1,35 @@
+// Diagnostics kernels (not on any training path).
+//
+// comm_emulator: stands in for an RCCL collective that shares the GPU with the backward
+// pass.  RCCL's generic kernel (librccl gfx950 code object metadata: 37,664 B of LDS, up to
+// 512 threads, 248-256 VGPRs per wave) occupies `blocks` CUs for the duration of a
+// collective; the persistent conv kernels (146-150 KB of LDS per block) cannot share a CU
+// with it.  bench.py --emulate-comm launches this on a side stream when the classifier's
+// gradient lands - the moment the data-parallel bucketer starts its first all-reduce - so
+// the single-GPU step shows what overlapping comm costs the compute kernels.
+#include "common.h"
+#include "api.h"
+
+namespace mpa {
+
+__global__ __launch_bounds__(512) void comm_emulator_kernel(float* __restrict__ sink,
+                                                            long long cycles) {
+  extern __shared__ float buf[];
+  buf[threadIdx.x] = (float)threadIdx.x;  // touch the LDS allocation
+  __syncthreads();
+  const long long t0 = wall_clock64();
+  float acc = buf[(threadIdx.x + 1) % blockDim.x];
+  while (wall_clock64() - t0 < cycles) acc = acc * 0.999f + 1.f;
+  if (acc == -1.f) sink[blockIdx.x] = acc;  // never true; keeps the loop
+}
+
+void comm_emulator(int blocks, int threads, int lds_bytes, double us, float* sink, hipStream_t s) {
+  int dev = 0, khz = 100000;  // wall_clock64 ticks at the device's fixed reference clock
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  const long long cycles = (long long)(us * 1e-3 * khz);
+  hipLaunchKernelGGL(comm_emulator_kernel, dim3(blocks), dim3(threads), (size_t)lds_bytes, s,
+                     sink, cycles);
+}
+
+}  // namespace mpa
