@@ -608,6 +608,14 @@ void comm_emulator(int64_t blocks, int64_t threads, int64_t lds_bytes, double us
   mpa::comm_emulator(blocks, threads, lds_bytes, us, sink.data_ptr<float>(), cur_stream());
 }
 
+void atomic_latency(int64_t blocks, int64_t iters, int64_t mode, Tensor q) {
+  CHECK_CUDA(q);
+  TORCH_CHECK(q.scalar_type() == at::kInt && q.numel() >= std::max<int64_t>(blocks * 32, 1 << 20) + 1,
+              "atomic_latency: q int32 with >= max(32 blocks, 2^20) + 1 words");
+  const c10::OptionalDeviceGuard g(device_of(q));
+  mpa::atomic_latency(blocks, iters, mode, q.data_ptr<int>(), cur_stream());
+}
+
 // ------------------------------------------------------------------------ loss / acc
 // logits: [B][NC] bf16 with unit column stride; rows may be padded (stride(0) >= NC, a
 // view of a classifier's padded output)
@@ -822,6 +830,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("comm_emulator", &comm_emulator, "diagnostics: occupy CUs like a concurrent collective");
+  m.def("atomic_latency", &atomic_latency, "diagnostics: dependent atomic round trips");
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, py::arg("z"), py::arg("stats"),

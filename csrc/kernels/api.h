@@ -109,6 +109,7 @@ bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path
 // a K-contiguous B); run_rows / the fused-reduction dgrad take it when conv3_halo_ok
 bool conv3_halo_ok(const IGemmArgs& a);
 int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
+int* wq_slice(int n);  // zeroed work-queue counters for a persistent launch (igemm.hip)
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
 // halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z
@@ -240,5 +241,6 @@ void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf
 
 // diag.hip: stand-in for a concurrent RCCL collective (bench.py --emulate-comm)
 void comm_emulator(int blocks, int threads, int lds_bytes, double us, float* sink, hipStream_t s);
+void atomic_latency(int blocks, int iters, int mode, int* q, hipStream_t s);  // diag.hip
 
 }  // namespace mpa

@@ -32,4 +32,25 @@ void comm_emulator(int blocks, int threads, int lds_bytes, double us, float* sin
                      sink, cycles);
 }
 
+// atomic_latency: `iters` dependent device-scope atomicAdds (or, mode 3, dependent loads) by
+// thread 0 of each of `blocks` blocks; the kernel time / iters is the round trip the
+// persistent kernels' work-queue tickets must hide.  mode 0: one counter for all blocks,
+// 1: one per XCD (block % 8), 2: one per block, 3: loads of a per-block word.
+__global__ void atomic_latency_kernel(int* q, int iters, int mode) {
+  if (threadIdx.x != 0) return;
+  const int b = blockIdx.x;
+  int* c = q + (mode == 0 ? 0 : mode == 1 ? (b & 7) * 32 : b * 32);
+  int r = 0;
+  if (mode == 3) {
+    for (int i = 0; i < iters; ++i) r += __atomic_load_n(c + (r >> 30), __ATOMIC_RELAXED) & 1;
+  } else {
+    for (int i = 0; i < iters; ++i) r = atomicAdd(c + (r >> 30), 1);
+  }
+  if (r == -7) q[1 << 20] = r;  // never true: keeps the chain
+}
+
+void atomic_latency(int blocks, int iters, int mode, int* q, hipStream_t s) {
+  hipLaunchKernelGGL(atomic_latency_kernel, dim3(blocks), dim3(64), 0, s, q, iters, mode);
+}
+
 }  // namespace mpa
