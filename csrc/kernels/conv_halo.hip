@@ -470,11 +470,14 @@ struct HaloWPlan {
   int dbg;  // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
 };
 
+// W2T: the halo pitch as a compile-time constant (16 / 32 / 48 / 64: every ResNet and
+// Inception size), so a tap's row offset is an immediate DS offset; 0 = runtime pitch.
+template <int W2T>
 __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = p.H, W = p.W, HW = H * W, W2 = h.w2, C = p.C, K = p.Kout;
+  const int H = p.H, W = p.W, HW = H * W, W2 = W2T ? W2T : h.w2, C = p.C, K = p.Kout;
   const int M = p.Mpix, nimg = M / HW;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
 
@@ -502,6 +505,10 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     const uint32_t lc = (lane & 3) ^ (((hp >> 3) & 1) << 1);
     hsc[j] = sl | (colp << 10) | (lc << 18);
   }
+  // buffer descriptors, once: dy and the partition's two 32-channel halo chunks
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, h.dy_bytes);
+  const __amdgpu_buffer_rsrc_t rx0 = make_rsrc(p.x, h.x_bytes);
+  const __amdgpu_buffer_rsrc_t rx1 = make_rsrc((const char*)p.x + 64, h.x_bytes);
   uint32_t hv[HW_HIW], dv[4];
   // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
   const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
@@ -549,14 +556,15 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       }
   };
   // DMA instruction j of a tile: dy rows (0..3), halo chunk 0 (4..10), halo chunk 1 (11..17)
+  const uint32_t sw = lds_base(smem) + wave * 4096;  // this wave's DMA pieces: + 1 KiB each
   auto dmaw = [&](int stage, int j) {
-    char* st = smem + stage * HW_STAGE;
+    const uint32_t st = sw + stage * HW_STAGE;
     if (j < 4) {
-      buf_lds16_asm(make_rsrc(p.dy, h.dy_bytes), st + (4 * wave + j) * 1024, dv[j]);
+      buf_lds16_at(rdy, st + j * 1024, dv[j]);
     } else {
       const int ch = (j - 4) / HW_HIW, jj = (j - 4) % HW_HIW;
-      const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)p.x + ch * 64, h.x_bytes);
-      buf_lds16_asm(rx, st + HW_DBYTES + ch * HW_HBYTES + (wave * HW_HIW + jj) * 1024, hv[jj]);
+      buf_lds16_at(ch ? rx1 : rx0, st - wave * 4096 + HW_DBYTES + ch * HW_HBYTES +
+                                       (wave * HW_HIW + jj) * 1024, hv[jj]);
     }
   };
   auto issue = [&](int stage) {
@@ -575,18 +583,24 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     prep(z);
     issue(0);
   }
-  for (int k = 0; k < ntiles; ++k) {
+  // tile k from stage k & 1; MORE (all but the block's last tile): prepare tile k + 1 and
+  // issue its 18 DMAs into the other stage inside this tile's MFMA stream, one per two
+  // tap-steps.  The last tile is peeled so the loop body carries no per-DMA branch.
+  auto tile = [&](int k, auto nmore) {
+    constexpr bool MORE = decltype(nmore)::value;
     const int st = k & 1;
     wait_all_barrier();
+    // this tile's B-row bases at row tap dh = -1 in stage st (tap dh adds (dh+1)*W2*64: an
+    // immediate offset when W2T != 0); also frees hbw for the next tile's prep
     int hbk[4][2][3];
+    const int hb0 = st * HW_STAGE + hoff - W2 * 64;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int d = 0; d < 3; ++d) hbk[ks][e][d] = hbw[ks][e][d];
-    const bool more = k + 1 < ntiles;
-    if (more) prep(z + (k + 1) * h.Z);  // next tile's 18 DMAs: one per 2 tap-steps below
+        for (int d = 0; d < 3; ++d) hbk[ks][e][d] = hbw[ks][e][d] + hb0;
+    if constexpr (MORE) prep(z + (k + 1) * h.Z);
     const char* sbase = smem + st * HW_STAGE;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -595,22 +609,26 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sbase + ks * 4096, 16 * km, lane);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int base = st * HW_STAGE + hoff + (t / 3 - 1) * W2 * 64;  // wave-uniform
+        const int off = (t / 3) * W2 * 64;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + base + hbk[ks][0][t % 3]));
+            LDS_PTR(s16x4, smem + hbk[ks][0][t % 3] + off));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + base + hbk[ks][1][t % 3]));
+            LDS_PTR(s16x4, smem + hbk[ks][1][t % 3] + off));
         s16x8 r;
         r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
         r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
         for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
-        if (more && !h.dbg && ((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
+        if constexpr (MORE) {
+          if (((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
+        }
       }
     }
     // (no barrier: tile k + 2's DMAs into stage st follow tile k + 1's top barrier)
-  }
+  };
+  for (int k = 0; k + 1 < ntiles; ++k) tile(k, std::true_type{});
+  if (ntiles > 0) tile(ntiles - 1, std::false_type{});
   // partial of this block -> slab z: dw[k][t][c] at k = k0 + 16 km + lane%16,
   // c = c0 + 16 wave + 4 (lane/16) .. +3
   const int64_t ncols = 9 * (int64_t)C;
@@ -794,7 +812,14 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
   h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
-  hipLaunchKernelGGL(conv3_halo_wgrad_kernel, dim3(h.parts * h.Z), dim3(256), 0, s, a, h);
+  const dim3 grid(h.parts * h.Z), blk(256);
+  switch (W2) {
+    case 16: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<16>, grid, blk, 0, s, a, h); break;
+    case 32: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<32>, grid, blk, 0, s, a, h); break;
+    case 48: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<48>, grid, blk, 0, s, a, h); break;
+    case 64: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<64>, grid, blk, 0, s, a, h); break;
+    default: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<0>, grid, blk, 0, s, a, h); break;
+  }
   return h.Z;
 }
 

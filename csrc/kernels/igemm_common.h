@@ -83,6 +83,19 @@ __device__ __forceinline__ void buf_lds16_asm(__amdgpu_buffer_rsrc_t r, const ch
                : "memory", "m0");
 }
 
+// The same with the LDS byte address as a wave-uniform 32-bit value (lds_base(smem) +
+// offset): converting a generic pointer per DMA costs a null check (s_cmp_lg_u64 +
+// s_cselect) and a 64-bit add on the scalar unit every time.
+__device__ __forceinline__ uint32_t lds_base(const void* smem) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)smem;
+}
+__device__ __forceinline__ void buf_lds16_at(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(lds), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void halo_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");

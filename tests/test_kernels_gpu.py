@@ -205,6 +205,8 @@ HALO_CASES = [
     (3, 9, 11, 96, 128),     # odd W, 3 chunks, two N-tiles, partial last M-tile
     (1, 5, 3, 32, 64),       # single chunk, tiny image, one partial M-tile
     (2, 35, 35, 64, 96),     # Inception-style odd spatial size
+    (2, 35, 35, 64, 128),    # halo wgrad at pitch 48
+    (3, 17, 17, 128, 64),    # halo wgrad at pitch 32, odd W, tiles across images
 ]
 
 
