@@ -92,7 +92,18 @@ __device__ __forceinline__ uint32_t lds_base(const void* smem) {
 __device__ __forceinline__ void buf_lds16_at(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :
-               : "s"(lds), "v"(voff), "s"(r)
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+
+// ... and with a wave-uniform soffset added to every lane's address (a per-step scalar
+// offset, e.g. the weight tap, at no VALU cost); soff must be >= 0
+__device__ __forceinline__ void buf_lds16_so(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff,
+                                             int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r),
+                 "s"(__builtin_amdgcn_readfirstlane(soff))
                : "memory", "m0");
 }
 

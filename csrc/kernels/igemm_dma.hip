@@ -24,6 +24,7 @@
 //    vmcnt(0) before the first ds_read of every K-step).
 // Requires 16-B granularity on both operands (the VW = 8 case of igemm.hip); the host
 // falls back to the register-staged engine otherwise.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include "igemm_common.h"
@@ -262,7 +263,7 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
 // MFMA busy 19 % - issue-bound on address arithmetic, not on LDS or memory.
 // ======================================================================================
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
-__global__ __launch_bounds__(WM * WN * 64, dma_occ(3 * (BM + BN) * 64 + MAXT * 8, WM * WN))
+__global__ __launch_bounds__(WM * WN * 64, dma_occ(3 * (BM + BN) * 64 + MAXT * 16, WM * WN))
 void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
@@ -274,13 +275,14 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
   static_assert(IA % NW == 0 && (NW == 4 || NW == 8), "tile");
-  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE + MAXT * 8];
-  int* tap_hw = (int*)(smem + 3 * STAGE);
-  int* tap_b = tap_hw + MAXT;
+  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE + MAXT * 16];
+  int* tap_hw = (int*)(smem + 3 * STAGE);  // (dh << 16) | (dw & 0xffff)
+  int* tap_b = tap_hw + MAXT;              // weight tap (| super-tap column count << 12)
+  int* tap_ab = tap_b + MAXT;              // byte offsets: A pixel shift [MAXT], B tap [MAXT]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
   int tile = xcd_remap(blockIdx.x, p.tiles_total);
@@ -304,19 +306,30 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const int ktiles = Ktot / BK;  // aC % 32 == 0 => Ktot % 32 == 0
   const int kbeg = blockIdx.z * kps;
   const int kend = min(ktiles, kbeg + kps);
+  const int aC = p.aC;
 
   for (int t = tid; t < T; t += NT) {
-    tap_hw[t] = ((int)p.taps.dh[tap0 + t] << 16) | ((int)p.taps.dw[tap0 + t] & 0xffff);
-    tap_b[t] = p.taps.bt[tap0 + t];
+    const int dh = p.taps.dh[tap0 + t], dw = p.taps.dw[tap0 + t], bt = p.taps.bt[tap0 + t];
+    tap_hw[t] = (dh << 16) | (dw & 0xffff);
+    tap_b[t] = bt;
+    tap_ab[t] = (dh * p.aW + dw) * aC * 2;
+    tap_ab[MAXT + t] = BKC ? (bt & 0xfff) * aC * 2 : (bt & 0xfff) * p.ldb * 2;
   }
   __syncthreads();
 
+  // Operands as buffer descriptors with 32-bit byte offsets (the host keeps both tensors
+  // under 2 GiB); a lane past an edge gets offset 2^31 >= num_records and DMAs zeros.  Per
+  // K-step an A DMA is one add and one select, a B DMA is free: the weight tap's offset
+  // rides in the scalar soffset.  (The 64-bit pointer form cost ~9 VALU + 5 SALU per MFMA:
+  // issue-bound, MFMA busy ~25 %.)
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, 0x7fffffffu);
+  const uint32_t s32 = lds_base(smem);
   const int kch = kc_lane_chunk(lane);
-  const int aC = p.aC;
   // K elements per tap-table entry: aC, or 32 for super-taps (4 kernel columns x 8 ch)
   const int kpt = p.stap ? BK : aC;
   // ---- A rows (rows past M clamp to M-1: their outputs are discarded)
-  const bf16_t* a_ptr[IAW];
+  uint32_t a_off[IAW];
   int a_bh[IAW], a_bw[IAW];
 #pragma unroll
   for (int i = 0; i < IAW; ++i) {
@@ -327,52 +340,47 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     const int oh = r / g.oW;
     a_bh[i] = oh * p.Uh + p.Oh;
     a_bw[i] = (r - oh * g.oW) * p.Uw + p.Ow;
-    const int64_t base = (((int64_t)img * p.aH + a_bh[i]) * p.aW + a_bw[i]) * aC + kch * 8;
-    a_ptr[i] = p.A + base;
+    // (may be "negative" for a padded origin; the valid taps bring it back in range)
+    a_off[i] = (uint32_t)((((img * p.aH + a_bh[i]) * p.aW + a_bw[i]) * aC + kch * 8) * 2);
     if (p.stap) a_bw[i] += kch;  // super-tap: chunk kch is the input pixel kch columns right
   }
   // ---- B rows (K-contig) or k-rows x column chunks (N-contig), clamped
-  const bf16_t* b_ptr[IBW];
+  uint32_t b_off[IBW];
 #pragma unroll
   for (int i = 0; i < IBW; ++i) {
     const int jb = min(wave + NW * i, IB - 1);
     if constexpr (BKC) {
       const int n = min(n0 + 16 * jb + (lane >> 2), p.N - 1);
-      b_ptr[i] = p.B + (size_t)n * p.ldb + kch * 8;
+      b_off[i] = (uint32_t)((n * p.ldb + kch * 8) * 2);
     } else {
       const int krow = RPI * jb + lane / CPR;
       const int col = min(n0 + (((lane % CPR) ^ mn_swz<BN>(krow)) << 3), p.N - 8);
-      b_ptr[i] = p.B + (size_t)krow * p.RS * p.ldb + col;
+      b_off[i] = (uint32_t)((krow * p.RS * p.ldb + col) * 2);
     }
   }
-  const bf16_t* const zp = (const bf16_t*)g_zero16;
 
   // K-step state (wave-uniform): tap index and channel offset of k = kt * 32
   int t_s = (kbeg * BK) / kpt;
   int c_s = kbeg * BK - t_s * kpt;
-  auto issue = [&](int kt, char* st) {
+  auto issue = [&](uint32_t st) {  // st: the stage's LDS byte address
     const int hwv = __builtin_amdgcn_readfirstlane(tap_hw[t_s]);
     const int dh = hwv >> 16, dw = (short)(hwv & 0xffff);
-    const int64_t toff = ((int64_t)dh * p.aW + dw) * aC + c_s;
+    const int toff = __builtin_amdgcn_readfirstlane(tap_ab[t_s]) + c_s * 2;
 #pragma unroll
     for (int i = 0; i < IAW; ++i) {
       const bool ok = ((unsigned)(a_bh[i] + dh) < (unsigned)p.aH) &
                       ((unsigned)(a_bw[i] + dw) < (unsigned)p.aW);
-      glds16(ok ? a_ptr[i] + toff : zp, st + (wave * IAW + i) * 1024);
+      buf_lds16_at(ra, st + (wave * IAW + i) * 1024, ok ? a_off[i] + toff : 0x80000000u);
     }
-    char* bimg = st + A_BYTES;
-    // weight tap in bits 0..11; super-taps carry their valid column count in bits 12..14
-    const int btv = __builtin_amdgcn_readfirstlane(tap_b[t_s]);
-    const int bt = btv & 0xfff;
-    int64_t boff;
-    if constexpr (BKC) boff = (int64_t)bt * aC + c_s;  // weight K index (bt, c)
-    else boff = ((int64_t)c_s * p.RS + bt) * p.ldb;
+    const uint32_t bst = st + A_BYTES;
+    const int boff = __builtin_amdgcn_readfirstlane(tap_ab[MAXT + t_s]) +
+                     (BKC ? c_s * 2 : c_s * p.RS * p.ldb * 2);
     // super-tap: chunks past the kernel's last column read zeros (ns valid columns)
-    const bool bok = !p.stap || kch < (btv >> 12);
+    const bool bok = !p.stap || kch < (__builtin_amdgcn_readfirstlane(tap_b[t_s]) >> 12);
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
       const int jb = wave + NW * i;
-      if (jb < IB) glds16(bok ? b_ptr[i] + boff : zp, bimg + jb * 1024);
+      if (jb < IB) buf_lds16_so(rb, bst + jb * 1024, bok ? b_off[i] : 0x80000000u, boff);
     }
     c_s += BK;
     if (c_s >= kpt) { c_s = 0; ++t_s; }
@@ -403,15 +411,17 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   };
 
   if (kbeg < kend) {
-    issue(kbeg, smem);
-    if (kbeg + 1 < kend) issue(kbeg + 1, smem + STAGE);
+    issue(s32);
+    if (kbeg + 1 < kend) issue(s32 + STAGE);
     int kt = kbeg;
-    // one ring revolution per iteration: stage offsets are compile-time constants
+    // one ring revolution per iteration: stage offsets are compile-time constants.  The
+    // DMAs are inline asm (invisible to the compiler's waits): the counted wait_barrier is
+    // the only thing that orders them before the fragment reads.
     auto step = [&](auto sc) {
       constexpr int S = decltype(sc)::value;
       if (kt + 1 < kend) wait_barrier<WAITN>();
       else wait_barrier<0>();
-      if (kt + 2 < kend) issue(kt + 2, smem + ((S + 2) % 3) * STAGE);
+      if (kt + 2 < kend) issue(s32 + ((S + 2) % 3) * STAGE);
       compute(smem + S * STAGE);
       ++kt;
     };
@@ -726,9 +736,21 @@ static bool g_dma_uni = [] {
 }();
 void igemm_set_dma_uni(int on) { g_dma_uni = on != 0; }
 bool igemm_stap_ok() { return g_dma_uni && igemm_engine() >= 1; }
+// byte extents of the rows kernel's operands: the uniform-tap kernel addresses both with
+// 32-bit offsets
+static bool rows_uni_fits(const IGemmArgs& a, bool bkc) {
+  const PhaseDesc* d = a.nphase > 0 ? &a.ph[0] : nullptr;
+  const int64_t hw = d ? (int64_t)d->oH * d->oW : (int64_t)a.oH * a.oW;
+  const int64_t m = d ? d->M : a.M;
+  const int64_t nimg = hw > 0 ? (m + hw - 1) / hw : 0;
+  const int64_t abytes = nimg * a.aH * a.aW * a.aC * 2;
+  const int64_t bbytes = (bkc ? (int64_t)a.N : (int64_t)a.aC * a.RS) * a.ldb * 2;
+  return abytes < (1ll << 31) && bbytes < (1ll << 31);
+}
+
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
 static void launch_rows_dma_v(const IGemmArgs& a, dim3 grid, hipStream_t s) {
-  if ((a.aC % BK == 0 || a.stap) && g_dma_uni)
+  if ((a.aC % BK == 0 || a.stap) && g_dma_uni && rows_uni_fits(a, BKC))
     hipLaunchKernelGGL((igemm_rows_dma_uni_kernel<BM, BN, WM, WN, BKC, SPLIT, PH>), grid,
                        dim3(WM * WN * 64), 0, s, a);
   else
