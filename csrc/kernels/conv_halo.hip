@@ -212,6 +212,7 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
 
 template <bool WRES, int EPI, bool FULL>
 __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
+  constexpr int HB_DPT = WRES ? 2 : 4;  // next-item DMAs per tap
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
   char* const hal = smem;
   char* const wst = smem + 2 * HB_HBYTES;
@@ -370,8 +371,10 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
         for (int jn = 0; jn < 4; ++jn)
           acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
                               (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
-      nd(2 * t);
-      nd(2 * t + 1);
+      // the next item's DMAs, front-loaded: its 18 (9 with resident weights) land by tap
+      // 4, so the top-of-item wait finds them done instead of waiting out the last ones
+#pragma unroll
+      for (int d = 0; d < HB_DPT; ++d) nd(HB_DPT * t + d);
     }
   };
 
