@@ -808,6 +808,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_engine", &mpa::igemm_engine, "GEMM staging engine: 1 LDS-DMA, 0 register");
   m.def("igemm_set_engine", &mpa::igemm_set_engine);
   m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
+  m.def("igemm_set_tune", &mpa::igemm_set_tune, "tile autotuner on/off (MPA_TUNE)");
+  m.def("igemm_tuned_table", &mpa::igemm_tuned_table, "autotuned GEMM tiles so far");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");
   m.def("igemm_halo_enabled", &mpa::igemm_halo_enabled);

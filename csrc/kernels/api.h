@@ -2,6 +2,7 @@
 // structs, no torch headers: the .hip translation units compile in seconds and the
 // torch-facing binding layer (csrc/bindings.cpp) validates shapes and allocates.
 #pragma once
+#include <string>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -103,13 +104,15 @@ int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split sl
 int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LDS-DMA all
 void igemm_set_engine(int engine);
 void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
+// tile autotuner (igemm.hip): on by default (MPA_TUNE=0 off); the cached choices as text
+void igemm_set_tune(int on);
+std::string igemm_tuned_table();
 void igemm_set_dma_uni(int on);  // LDS-DMA uniform-tap fast path (default on)
 bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path on)
 // conv_halo.hip: halo-staged direct 3x3 / stride-1 conv (forward and stride-1 dgrad with
 // a K-contiguous B); run_rows / the fused-reduction dgrad take it when conv3_halo_ok
 bool conv3_halo_ok(const IGemmArgs& a);
 int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
-int* wq_slice(int n);  // zeroed work-queue counters for a persistent launch (igemm.hip)
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
 // halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z

@@ -27,7 +27,11 @@
 // flight while tile k's MFMAs run, one barrier per K-step.  Blocks are remapped so tiles
 // sharing an operand panel land on the same XCD (private L2).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
 #include "igemm_common.h"
 
 namespace mpa {
@@ -534,6 +538,90 @@ void igemm_force_tile(int bm, int bn, int splits) {
   g_force_bm = bm; g_force_bn = bn; g_force_splits = splits;
 }
 
+// ---------------------------------------------------------------------- tile autotuner
+// The static plans (rows_plan / wgrad_plan) were fitted on a few shapes and miss by 10-25 %
+// elsewhere (tools/bench_kernels.py sweep at batch 512: layer4's strided conv runs 24 %
+// faster on 256x128, layer2's strided wgrad 10 % faster on 128x256, layer3's 15 % faster on
+// 128x128).  Like cudnn.benchmark, the first launch of each GEMM shape on the LDS-DMA
+// engine times every eligible tile on scratch outputs (a warm-up run, then 3 timed ones)
+// and caches the fastest; later launches reuse it.  The sweep costs a few ms once per shape
+// (the warm-up steps of a training run), is skipped while a HIP graph is being captured
+// (the static plan runs then) and is off with MPA_TUNE=0.  Tiles never change a result's
+// summation order except through the split-K count, which candidates may not raise past
+// the caller's workspace.
+static bool g_tune = [] {
+  const char* e = getenv("MPA_TUNE");
+  return !(e && e[0] == '0');
+}();
+void igemm_set_tune(int on) { g_tune = on != 0; }
+
+struct TunedTile {
+  int bm, bn;
+};
+static std::mutex g_tune_mu;
+static std::map<std::string, TunedTile> g_tuned;
+
+static bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+// grow-only per-device scratch for the candidates' outputs
+static char* tune_scratch(size_t bytes) {
+  static char* buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (bytes > cap[dev]) {
+    if (buf[dev]) (void)hipFree(buf[dev]);
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc(&buf[dev], bytes) != hipSuccess) return nullptr;
+    cap[dev] = bytes;
+  }
+  return buf[dev];
+}
+
+// mean time of fn() over 3 launches after one warm-up, in ms
+template <class F>
+static float time_launches(F&& fn, hipStream_t s) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  fn();
+  (void)hipEventRecord(e0, s);
+  for (int i = 0; i < 3; ++i) fn();
+  (void)hipEventRecord(e1, s);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms / 3.f;
+}
+
+static bool tuned_lookup(const std::string& key, int& bm, int& bn) {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  auto it = g_tuned.find(key);
+  if (it == g_tuned.end()) return false;
+  bm = it->second.bm;
+  bn = it->second.bn;
+  return true;
+}
+static void tuned_store(const std::string& key, int bm, int bn) {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  g_tuned[key] = TunedTile{bm, bn};
+}
+
+// number of tuned shapes and a readable dump ("key -> BMxBN" lines) for diagnostics
+std::string igemm_tuned_table() {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  std::string out;
+  for (const auto& kv : g_tuned)
+    out += kv.first + " -> " + std::to_string(kv.second.bm) + "x" + std::to_string(kv.second.bn) + "\n";
+  return out;
+}
+
 template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
 static void launch_rows(const IGemmArgs& a, int splits, hipStream_t s) {
   dim3 grid(a.tiles_total, 1, splits);
@@ -589,19 +677,24 @@ static void finish_split_plan(int ktiles, int& splits, int& per_split) {
 // through igemm_force_tile; tools/bench_kernels.py sweep measures them slower than 128x128
 // on every ResNet layer: they leave the grid under one block per CU or force split-K,
 // whose fp32 partial slab costs more than the tile saves).
-static void rows_plan(IGemmArgs& a, int& BM, int& BN, int& splits, bool allow_split, bool dma) {
+static bool rows_tile_ok(int bm, int bn, bool dma) {
+  const bool ok_reg = (bm == 128 && bn == 128) || (bm == 256 && bn == 64) || (bm == 128 && bn == 32);
+  const bool ok_dma = ok_reg || (bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && bn == 64);
+  return dma ? ok_dma : ok_reg;
+}
+
+// tbm / tbn: a tile chosen by the autotuner (0: the heuristic); igemm_force_tile wins
+static void rows_plan(IGemmArgs& a, int& BM, int& BN, int& splits, bool allow_split, bool dma,
+                      int tbm = 0, int tbn = 0) {
   BN = choose_bn(a.N);
   // 64-wide GEMMs: the DMA engine's 128x64 tile (36 KiB ring, 4 blocks/CU) beats 256x64
   // (60 KiB, 2 blocks/CU) on every ResNet-18 64-channel layer by 8-20 % (tile sweep)
   BM = (BN == 64 && !dma) ? 256 : 128;
   const int ktiles = (a.Ktot + BK - 1) / BK;
-  if (g_force_bm && g_force_bn) {
-    const bool ok_reg = (g_force_bm == 128 && g_force_bn == 128) ||
-                        (g_force_bm == 256 && g_force_bn == 64) ||
-                        (g_force_bm == 128 && g_force_bn == 32);
-    const bool ok_dma = ok_reg || (g_force_bm == 256 && (g_force_bn == 256 || g_force_bn == 128)) ||
-                        (g_force_bm == 128 && g_force_bn == 64);
-    if (dma ? ok_dma : ok_reg) { BM = g_force_bm; BN = g_force_bn; }
+  if (tbm && tbn && rows_tile_ok(tbm, tbn, dma)) { BM = tbm; BN = tbn; }
+  if (g_force_bm && g_force_bn && rows_tile_ok(g_force_bm, g_force_bn, dma)) {
+    BM = g_force_bm;
+    BN = g_force_bn;
   }
   a.tiles_n = (a.N + BN - 1) / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
@@ -633,8 +726,68 @@ static int64_t slab_rows_max(int M) {
 
 int64_t igemm_slab_floats(int M, int N) { return slab_rows_max(M) * 2 * N + 2 * N; }
 
+static void rows_run_plan(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s,
+                          int tbm, int tbn);
+
+static std::string rows_key(const IGemmArgs& a, bool bkc, bool split) {
+  char k[256];
+  snprintf(k, sizeof k, "rows%d%d M%d N%d K%d a%dx%dx%d o%dx%d U%d,%d O%d,%d T%d s%d b%d r%d p%d",
+           (int)bkc, (int)split, a.M, a.N, a.Ktot, a.aH, a.aW, a.aC, a.oH, a.oW, a.Uh, a.Uw,
+           a.Oh, a.Ow, a.T, a.stap, a.beta, a.relu, a.nphase);
+  std::string key(k);
+  for (int i = 0; i < a.nphase; ++i)
+    key += " " + std::to_string(a.ph[i].M) + "," + std::to_string(a.ph[i].Ktot);
+  return key;
+}
+
+static const int kRowsCands[][2] = {{128, 128}, {256, 128}, {128, 64}, {256, 64}, {128, 32}};
+
+static bool rows_cand_ok(int bm, int bn, int N) {
+  (void)bm;
+  if (bn == 128 && N <= 64) return false;  // half-empty tiles
+  if (bn == 64 && (N <= 32 || N > 1024)) return false;
+  if (bn == 32 && N > 32) return false;
+  return true;
+}
+
+// autotuned tile of a rows GEMM (fills tbm / tbn; leaves them 0 to keep the heuristic)
+static void tuned_rows_tile(const IGemmArgs& a, bool bkc, int vw, bool allow_split, hipStream_t s,
+                            int& tbm, int& tbn) {
+  if (!g_tune || (g_force_bm && g_force_bn) || a.M <= 0 || stream_capturing(s)) return;
+  const std::string key = rows_key(a, bkc, allow_split);
+  if (tuned_lookup(key, tbm, tbn)) return;
+  const int64_t ws_cap = allow_split ? igemm_ws_floats(a.M, a.N, a.Ktot) : 0;
+  const int64_t cbytes = ((int64_t)a.M * std::max(a.ldc, a.N) * 2 + 255) / 256 * 256;
+  const int64_t sbytes = (igemm_slab_floats(a.M, a.N) + 2 * a.N) * 4;
+  float best = 1e30f;
+  int bbm = 0, bbn = 0;
+  for (const auto& c : kRowsCands) {
+    if (!rows_cand_ok(c[0], c[1], a.N)) continue;
+    IGemmArgs b = a;
+    int BM, BN, sp;
+    rows_plan(b, BM, BN, sp, allow_split, true, c[0], c[1]);
+    if (BM != c[0] || BN != c[1]) continue;
+    if (sp > 1 && (int64_t)sp * a.M * a.N > ws_cap) continue;
+    const int64_t wbytes = sp > 1 ? (int64_t)sp * a.M * a.N * 4 : 0;
+    char* scr = tune_scratch(cbytes + sbytes + wbytes + 512);
+    if (!scr) return;
+    b = a;
+    b.C = scr;
+    float* slab = (float*)(scr + cbytes);
+    if (a.stats) b.stats = slab + igemm_slab_floats(a.M, a.N);  // [2][N] after the slab
+    float* ws = sp > 1 ? (float*)(scr + cbytes + sbytes) : nullptr;
+    if (!allow_split) ws = nullptr;
+    else if (!ws) ws = (float*)(scr + cbytes + sbytes);  // (unused: no split)
+    const float t = time_launches([&] { rows_run_plan(b, bkc, vw, ws, slab, s, c[0], c[1]); }, s);
+    if (t < best) { best = t; bbm = c[0]; bbn = c[1]; }
+  }
+  if (!bbm) return;
+  tuned_store(key, bbm, bbn);
+  tbm = bbm;
+  tbn = bbn;
+}
+
 static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
-  int BM, BN, splits;
   const bool dma = use_dma(vw);
   if (dma && bkc && conv_stem_ok(a)) {  // 7x7 pixel-pair stem: row-staged direct conv
     float* stats = a.stats;
@@ -653,7 +806,17 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s);
     return;
   }
-  rows_plan(a, BM, BN, splits, ws != nullptr, dma);
+  int tbm = 0, tbn = 0;
+  if (dma) tuned_rows_tile(a, bkc, vw, ws != nullptr, s, tbm, tbn);
+  rows_run_plan(a, bkc, vw, ws, slab, s, tbm, tbn);
+}
+
+// the GEMM part of run_rows for a given (tuned) tile
+static void rows_run_plan(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s,
+                          int tbm, int tbn) {
+  int BM, BN, splits;
+  const bool dma = use_dma(vw);
+  rows_plan(a, BM, BN, splits, ws != nullptr, dma, tbm, tbn);
   const int tiles_m = (a.M + BM - 1) / BM;
   void* final_out = a.C;
   float* stats = a.stats;
@@ -709,7 +872,7 @@ int64_t igemm_bnred_slab_floats(int M, int N, int nphase) {
 }
 
 // tile plan of a merged stride-phase launch; returns the number of (phase, m-tile) rows
-static int plan_phases(IGemmArgs& a, int& BM, int& BN) {
+static int plan_phases(IGemmArgs& a, int& BM, int& BN, int tbm = 0, int tbn = 0) {
   IGemmArgs probe = a;
   probe.M = 0;
   probe.Ktot = 0;
@@ -718,7 +881,7 @@ static int plan_phases(IGemmArgs& a, int& BM, int& BN) {
     probe.Ktot = std::max(probe.Ktot, a.ph[i].Ktot);
   }
   int splits;
-  rows_plan(probe, BM, BN, splits, false, true);
+  rows_plan(probe, BM, BN, splits, false, true, tbm, tbn);
   a.tiles_n = (a.N + BN - 1) / BN;
   int most = 0, rows = 0;
   for (int i = 0; i < a.nphase; ++i) {
@@ -766,8 +929,30 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
   a.bias = nullptr;
   if (a.nphase <= 0) return;
   if (use_dma(vw) && a.nphase <= MAXPH) {
+    int tbm = 0, tbn = 0;
+    if (g_tune && !(g_force_bm && g_force_bn) && !stream_capturing(s)) {
+      const std::string key = rows_key(a, bkc, false);
+      if (!tuned_lookup(key, tbm, tbn)) {  // time the merged launch per candidate tile
+        const int64_t hw0 = std::max(1, a.ph[0].oH * a.ph[0].oW);
+        const int64_t rows = (a.ph[0].M + hw0 - 1) / hw0 * a.dH * a.dW;  // dx pixels
+        const int64_t cbytes = rows * std::max(a.ldc, a.N) * 2;
+        char* scr = tune_scratch(cbytes + 256);
+        float best = 1e30f;
+        for (const auto& c : kRowsCands) {
+          if (!scr || !rows_cand_ok(c[0], c[1], a.N)) continue;
+          IGemmArgs b = a;
+          int BM, BN;
+          plan_phases(b, BM, BN, c[0], c[1]);
+          if (BM != c[0] || BN != c[1] || b.tiles_total <= 0) continue;
+          b.C = scr;
+          const float t = time_launches([&] { igemm_rows_dma(b, BM, BN, bkc, 1, s); }, s);
+          if (t < best) { best = t; tbm = c[0]; tbn = c[1]; }
+        }
+        if (tbm) tuned_store(key, tbm, tbn);
+      }
+    }
     int BM, BN;
-    plan_phases(a, BM, BN);
+    plan_phases(a, BM, BN, tbm, tbn);
     if (a.tiles_total > 0 && igemm_rows_dma(a, BM, BN, bkc, 1, s)) return;
   }
   for (int i = 0; i < a.nphase; ++i) {  // one launch per phase
@@ -818,17 +1003,24 @@ static bool wgrad_big(const WGradArgs& a, bool dma_ok) {
   return dma_ok && (a.Kout >= 256 || ((int64_t)a.Kout * a.Ncols <= 32768 && a.Mpix >= (1 << 20)));
 }
 
-static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bool big) {
+static bool wgrad_tile_ok(int bm, int bn, bool dma) {
+  const bool ok_reg = (bm == 64 || bm == 128) && bn == 128;
+  const bool ok_dma = ok_reg || (bn == 256 && (bm == 64 || bm == 128 || bm == 256));
+  return dma ? ok_dma : ok_reg;
+}
+
+static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bool big,
+                       int tbm = 0, int tbn = 0) {
   BM = (a.Kout <= 64) ? 64 : 128;
   BN = 128;
   // few 128-row tiles (e.g. a 1x1 downsample: Ncols = C_in): halve BM for parallelism
   if (dma && BM == 128 && ((a.Kout + 127) / 128) * ((a.Ncols + 127) / 128) < 4) BM = 64;
   if (big) BN = 256, BM = (a.Kout <= 64) ? 64 : 128;  // 64-row stems: no half-empty tile
-  if (g_force_bm && g_force_bn) {
-    const bool ok_reg = (g_force_bm == 64 || g_force_bm == 128) && g_force_bn == 128;
-    const bool ok_dma = ok_reg || (g_force_bn == 256 && (g_force_bm == 64 || g_force_bm == 128 ||
-                                                         g_force_bm == 256));
-    if (dma ? ok_dma : ok_reg) { BM = g_force_bm; BN = g_force_bn; }
+  const bool tuned = tbm && tbn && wgrad_tile_ok(tbm, tbn, dma);
+  if (tuned) { BM = tbm; BN = tbn; }
+  if (g_force_bm && g_force_bn && wgrad_tile_ok(g_force_bm, g_force_bn, dma)) {
+    BM = g_force_bm;
+    BN = g_force_bn;
   }
   a.tiles_n = (a.Ncols + BN - 1) / BN;
   const int tiles_m = (a.Kout + BM - 1) / BM;
@@ -838,7 +1030,7 @@ static void wgrad_plan(WGradArgs& a, int& BM, int& BN, int& splits, bool dma, bo
   // column tiles x 512 splits instead of one 64x256 tile x 512 splits
   // (profiles/stem_sweep_b512.txt, batch 512: 64x128/s512 439.4 us, 64x128/s1024 449.2 us,
   // 64x256/s512 493.7 us). 512 splits keep the fp32 slab at 29 MB (1024: 58.7 MB).
-  const bool stem2 = big && BM == 64 && BN == 256 && !(g_force_bm && g_force_bn) &&
+  const bool stem2 = big && BM == 64 && BN == 256 && !(g_force_bm && g_force_bn) && !tuned &&
                      a.Ncols > 128 && a.Ncols <= 256;
   if (stem2) {
     BN = 128;
@@ -866,8 +1058,44 @@ int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
   return best;
 }
 
+static void wgrad_run_plan(WGradArgs a, int vwa, int vwb, hipStream_t s, int tbm, int tbn);
+
+static const int kWgradCands[][2] = {{64, 128}, {128, 128}, {64, 256}, {128, 256}, {256, 256}};
+
+// autotuned tile of a (non-halo) weight-gradient GEMM; candidates run on a scratch slab
+// and a scratch dw, and may not need more split slab than the caller allocated
+static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s, int& tbm,
+                             int& tbn) {
+  if (!g_tune || (g_force_bm && g_force_bn) || a.Mpix <= 0 || stream_capturing(s)) return;
+  char k[200];
+  snprintf(k, sizeof k, "wgrad K%d N%d P%d x%dx%dx%d o%dx%d f%dx%d s%d,%d p%d,%d", a.Kout, a.Ncols,
+           a.Mpix, a.H, a.W, a.C, a.P, a.Q, a.R, a.S, a.sh, a.sw, a.ph, a.pw);
+  const std::string key(k);
+  if (tuned_lookup(key, tbm, tbn)) return;
+  const int64_t out = (int64_t)a.Kout * a.Ncols;
+  const int64_t cap = igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix);
+  float best = 1e30f;
+  for (const auto& c : kWgradCands) {
+    if (c[0] > 64 && a.Kout <= 64) continue;  // half-empty tiles
+    if (c[1] == 256 && a.Ncols <= 128) continue;
+    WGradArgs b = a;
+    int BM, BN, sp;
+    const bool big = c[1] == 256;
+    wgrad_plan(b, BM, BN, sp, true, big, c[0], c[1]);
+    if (BM != c[0] || BN != c[1]) continue;
+    if (sp > 1 && (int64_t)sp * out > cap) continue;
+    char* scr = tune_scratch((size_t)(out + (sp > 1 ? sp * out : 0)) * 4 + 256);
+    if (!scr) return;
+    b = a;
+    b.dw = (float*)scr;
+    b.slab = a.slab ? (float*)scr + out : nullptr;
+    const float t = time_launches([&] { wgrad_run_plan(b, vwa, vwb, s, c[0], c[1]); }, s);
+    if (t < best) { best = t; tbm = c[0]; tbn = c[1]; }
+  }
+  if (tbm) tuned_store(key, tbm, tbn);
+}
+
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
-  int BM, BN, splits;
   if (igemm_engine() >= 1 && conv3_halo_wgrad_ok(a)) {  // 3x3 / stride 1: halo-staged
     const int z = conv3_halo_wgrad(a, s);
     const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 64 == 0: float4 rows
@@ -883,12 +1111,21 @@ void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
     return;
   }
   const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
-  const bool big = wgrad_big(a, dma_ok);
+  int tbm = 0, tbn = 0;
+  if (dma_ok) tuned_wgrad_tile(a, vwa, vwb, s, tbm, tbn);
+  wgrad_run_plan(a, vwa, vwb, s, tbm, tbn);
+}
+
+// the GEMM + split reduction of igemm_wgrad for a given (tuned) tile
+static void wgrad_run_plan(WGradArgs a, int vwa, int vwb, hipStream_t s, int tbm, int tbn) {
+  int BM, BN, splits;
+  const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
+  const bool big = (tbm && tbn) ? tbn == 256 : wgrad_big(a, dma_ok);
   // engine 1: big 8-wave tile where it wins, else the incremental-pixel DMA kernel
   // (tools/bench_kernels.py sweep: equal or faster than register staging on every
   // ResNet-18 wgrad shape it covers), else register staging
   const bool dma = big || (dma_ok && (igemm_engine() == 2 || igemm_wgrad_inc_ok(a)));
-  wgrad_plan(a, BM, BN, splits, dma, big);
+  wgrad_plan(a, BM, BN, splits, dma, big, tbm, tbn);
   if (dma && igemm_wgrad_dma(a, BM, BN, splits, s)) {
     // LDS-DMA engine (igemm_dma.hip)
   } else if (BM == 64) {

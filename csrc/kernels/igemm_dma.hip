@@ -772,7 +772,7 @@ static void launch_rows_dma(const IGemmArgs& a, int splits, hipStream_t s) {
 template <bool BKC>
 static bool rows_dma_tile(const IGemmArgs& a, int BM, int BN, int splits, hipStream_t s) {
   if (BM == 256 && BN == 256) launch_rows_dma<256, 256, 2, 4, BKC>(a, splits, s);
-  else if (BM == 256 && BN == 128) launch_rows_dma<256, 128, 4, 2, BKC>(a, splits, s);
+  else if (BM == 256 && BN == 128) launch_rows_dma<256, 128, 2, 2, BKC>(a, splits, s);
   else if (BM == 128 && BN == 128) launch_rows_dma<128, 128, 2, 2, BKC>(a, splits, s);
   else if (BM == 256 && BN == 64) launch_rows_dma<256, 64, 4, 1, BKC>(a, splits, s);
   else if (BM == 128 && BN == 64) launch_rows_dma<128, 64, 2, 2, BKC>(a, splits, s);

@@ -289,6 +289,48 @@ def test_conv_halo_wgrad(gpu, case):
     assert rel(dw, dwi) < 1e-3 and rel(dw - dw0, dwr - dw0) < 1e-2
 
 
+@pytest.mark.parametrize("case", [
+    # N, H, W, C, K, R, stride, pad: strided 3x3, 1x1 downsample, deep-K strided
+    (4, 14, 14, 64, 128, 3, 2, 1),
+    (4, 14, 14, 64, 128, 1, 2, 0),
+    (2, 7, 7, 256, 512, 3, 2, 1),
+])
+def test_gemm_autotune(gpu, case):
+    """Tile autotuner (igemm.hip, MPA_TUNE): the tuned plans give the static plans' results
+    (rows GEMMs keep their K order; a wgrad's split count may change) and the choices are
+    cached per shape."""
+    torch.manual_seed(31)
+    N, H, W, Cc, K, R, st, pd = case
+    P = (H + 2 * pd - R) // st + 1
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, R, R, Cc, dev=gpu, scale=1.0 / math.sqrt(R * R * Cc))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, R * R, K).contiguous()
+    dy = bf(N, P, P, K, dev=gpu)
+    e = torch.empty(0, device=gpu)
+
+    def run():
+        stt = torch.zeros(2, K, device=gpu)
+        y = C().conv_fwd(x, w, e, st, st, pd, pd, False, stt, e)
+        dx = C().conv_dgrad(dy, w, H, W, st, st, pd, pd, wt)
+        dw = torch.zeros(K, R, R, Cc, device=gpu)
+        C().conv_wgrad(dy, x, dw, st, st, pd, pd)
+        torch.cuda.synchronize()
+        return y, stt, dx, dw
+
+    C().igemm_set_tune(0)
+    try:
+        ref0 = run()
+    finally:
+        C().igemm_set_tune(1)
+    tuned = run()   # first call: tunes, then runs the chosen tiles
+    again = run()   # cached choice
+    for a, b, c in zip(ref0, tuned, again):
+        assert torch.isfinite(b.float()).all()
+        assert rel(b, a) < 1e-3 and torch.equal(b, c)
+    table = C().igemm_tuned_table()
+    assert "rows" in table and "wgrad" in table
+
+
 def test_conv_halo_repeatable(gpu):
     """Persistent 2-stage ring: repeated launches are bitwise identical (race screen)."""
     torch.manual_seed(23)

@@ -3,6 +3,7 @@ shapes at a given batch, reported as TFLOP/s.
 
     python tools/bench_kernels.py [batch] [iters]          engines 0 (register) and 1/2 (DMA)
     python tools/bench_kernels.py [batch] [iters] sweep    every tile on the DMA engine
+    (MPA_SWEEP_SHAPES=s2,ds: only the shapes whose name contains one of those)
 
 MPA_BENCH_ENGINES=0,1,1h,2 selects engines ("1h": halo 3x3/s1 kernel on); MPA_IGEMM_OCC=2|3|4 the register engine's
 occupancy target.  Sweep rows print each tile's time (us) with its split count forced to
@@ -68,7 +69,10 @@ def tensors(H, Ci, Co, R, st, pd):
 if SWEEP:
     C.igemm_set_engine(2)
     print("tile sweep, DMA engine, batch %d (us; TF in brackets)" % B)
+    only = os.environ.get("MPA_SWEEP_SHAPES")  # e.g. "s2,ds": names containing either
     for name, H, Ci, Co, R, st, pd in SHAPES:
+        if only and not any(k in name for k in only.split(",")):
+            continue
         flop, (f, d, w) = tensors(H, Ci, Co, R, st, pd)
         for label, fn, tiles in (("fwd", f, ROWS_TILES), ("dgrad", d, ROWS_TILES),
                                  ("wgrad", w, WGRAD_TILES)):
