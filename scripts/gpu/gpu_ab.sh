@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B runner: ./gpu_ab.sh "ENV=val ENV2=val" "ENV=val" ...  (each spec -> one bench run,
+# A/B runner: scripts/gpu/gpu_ab.sh "ENV=val ENV2=val" "ENV=val" ...  (each spec -> one bench run,
 # whole list twice, alternating, so box drift shows up); "-" = no extra env.
 mkdir -p gpurun_out
 ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5"}

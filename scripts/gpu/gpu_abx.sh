@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B runner with bench arguments: ./gpu_abx.sh "ENV=V ... | --bench-args ..." ...
+# A/B runner with bench arguments: scripts/gpu/gpu_abx.sh "ENV=V ... | --bench-args ..." ...
 # (either side of | may be empty; the list runs twice, alternating)
 mkdir -p gpurun_out
 BASE=${BENCH_ARGS:-"--steps 20 --warmup 5"}

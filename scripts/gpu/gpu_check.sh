@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU session runner: ./gpu_check.sh step1 step2 ...  Steps: kernels models smoke bench prof diag
+# GPU session runner: scripts/gpu/gpu_check.sh step1 step2 ...  Steps: kernels models smoke bench prof diag
 # Stops at the first crash/timeout (pytest rc 1 = test failures only, continue).
 mkdir -p gpurun_out
 export TMPDIR=/tmp

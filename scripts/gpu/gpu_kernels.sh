@@ -1,0 +1,8 @@
+#!/bin/bash
+# all kernel GPU tests + bench + one-step kernel sequence
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 500 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/t_kern.log 2>&1 || { echo "kernel tests rc=$?"; tail -30 gpurun_out/t_kern.log; exit 1; }
+tail -1 gpurun_out/t_kern.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 2>/dev/null | tail -1 || exit 1
+scripts/gpu/gpu_seq2.sh ${1:-new}

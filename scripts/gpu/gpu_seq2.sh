@@ -1,5 +1,5 @@
 #!/bin/bash
-# one-step kernel sequence: ./gpu_seq2.sh TAG [ENV=VAL ...]
+# one-step kernel sequence: scripts/gpu/gpu_seq2.sh TAG [ENV=VAL ...]
 mkdir -p gpurun_out
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT

@@ -1,5 +1,5 @@
 #!/bin/bash
-# per-kernel summary of one model's training step: ./gpu_zoo_prof.sh MODEL SIZE BATCH
+# per-kernel summary of one model's training step: scripts/gpu/gpu_zoo_prof.sh MODEL SIZE BATCH
 mkdir -p gpurun_out
 M=$1; S=$2; B=$3
 R=$GRAFT_REPO_ROOT
