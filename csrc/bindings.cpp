@@ -320,9 +320,19 @@ Tensor act_bwd(Tensor dy, Tensor y, Tensor dbias) {
 }
 
 // -------------------------------------------------------------------------------- BN
+static uint8_t* ymask_ptr(const c10::optional<Tensor>& m, const Tensor& like) {
+  if (!m || !m->defined() || m->numel() == 0) return nullptr;
+  TORCH_CHECK(m->scalar_type() == torch::kUInt8 && m->is_contiguous() && m->numel() == like.numel() / 8 &&
+                  m->device() == like.device(),
+              "bn: ReLU mask must be contiguous uint8 [numel / 8] on the activation's device");
+  return m->data_ptr<uint8_t>();
+}
+
+// mask (optional, uint8 [numel / 8]): receives the ReLU bit mask of y (bit j of byte i =
+// element 8 i + j > 0) for bn_bwd(ymask=...), which then never reads y
 std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
                                  Tensor rvar, double momentum, double eps, Tensor res, bool relu,
-                                 c10::optional<Tensor> counter) {
+                                 c10::optional<Tensor> counter, c10::optional<Tensor> mask) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
@@ -343,7 +353,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
                     mean.data_ptr<float>(), rstd.data_ptr<float>(),
                     (counter && counter->defined() && counter->numel() == 1)
                         ? counter->data_ptr<int64_t>() : nullptr,
-                    cur_stream());
+                    cur_stream(), ymask_ptr(mask, x));
   return {y, mean, rstd};
 }
 
@@ -362,7 +372,7 @@ Tensor bn_fwd_eval(Tensor x, Tensor gamma, Tensor beta, Tensor rmean, Tensor rva
 
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd, Tensor gamma,
                            Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g,
-                           c10::optional<Tensor> zmask_beta) {
+                           c10::optional<Tensor> zmask_beta, c10::optional<Tensor> ymask) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
@@ -377,7 +387,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   if (has(zb)) TORCH_CHECK(zb.numel() == C, "bn_bwd: zmask beta size");
   mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
               fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr, want_g ? bpm(gout) : nullptr,
-              ws.data_ptr<float>(), cur_stream(), fopt(zb));
+              ws.data_ptr<float>(), cur_stream(), fopt(zb), ymask_ptr(ymask, x));
   return {dx, gout};
 }
 
@@ -825,11 +835,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("act_bwd", &act_bwd);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
-        py::arg("res"), py::arg("relu"), py::arg("counter") = py::none());
+        py::arg("res"), py::arg("relu"), py::arg("counter") = py::none(),
+        py::arg("mask") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
-        py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none());
+        py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none(),
+        py::arg("ymask") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("comm_emulator", &comm_emulator, "diagnostics: occupy CUs like a concurrent collective");
   m.def("atomic_latency", &atomic_latency, "diagnostics: dependent atomic round trips");

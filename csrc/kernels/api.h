@@ -147,7 +147,8 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
-                  int64_t* counter, hipStream_t s);  // counter (num_batches_tracked) += 1
+                  int64_t* counter, hipStream_t s,  // counter (num_batches_tracked) += 1
+                  uint8_t* ymask = nullptr);  // optional ReLU bit mask of y ([M*C/8] bytes)
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s);
@@ -156,7 +157,8 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s,
-            const float* zmask_beta = nullptr);
+            const float* zmask_beta = nullptr,
+            const uint8_t* ymask = nullptr);  // bit mask from bn_fwd_train, used instead of y
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);

@@ -52,6 +52,14 @@ static int bn_unr() {
   }();
   return v;
 }
+// as BN_LAUNCH, for kernels with a second (bool) template parameter
+#define BN_LAUNCH_T(kern, T, grid, ...)                                                   \
+  do {                                                                                    \
+    const int u_ = bn_unr();                                                              \
+    if (u_ == 4) hipLaunchKernelGGL((kern<4, T>), grid, dim3(256), 0, __VA_ARGS__);       \
+    else if (u_ == 2) hipLaunchKernelGGL((kern<2, T>), grid, dim3(256), 0, __VA_ARGS__);  \
+    else hipLaunchKernelGGL((kern<1, T>), grid, dim3(256), 0, __VA_ARGS__);               \
+  } while (0)
 #define BN_LAUNCH(kern, grid, ...)                                                        \
   do {                                                                                    \
     const int u_ = bn_unr();                                                              \
@@ -185,13 +193,28 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   }
 }
 
-// y = relu?(x * sc + sh (+ res)) over this thread's rows
-template <int UNR>
+// bit j = (bf16 element j of the 16-B vector > 0): the ReLU mask of a stored output
+__device__ __forceinline__ uint32_t posmask8(uint4 p) {
+  const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t lo = w[i] & 0xffffu, hi = w[i] >> 16;
+    m |= (uint32_t)(lo - 1u < 0x7fffu) << (2 * i);  // 1 .. 0x7fff: positive
+    m |= (uint32_t)(hi - 1u < 0x7fffu) << (2 * i + 1);
+  }
+  return m;
+}
+
+// y = relu?(x * sc + sh (+ res)) over this thread's rows; ym (optional): the ReLU mask of y,
+// one bit per element (byte r * C/8 + c0/8), which the backward reads instead of y
+template <int UNR, bool YM = false>
 __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, int c0,
                                               const float* sc, const float* sh,
                                               const bf16_t* __restrict__ x,
                                               const bf16_t* __restrict__ res, int relu,
-                                              bf16_t* __restrict__ y) {
+                                              bf16_t* __restrict__ y,
+                                              uint8_t* __restrict__ ym = nullptr) {
   sweep_rows_pl<UNR, 2>(
       cm, M,
       [&](int r, uint4 (&v)[2]) {
@@ -214,18 +237,20 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
-        *(uint4*)(y + (size_t)r * C + c0) = pack8(f);
+        const uint4 pk = pack8(f);
+        *(uint4*)(y + (size_t)r * C + c0) = pk;
+        if constexpr (YM) ym[(size_t)r * (C / 8) + c0 / 8] = (uint8_t)posmask8(pk);
       });
 }
 
 // ------------------------------------------------------------------- forward (train)
-template <int UNR>
+template <int UNR, bool YM>
 __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter) {
+    unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
@@ -246,7 +271,7 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
       rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
     }
   }
-  bn_apply_rows<UNR>(cm, M, C, c0, sc, sh, x, res, relu, y);
+  bn_apply_rows<UNR, YM>(cm, M, C, c0, sc, sh, x, res, relu, y, ymask);
 }
 
 // -------------------------------------------------------------------- forward (eval)
@@ -286,13 +311,17 @@ __device__ __forceinline__ bool bn_relu_live(float x, float sc, float sh) {
   return bf2f(f2bf(__builtin_fmaf(x, sc, sh))) > 0.f;
 }
 
-// zmask (beta != null, y == null): ReLU mask from x via bn_relu_live
+// ReLU mask, in order of preference: ym (bit mask written by the forward), zmask (beta !=
+// null, y == null: recomputed from x via bn_relu_live), y (the stored output).  (Here ym is
+// a runtime pointer: the compile-time variant scheduled the byte load between the row
+// loads and waited for each - 117 vs 78 us on layer1; the apply pass is the other way
+// round, see there.)
 template <int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, int M, int C,
-    float* __restrict__ slab, float* __restrict__ sums) {
+    float* __restrict__ slab, float* __restrict__ sums, const uint8_t* __restrict__ ym) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float sg[8], sgx[8];
@@ -307,17 +336,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     float mu[8], rs[8], msc[8], msh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
-    const bool zmask = !y && beta;
+    const bool zmask = !ym && !y && beta;
     if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
     sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
       uint4 dv[UNR], xr[UNR], yr[UNR];
+      uint32_t mb[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         if (u < n) {
           const size_t off = (size_t)(r + u * st) * C + c0;
           dv[u] = *(const uint4*)(dy + off);
           xr[u] = *(const uint4*)(x + off);
-          if (y) yr[u] = *(const uint4*)(y + off);
+          if (ym) mb[u] = ym[off / 8];
+          else if (y) yr[u] = *(const uint4*)(y + off);
         }
       }
 #pragma unroll
@@ -326,7 +357,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         float g[8], xv[8];
         unpack8(dv[u], g);
         unpack8(xr[u], xv);
-        if (y) {
+        if (ym) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = (mb[u] >> j) & 1u ? g[j] : 0.f;
+        } else if (y) {
           float yv[8];
           unpack8(yr[u], yv);
 #pragma unroll
@@ -355,14 +389,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 }
 
 // pass 2: dx = a*g + b + c*x ; optionally write g (residual-branch gradient); block 0
-// folds the sums into dgamma/dbeta.
-template <int UNR>
+// folds the sums into dgamma/dbeta.  YM (mask from bn_fwd_train) is a template parameter:
+// a runtime mask pointer slowed every variant of this pass by 10-40 % (its row loads no
+// longer stayed in flight).
+template <int UNR, bool YM>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ ws,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int M, int C,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ gout) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ gout, const uint8_t* __restrict__ ym) {
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -382,7 +418,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
   }
   if (!dx && !gout) return;
-  const bool zmask = !y && beta;
+  const bool zmask = !YM && !y && beta;
   float msc[8], msh[8];
   if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
   const bool need_x = dx || zmask;
@@ -391,14 +427,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       [&](int r, uint4 (&v)[3]) {
         const size_t off = (size_t)r * C + c0;
         v[0] = *(const uint4*)(dy + off);
-        if (y) v[2] = *(const uint4*)(y + off);
+        if constexpr (YM) v[2].x = ym[off / 8];
+        else if (y) v[2] = *(const uint4*)(y + off);
         if (need_x) v[1] = *(const uint4*)(x + off);
       },
       [&](int r, uint4 (&v)[3]) {
         const size_t off = (size_t)r * C + c0;
         float g[8];
         unpack8(v[0], g);
-        if (y) {
+        if constexpr (YM) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = (v[2].x >> j) & 1u ? g[j] : 0.f;
+          if (gout) *(uint4*)(gout + off) = pack8(g);
+        } else if (y) {
           float yv[8];
           unpack8(v[2], yv);
 #pragma unroll
@@ -1069,10 +1110,13 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
-                  int64_t* counter, hipStream_t s) {
-  BN_LAUNCH(bn_fwd_train_kernel, grid_for(M, C), s, x, stats, gamma,
-                     beta, rmean, rvar, momentum, eps, res, relu, M, C, y, mean, rstd,
-                     (unsigned long long*)counter);
+                  int64_t* counter, hipStream_t s, uint8_t* ymask) {
+  if (ymask)
+    BN_LAUNCH_T(bn_fwd_train_kernel, true, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
+                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask);
+  else
+    BN_LAUNCH_T(bn_fwd_train_kernel, false, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
+                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask);
 }
 
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
@@ -1084,15 +1128,21 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
-            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta) {
+            bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta,
+            const uint8_t* ymask) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials
   const dim3 gr = grid_for(M, C);
   float* slab = ws + 2 * C;
-  const float* zb = y ? nullptr : zmask_beta;
-  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws);
+  const float* zb = (y || ymask) ? nullptr : zmask_beta;
+  if (ymask) y = nullptr;
+  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws, ymask);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
-  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd,
-                     gamma, zb, ws, dgamma, dbeta, M, C, dx, g);
+  if (ymask)
+    BN_LAUNCH_T(bn_bwd_apply_kernel, true, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb, ws,
+                dgamma, dbeta, M, C, dx, g, ymask);
+  else
+    BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb,
+                ws, dgamma, dbeta, M, C, dx, g, ymask);
 }
 
 // apply pass only, with the reduction sums [sum g | sum g*xhat] already in `sums` (e.g.
@@ -1100,8 +1150,8 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s) {
-  BN_LAUNCH(bn_bwd_apply_kernel, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
-            (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g);
+  BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
+              (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,

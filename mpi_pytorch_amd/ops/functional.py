@@ -34,6 +34,8 @@ _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
 _NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
 _NO_ZSEL = os.environ.get("MPA_NO_ZSEL", "0") == "1"  # A/B: stem backward reduce from full z
+# A/B: residual blocks' backward reads y for the ReLU mask instead of a 1-bit-per-element mask
+_NO_YMASK = os.environ.get("MPA_NO_YMASK", "0") == "1"
 
 
 def K(t: torch.Tensor):
@@ -170,16 +172,22 @@ class _ConvBNAct(torch.autograd.Function):
         # BN statistics come out of the conv epilogue, shifted by the running mean
         z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
                        _empty(x) if _NO_SHIFT else bn.running_mean)
+        # relu(bn(z) + residual): the backward's ReLU mask as one bit per element, written by
+        # the forward, so neither backward pass reads y (two activation-sized reads less)
+        ymask = None
+        if relu and residual is not None and not _NO_YMASK:
+            ymask = torch.empty(z.numel() // 8, device=z.device, dtype=torch.uint8)
         y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
                                        bn.momentum_value(), bn.eps,
-                                       _or_empty(residual, x), relu, bn.num_batches_tracked)
+                                       _or_empty(residual, x), relu, bn.num_batches_tracked,
+                                       mask=ymask)
         ctx.conv = conv
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.bias = b
         ctx.params = (w, gamma, beta)
         ctx.in_hw = (x.shape[1], x.shape[2])
-        ctx.save_for_backward(x, z, y if relu else None, mean, rstd)
+        ctx.save_for_backward(x, z, y if (relu and ymask is None) else None, mean, rstd, ymask)
         ctx.link_in = link_in
         ctx.link_out = link_out
         ctx.join_x = join_x
@@ -191,7 +199,7 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, z, y, mean, rstd = ctx.saved_tensors
+        x, z, y, mean, rstd, ymask = ctx.saved_tensors
         w, gamma, beta = ctx.params
         conv = ctx.conv
         k = K(dy)
@@ -209,7 +217,7 @@ class _ConvBNAct(torch.autograd.Function):
                              _sink(beta, dy), True, want_g, beta)
         else:
             dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
-                             _sink(beta, dy), True, want_g)
+                             _sink(beta, dy), True, want_g, ymask=ymask)
         _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:

@@ -96,8 +96,21 @@ def act_bwd(dy, y, dbias):
 
 
 # ------------------------------------------------------------------------------------ BN
+def relu_bitmask(y):
+    """uint8 [numel / 8]: bit j of byte i = (element 8 i + j of y, flattened) > 0."""
+    b = (y.reshape(-1, 8) > 0).to(torch.int32)
+    w = torch.tensor([1 << j for j in range(8)], dtype=torch.int32, device=y.device)
+    return (b * w).sum(1).to(torch.uint8)
+
+
+def bitmask_unpack(m, shape):
+    """Inverse of relu_bitmask: bool tensor of ``shape``."""
+    bits = torch.arange(8, device=m.device, dtype=torch.int32)
+    return ((m.to(torch.int32).unsqueeze(1) >> bits) & 1).bool().reshape(shape)
+
+
 def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu,
-                 counter=None):
+                 counter=None, mask=None):
     # the oracle always uses exact two-pass statistics (``stats`` from a fused producer
     # epilogue is accepted for API parity but not needed)
     C = x.shape[-1]
@@ -117,7 +130,10 @@ def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, re
         rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
         if _opt(counter) is not None:
             counter.add_(1)
-    return y.reshape(x.shape).to(x.dtype), mean.contiguous(), rstd.contiguous()
+    y = y.reshape(x.shape).to(x.dtype)
+    if _opt(mask) is not None:
+        mask.copy_(relu_bitmask(y))
+    return y, mean.contiguous(), rstd.contiguous()
 
 
 def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
@@ -132,12 +148,16 @@ def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
     return y.reshape(x.shape).to(x.dtype)
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zmask_beta=None):
-    """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient).  With
-    ``zmask_beta`` and no ``y`` the mask of y = relu(bn(x)) is recomputed from x."""
+def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zmask_beta=None,
+           ymask=None):
+    """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient).  The mask
+    comes from ``ymask`` (bn_fwd_train's bit mask) if given, else from ``y``, else - with
+    ``zmask_beta`` - is recomputed from x for y = relu(bn(x))."""
     C = x.shape[-1]
     g = _f(dy).reshape(-1, C)
-    if _opt(y) is not None:
+    if _opt(ymask) is not None:
+        g = g * bitmask_unpack(ymask, g.shape)
+    elif _opt(y) is not None:
         g = g * (_f(y).reshape(-1, C) > 0)
     elif _opt(zmask_beta) is not None:
         sc = gamma * rstd

@@ -558,6 +558,32 @@ def test_bn_bwd_mask_from_z(gpu, M, Cc):
     assert torch.equal(dg, dg2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,Cc", [(4096, 64), (1003, 24)])
+def test_bn_relu_bitmask(gpu, M, Cc):
+    """relu(bn(z) + res): the forward's 1-bit ReLU mask equals (y > 0) packed 8 per byte, and
+    the backward from the mask == the backward from y, bit for bit (residual blocks)."""
+    torch.manual_seed(15)
+    x = (bf(M, Cc, dev=gpu, scale=2.0) + 0.3).to(torch.bfloat16)
+    r = bf(M, Cc, dev=gpu)
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu)
+    e = torch.empty(0, device=gpu)
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    mask = torch.empty(M * Cc // 8, dtype=torch.uint8, device=gpu)
+    y, mean, rstd = C().bn_fwd_train(x, e, g, b, rm, rv, 0.1, 1e-5, r, True, e, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(mask, ref.relu_bitmask(y))
+    assert torch.equal(ref.bitmask_unpack(mask, y.shape), y > 0)
+    dy = bf(M, Cc, dev=gpu)
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    dx, gg = C().bn_bwd(dy, x, y, mean, rstd, g, dg, db, True, True)
+    dxm, ggm = C().bn_bwd(dy, x, e, mean, rstd, g, dg2, db2, True, True, None, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(gg, ggm) and torch.equal(dx, dxm)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+
+
 def test_bn_stats_from_conv(gpu):
     """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
     torch.manual_seed(5)

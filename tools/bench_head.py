@@ -69,3 +69,17 @@ for bm, bn in ((128, 128), (256, 128), (256, 64), (128, 64), (256, 256)):
         cells.append("s%d %7.1f" % (sp, timeit(lambda: C.linear_fwd(x, w, b, False))))
     print("%3dx%-3d " % (bm, bn) + " | ".join(cells))
 C.igemm_force_tile(0, 0, 0)
+
+# vendor GEMMs (hipBLASLt through torch) on the same shapes, for comparison
+print("vendor (torch / hipBLASLt):")
+vrows = [("F.linear fwd", lambda: torch.nn.functional.linear(x, w, b.to(torch.bfloat16))),
+         ("mm dgrad", lambda: torch.mm(dy, w))]
+try:
+    torch.mm(dy.t(), x, out_dtype=torch.float32)
+    vrows.append(("mm wgrad fp32", lambda: torch.mm(dy.t(), x, out_dtype=torch.float32)))
+except Exception as ex:  # no bf16 -> fp32 mm on this build
+    print("  mm(out_dtype=float32) unavailable: %s" % str(ex)[:80])
+vrows.append(("mm wgrad bf16", lambda: torch.mm(dy.t(), x)))
+for name, fn in vrows:
+    t = timeit(fn)
+    print("%-14s %8.1f us  %6.0f TF" % (name, t, gflop / t * 1e-3 * 1e3))
