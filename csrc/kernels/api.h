@@ -2,6 +2,7 @@
 // structs, no torch headers: the .hip translation units compile in seconds and the
 // torch-facing binding layer (csrc/bindings.cpp) validates shapes and allocates.
 #pragma once
+#include <algorithm>
 #include <string>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,9 +23,23 @@ struct Taps {
 // and its tile count.  Tile g of the launch belongs to phase g % nphase (phases interleaved
 // so every XCD's contiguous share of the tile list holds an equal mix of long and short
 // phases), local tile g / nphase; phases are padded to the longest tile count.
+// n / d for 0 <= n < 2^31 as one multiply-high and a shift (Granlund-Montgomery: m =
+// ceil(2^(31 + l) / d), l = ceil(log2 d)); m == 0 encodes d == 1.  The rows kernels split
+// a pixel index into (image, row, column) with these instead of two 32-bit integer divisions
+// (~40 VALU each) per row in the prologue and again in the epilogue.
+struct FastDiv {
+  uint32_t m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  if (d <= 1) return FastDiv{0u, 0u};
+  const uint32_t l = 32u - (uint32_t)__builtin_clz(d - 1u);
+  return FastDiv{(uint32_t)(((1ull << (31 + l)) + d - 1) / d), l - 1u};
+}
+
 constexpr int MAXPH = 16;
 struct PhaseDesc {
   int M, oH, oW, Ktot, tap0, T, Poh, Pow, tiles;
+  FastDiv fd_hw, fd_ow;  // oH * oW, oW (set by the launchers: igemm_set_fastdiv)
 };
 
 // implicit GEMM whose rows are pixels of a gathered NHWC tensor (conv fwd / dgrad / linear)
@@ -70,7 +85,18 @@ struct IGemmArgs {
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
   int beta;               // 1: accumulate, C = acc + C (bf16 read-add-write, one rounding):
                           // a second gradient contribution lands in the first one's buffer
+  FastDiv fd_hw, fd_ow;   // oH * oW, oW (igemm_set_fastdiv, right before a launch)
 };
+
+// fill the FastDiv fields of a rows launch (and of its stride phases)
+inline void igemm_set_fastdiv(IGemmArgs& a) {
+  a.fd_hw = make_fastdiv((uint32_t)std::max(1, a.oH * a.oW));
+  a.fd_ow = make_fastdiv((uint32_t)std::max(1, a.oW));
+  for (int i = 0; i < a.nphase && i < MAXPH; ++i) {
+    a.ph[i].fd_hw = make_fastdiv((uint32_t)std::max(1, a.ph[i].oH * a.ph[i].oW));
+    a.ph[i].fd_ow = make_fastdiv((uint32_t)std::max(1, a.ph[i].oW));
+  }
+}
 
 struct WGradArgs {
   const bf16_raw* dy;

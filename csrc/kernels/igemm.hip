@@ -74,9 +74,9 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
     const int m = m0 + (tid >> 2) + 64 * i;
     if (m < p.M) {
       const int hw = p.oH * p.oW;
-      const int img = m / hw;
+      const int img = (int)fdiv((uint32_t)m, p.fd_hw);
       const int r = m - img * hw;
-      const int oh = r / p.oW;
+      const int oh = (int)fdiv((uint32_t)r, p.fd_ow);
       const int ow = r - oh * p.oW;
       a_img[i] = img * p.aH * p.aW;
       a_bh[i] = oh * p.Uh + p.Oh;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
     }
   }
   rows_epilogue<BM, BN, WM, WN, SPLIT>(p, acc, smem, mt, m0, n0, wm, wrow0, wcol0, tid,
-                                       RowsGeom{p.M, p.oH, p.oW, p.Poh, p.Pow});
+                                       RowsGeom{p.M, p.oH, p.oW, p.Poh, p.Pow, p.fd_hw, p.fd_ow});
 }
 
 // ======================================================================================
@@ -623,7 +623,9 @@ std::string igemm_tuned_table() {
 }
 
 template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
-static void launch_rows(const IGemmArgs& a, int splits, hipStream_t s) {
+static void launch_rows(const IGemmArgs& a0, int splits, hipStream_t s) {
+  IGemmArgs a = a0;
+  igemm_set_fastdiv(a);
   dim3 grid(a.tiles_total, 1, splits);
   const int o = occ_target();
   if (o == 4)

@@ -168,7 +168,12 @@ __device__ __forceinline__ int nvalid(int idx, int lim) {
 // output-row geometry of the rows engine (per stride phase in a merged dgrad launch)
 struct RowsGeom {
   int M, oH, oW, Poh, Pow;
+  FastDiv fd_hw, fd_ow;
 };
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return f.m ? (__umulhi(n, f.m) >> f.s) : n;
+}
 
 template <int BM, int BN, int WM, int WN, bool SPLIT>
 __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
@@ -234,9 +239,9 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
       orows[i] = 0;
       if (moks[i]) {
         const int hw = g.oH * g.oW;
-        const int img = m / hw;
+        const int img = (int)fdiv((uint32_t)m, g.fd_hw);
         const int rr = m - img * hw;
-        const int oh = rr / g.oW;
+        const int oh = (int)fdiv((uint32_t)rr, g.fd_ow);
         const int ow = rr - oh * g.oW;
         orows[i] = ((size_t)img * p.dH * p.dW + (size_t)(oh * p.Uoh + g.Poh) * p.dW +
                     (ow * p.Uow + g.Pow)) * p.ldc;

@@ -90,7 +90,7 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
 
   int tile = xcd_remap(blockIdx.x, p.tiles_total);
   // merged stride-phase launch: the block's phase sets output geometry, K and taps
-  RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow};
+  RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow, p.fd_hw, p.fd_ow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
   int row_base = 0;  // statistics-slab row of m-tile 0 of this block's phase (dense rows)
   if constexpr (PH) {
@@ -99,7 +99,7 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
     const PhaseDesc& d = p.ph[ph];
     if (tile >= d.tiles) return;  // padding tile of a shorter phase (whole block)
     for (int q = 0; q < ph; ++q) row_base += p.ph[q].tiles / p.tiles_n;
-    g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow};
+    g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow, d.fd_hw, d.fd_ow};
     Ktot = d.Ktot;
     T = d.T;
     tap0 = d.tap0;
@@ -127,9 +127,9 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
     const int m = m0 + 16 * (wave * IAW + i) + (lane >> 2);
     if (m < g.M) {
       const int hw = g.oH * g.oW;
-      const int img = m / hw;
+      const int img = (int)fdiv((uint32_t)m, g.fd_hw);
       const int r = m - img * hw;
-      const int oh = r / g.oW;
+      const int oh = (int)fdiv((uint32_t)r, g.fd_ow);
       a_img[i] = img * p.aH * p.aW;
       a_bh[i] = oh * p.Uh + p.Oh;
       a_bw[i] = (r - oh * g.oW) * p.Uw + p.Ow;
@@ -286,7 +286,7 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const int wm = wave / WN, wn = wave % WN;
 
   int tile = xcd_remap(blockIdx.x, p.tiles_total);
-  RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow};
+  RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow, p.fd_hw, p.fd_ow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
   int row_base = 0;  // statistics-slab row of m-tile 0 of this block's phase (dense rows)
   if constexpr (PH) {
@@ -295,7 +295,7 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     const PhaseDesc& d = p.ph[ph];
     if (tile >= d.tiles) return;
     for (int q = 0; q < ph; ++q) row_base += p.ph[q].tiles / p.tiles_n;
-    g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow};
+    g = RowsGeom{d.M, d.oH, d.oW, d.Poh, d.Pow, d.fd_hw, d.fd_ow};
     Ktot = d.Ktot;
     T = d.T;
     tap0 = d.tap0;
@@ -335,9 +335,9 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   for (int i = 0; i < IAW; ++i) {
     const int m = min(m0 + 16 * (wave * IAW + i) + (lane >> 2), g.M - 1);
     const int hw = g.oH * g.oW;
-    const int img = m / hw;
+    const int img = (int)fdiv((uint32_t)m, g.fd_hw);
     const int r = m - img * hw;
-    const int oh = r / g.oW;
+    const int oh = (int)fdiv((uint32_t)r, g.fd_ow);
     a_bh[i] = oh * p.Uh + p.Oh;
     a_bw[i] = (r - oh * g.oW) * p.Uw + p.Ow;
     // (may be "negative" for a padded origin; the valid taps bring it back in range)
@@ -749,7 +749,9 @@ static bool rows_uni_fits(const IGemmArgs& a, bool bkc) {
 }
 
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
-static void launch_rows_dma_v(const IGemmArgs& a, dim3 grid, hipStream_t s) {
+static void launch_rows_dma_v(const IGemmArgs& a0, dim3 grid, hipStream_t s) {
+  IGemmArgs a = a0;
+  igemm_set_fastdiv(a);
   if ((a.aC % BK == 0 || a.stap) && g_dma_uni && rows_uni_fits(a, BKC))
     hipLaunchKernelGGL((igemm_rows_dma_uni_kernel<BM, BN, WM, WN, BKC, SPLIT, PH>), grid,
                        dim3(WM * WN * 64), 0, s, a);
