@@ -207,6 +207,8 @@ HALO_CASES = [
     (2, 35, 35, 64, 96),     # Inception-style odd spatial size
     (2, 35, 35, 64, 128),    # halo wgrad at pitch 48
     (3, 17, 17, 128, 64),    # halo wgrad at pitch 32, odd W, tiles across images
+    (52, 14, 14, 256, 512),  # 320 tiles on 256 persistent blocks (two rounds), ragged last tile
+    (25, 56, 56, 64, 64),    # resident weights, 307 tiles
 ]
 
 
@@ -222,24 +224,29 @@ def _halo_pair(fn):
 
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_fwd(gpu, case):
-    """Halo-staged 3x3/s1 forward (bias, ReLU, shifted BN statistics) == implicit GEMM and
-    the fp32 oracle."""
+    """Halo-staged 3x3/s1 forward == implicit GEMM and the fp32 oracle, in the flavours the
+    halo kernel instantiates: shifted BN statistics (the training path), bias + ReLU, and
+    bias + statistics (bias + ReLU + statistics falls back to the implicit GEMM)."""
     torch.manual_seed(21)
     N, H, W, Cc, K = case
     x = bf(N, H, W, Cc, dev=gpu)
     w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * Cc))
     b = torch.randn(K, device=gpu)
+    e = torch.empty(0, device=gpu)
     shift = torch.randn(K, device=gpu) * 0.1
+    for bias, relu, stats in ((e, False, True), (b, True, False), (b, False, True),
+                              (b, True, True)):
 
-    def run():
-        st = torch.zeros(2, K, device=gpu)
-        return C().conv_fwd(x, w, b, 1, 1, 1, 1, True, st, shift), st
+        def run():
+            st = torch.zeros(2, K, device=gpu) if stats else e
+            return C().conv_fwd(x, w, bias, 1, 1, 1, 1, relu, st, shift if stats else e), st
 
-    (y, st), (y0, st0) = _halo_pair(run)
-    str_ = torch.zeros(2, K, device=gpu)
-    yr = ref.conv_fwd(x, w, b, 1, 1, 1, 1, True, str_, shift)
-    assert rel(y, y0) < 1e-2 and rel(st, st0) < 1e-3
-    assert rel(y, yr) < 2e-2 and rel(st, str_) < 2e-2
+        (y, st), (y0, st0) = _halo_pair(run)
+        str_ = torch.zeros(2, K, device=gpu) if stats else e
+        yr = ref.conv_fwd(x, w, bias, 1, 1, 1, 1, relu, str_, shift if stats else e)
+        assert rel(y, y0) < 1e-2 and rel(y, yr) < 2e-2
+        if stats:
+            assert rel(st, st0) < 1e-3 and rel(st, str_) < 2e-2
 
 
 @pytest.mark.parametrize("case", HALO_CASES)
