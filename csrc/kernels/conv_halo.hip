@@ -51,7 +51,8 @@ constexpr int HB_HBYTES = HB_HPX * 64;          // 36 KiB
 constexpr int HB_WIW = 9;                       // weight DMA instructions per wave per chunk
 constexpr int HB_WBYTES = 9 * HB_BN * 64;       // 36 KiB: [tap][64 cols][32 k]
 constexpr int HB_RED = HB_NW * HB_BN * 2 * 4;   // epilogue cross-wave statistics
-constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED;  // 149,504 B
+constexpr int HB_COLS = 2 * HB_BN * 4;          // per-column epilogue operands [2][64]
+constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED + HB_COLS;  // 150,016 B
 
 struct HaloPlan {
   int w2;               // halo row pitch P: W + 1 (one shared zero column) rounded up to 8
@@ -210,16 +211,18 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
   }
 }
 
-template <bool WRES, int EPI, bool FULL>
-__global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
-  constexpr int HB_DPT = WRES ? 2 : 4;  // next-item DMAs per tap
+template <bool WRES, int EPI, bool FULL, bool PROD>
+__global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
+  constexpr int HB_DPT = WRES ? 2 : 4;  // next-item DMAs per tap (no producer waves)
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
   char* const hal = smem;
   char* const wst = smem + 2 * HB_HBYTES;
   char* const red = smem + 2 * HB_HBYTES + 2 * HB_WBYTES;
+  float* const cst = (float*)(red + HB_RED);  // [2][64] per-column epilogue operands
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = wave_all & (HB_NW - 1);  // MFMA wave / DMA lane group
   const int H = p.aH, W = p.aW, HW = H * W, W2 = h.w2, aC = p.aC;
   const int nimg = p.M / HW;
   const int jq = lane >> 4, l15 = lane & 15;
@@ -234,95 +237,119 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   const int nitems = ntiles * CC;
   const int nt = (tbeg + loc) % p.tiles_n;
   const int n0 = nt * HB_BN;
+  auto tile_of = [&](int tk) { return tbeg + loc + tk * G8; };
+  auto m0_of = [&](int tk) { return (tile_of(tk) / p.tiles_n) * HB_BM; };
+
+  // ---- staging: the DMA lanes of lane group `wave` and the instructions of one item
+  auto stager = [&](auto body) {
+    // halo lanes: tile-independent (slot, column, logical chunk) of each DMA lane
+    uint32_t hsc[HB_HIW];  // slot | (col + 1) << 10 | chunk << 18
+#pragma unroll
+    for (int j = 0; j < HB_HIW; ++j) {
+      const uint32_t hp = 16 * (wave * HB_HIW + j) + (lane >> 2);
+      const uint32_t s = udiv(hp, h.mag_w2);
+      const uint32_t colp = hp - s * W2;
+      const uint32_t lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
+      hsc[j] = s | (colp << 10) | (lc << 18);
+    }
+    // weight lanes: row r = 16 q + lane/4 of the [tap][64][32] image, tap = q / 4; the
+    // block's column tile is fixed, so the offsets are too
+    uint32_t wv[HB_WIW];
+#pragma unroll
+    for (int j = 0; j < HB_WIW; ++j) {
+      const int q = wave * HB_WIW + j;
+      const int r = 16 * q + (lane >> 2);
+      const int n = r & 63;
+      const int lc = (lane & 3) ^ (((r >> 2) & 1) << 1);
+      wv[j] = (n0 + n < p.N) ? (uint32_t)(n0 + n) * p.ldb * 2 + h.btoff[q >> 2] + lc * 16
+                             : 0x80000000u;
+    }
+    uint32_t hv[HB_HIW];
+    auto prep_tile = [&](int tk) {  // DMA source offsets of a tile's halo
+      const int m0 = m0_of(tk);
+      const int img0 = m0 / HW;
+      const int oh0 = (m0 - img0 * HW) / W;
+#pragma unroll
+      for (int j = 0; j < HB_HIW; ++j) {
+        const int s = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
+        const int v = s + oh0 - 1;                                     // >= -1
+        const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;  // floor(v / (H+1))
+        const int row = v - d * (H + 1);
+        const int img = img0 + d;
+        const bool ok = row < H && (unsigned)col < (unsigned)W && img < nimg;
+        hv[j] = ok ? ((((uint32_t)img * H + row) * W + col) * aC) * 2 + (hsc[j] >> 18) * 16
+                   : 0x80000000u;
+      }
+    };
+    // DMA instruction j (halo 0..8, then weights 9..17 unless resident) of item (cc, stage)
+    auto dma = [&](int cc, int stage, int j) {
+      if (j < HB_HIW) {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
+        buf_lds16(ra, hal + stage * HB_HBYTES + (wave * HB_HIW + j) * 1024, hv[j]);
+      } else if (!WRES && j < HB_HIW + HB_WIW) {
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+        buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j - HB_HIW) * 1024,
+                  wv[j - HB_HIW]);
+      }
+    };
+    auto issue = [&](int cc, int stage) {
+#pragma unroll
+      for (int j = 0; j < HB_HIW + HB_WIW; ++j) dma(cc, stage, j);
+    };
+    if (nitems > 0) {
+      if constexpr (WRES) {  // whole weight tile (tiles_n == 1, CC <= 2) once per block
+        for (int cc = 0; cc < CC; ++cc) {
+          const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+          char* wdst = wst + cc * HB_WBYTES + wave * HB_WIW * 1024;
+#pragma unroll
+          for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
+        }
+      }
+      prep_tile(0);
+      issue(0, 0);
+    }
+    body(prep_tile, dma, issue);
+  };
+
+  if constexpr (PROD) {
+    // Producer waves 4..7: all of the block's LDS-DMAs.  Item k's top barrier publishes
+    // stage k & 1 (every producer has waited for its DMAs) and frees stage (k + 1) & 1 (every
+    // MFMA wave is done with item k - 1), so item k + 1's DMAs go out right behind it and get
+    // the whole of item k to land.  The MFMA waves' instruction streams carry no DMA at all:
+    // issuing the 18 per item between the MFMAs cost those waves ~10 % (MPA_HALO_DBG=1 A/B,
+    // docs/KERNELS.md), waiting for them nothing measurable.  Barrier count per wave:
+    // nitems (+1 for the statistics flush) on both sides.
+    if (wave_all >= HB_NW) {
+      stager([&](auto& prep_tile, auto&, auto& issue) {
+        int cc1 = 0;
+        for (int k = 0; k < nitems; ++k) {
+          wait_all_barrier();
+          if (++cc1 == CC) cc1 = 0;
+          if (k + 1 < nitems) {
+            if (cc1 == 0) prep_tile((k + 1) / CC);
+            if (!h.dbg) issue(cc1, (k + 1) & 1);
+          }
+        }
+      });
+      if constexpr (EPI & (EP_STATS | EP_BNRED)) __syncthreads();  // halo_stats_flush's
+      return;
+    }
+  }
 
   // per-column epilogue operands of the block's 64 columns: bias (or BN mean) and stats
-  // shift (or BN rstd)
-  f32x4 colb[4], cols[4];
-  {
+  // shift (or BN rstd), parked in LDS rather than in 32 VGPRs held through every MFMA; the
+  // first item's barrier publishes them
+  if (tid < HB_BN) {
     const float* bsrc = (EPI & EP_BNRED) ? p.ep_mean : p.bias;
     const float* ssrc = (EPI & EP_BNRED) ? p.ep_rstd : p.stats_shift;
-#pragma unroll
-    for (int jn = 0; jn < 4; ++jn) {
-      const int n = n0 + jn * 16 + jq * 4;
-      colb[jn] = bsrc ? *(const f32x4*)(bsrc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      cols[jn] = ssrc ? *(const f32x4*)(ssrc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    cst[tid] = bsrc ? bsrc[n0 + tid] : 0.f;
+    cst[HB_BN + tid] = ssrc ? ssrc[n0 + tid] : 0.f;
   }
   float ss[4][4], sq[4][4];
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { ss[jn][r] = 0.f; sq[jn][r] = 0.f; }
-
-  // ---- halo lanes: tile-independent (slot, column, logical chunk) of each DMA lane
-  uint32_t hsc[HB_HIW];  // slot | (col + 1) << 10 | chunk << 18
-#pragma unroll
-  for (int j = 0; j < HB_HIW; ++j) {
-    const uint32_t hp = 16 * (wave * HB_HIW + j) + (lane >> 2);
-    const uint32_t s = udiv(hp, h.mag_w2);
-    const uint32_t colp = hp - s * W2;
-    const uint32_t lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
-    hsc[j] = s | (colp << 10) | (lc << 18);
-  }
-  // ---- weight lanes: row r = 16 q + lane/4 of the [tap][64][32] image, tap = q / 4; the
-  // block's column tile is fixed, so the offsets are too
-  uint32_t wv[HB_WIW];
-#pragma unroll
-  for (int j = 0; j < HB_WIW; ++j) {
-    const int q = wave * HB_WIW + j;
-    const int r = 16 * q + (lane >> 2);
-    const int n = r & 63;
-    const int lc = (lane & 3) ^ (((r >> 2) & 1) << 1);
-    wv[j] = (n0 + n < p.N) ? (uint32_t)(n0 + n) * p.ldb * 2 + h.btoff[q >> 2] + lc * 16
-                           : 0x80000000u;
-  }
-  uint32_t hv[HB_HIW];
-  auto tile_of = [&](int tk) { return tbeg + loc + tk * G8; };
-  auto m0_of = [&](int tk) { return (tile_of(tk) / p.tiles_n) * HB_BM; };
-  auto prep_tile = [&](int tk) {  // DMA source offsets of a tile's halo
-    const int m0 = m0_of(tk);
-    const int img0 = m0 / HW;
-    const int oh0 = (m0 - img0 * HW) / W;
-#pragma unroll
-    for (int j = 0; j < HB_HIW; ++j) {
-      const int s = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
-      const int v = s + oh0 - 1;                                     // >= -1
-      const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;  // floor(v / (H+1))
-      const int row = v - d * (H + 1);
-      const int img = img0 + d;
-      const bool ok = row < H && (unsigned)col < (unsigned)W && img < nimg;
-      hv[j] = ok ? ((((uint32_t)img * H + row) * W + col) * aC) * 2 + (hsc[j] >> 18) * 16
-                 : 0x80000000u;
-    }
-  };
-  // DMA instruction j (halo 0..8, then weights 9..17 unless resident) of item (cc, stage)
-  auto dma = [&](int cc, int stage, int j) {
-    if (j < HB_HIW) {
-      const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
-      buf_lds16(ra, hal + stage * HB_HBYTES + (wave * HB_HIW + j) * 1024, hv[j]);
-    } else if (!WRES && j < HB_HIW + HB_WIW) {
-      const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
-      buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j - HB_HIW) * 1024,
-                wv[j - HB_HIW]);
-    }
-  };
-  auto issue = [&](int cc, int stage) {
-#pragma unroll
-    for (int j = 0; j < HB_HIW + HB_WIW; ++j) dma(cc, stage, j);
-  };
-
-  if (nitems > 0) {
-    if constexpr (WRES) {  // whole weight tile (tiles_n == 1, CC <= 2) once per block
-      for (int cc = 0; cc < CC; ++cc) {
-        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
-        char* wdst = wst + cc * HB_WBYTES + wave * HB_WIW * 1024;
-#pragma unroll
-        for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
-      }
-    }
-    prep_tile(0);
-    issue(0, 0);
-  }
 
   // B fragment byte offsets (tap 0, column group 0): row l15 of the [tap][64][32] image
   const int boff = l15 * 64 + ((jq ^ ((l15 >> 1) & 2)) << 4);
@@ -339,16 +366,20 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     constexpr bool F = decltype(full)::value;
     const int m = m0e + wave * 64 + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
-    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb[jn],
-                     cols[jn], ss[jn], sq[jn]);
+    const f32x4 colb = *(const f32x4*)(cst + jn * 16 + jq * 4);
+    const f32x4 cols = *(const f32x4*)(cst + HB_BN + jn * 16 + jq * 4);
+    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb, cols,
+                     ss[jn], sq[jn]);
   };
 
   // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + 4 B fragments (the next
-  // tap's 8 reads in flight under this tap's 16 MFMAs) and two of the next item's 18
-  // LDS-DMAs in the MFMA shadow.  FIRST: the tile's first chunk (accumulators start at 0).
-  // (Measured: a row-major body that held the chunk's B fragments in registers and ran the
-  // previous tile's epilogue interleaved with the next tile's MFMAs was 10-15 % slower once
-  // the DMA issue moved into the MFMA stream and the A addresses were precomputed.)
+  // tap's 8 reads in flight under this tap's 16 MFMAs) and, without producer waves, four of
+  // the next item's LDS-DMAs in the MFMA shadow (front-loaded: all by tap 4, so the
+  // top-of-item wait finds them done).  FIRST: the tile's first chunk (accumulators start
+  // at 0).  (Measured: a row-major body that held the chunk's B fragments in registers and
+  // ran the previous tile's epilogue interleaved with the next tile's MFMAs was 10-15 %
+  // slower once the DMA issue moved into the MFMA stream and the A addresses were
+  // precomputed.)
   auto mma_chunk = [&](int st, int cc, auto first, auto nd) {
     constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HB_HBYTES;
@@ -371,10 +402,10 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
         for (int jn = 0; jn < 4; ++jn)
           acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
                               (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
-      // the next item's DMAs, front-loaded: its 18 (9 with resident weights) land by tap
-      // 4, so the top-of-item wait finds them done instead of waiting out the last ones
+      if constexpr (!PROD) {
 #pragma unroll
-      for (int d = 0; d < HB_DPT; ++d) nd(HB_DPT * t + d);
+        for (int d = 0; d < HB_DPT; ++d) nd(HB_DPT * t + d);
+      }
     }
   };
 
@@ -382,19 +413,27 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // (accumulate: old output; fused BN reduction: z, y) are loaded right after the top wait
   // of the tile's second-to-last item, so they are in flight under its MFMAs (a load issued
   // in front of a wait would be waited for with the DMAs).
-  auto run_tile = [&](int tk) {
+  auto run_tile = [&](int tk, auto& prep_tile, auto& dma) {
     const int m0 = m0_of(tk);
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       const int st = k & 1;
-      // this item's DMAs were issued during the previous item's MFMAs; the next item's
-      // are issued during this one's (stage st ^ 1 was freed by the previous barrier)
-      wait_all_barrier();
+      // this item's DMAs were issued during the previous item; the next item's are issued
+      // during this one's (stage st ^ 1 was freed by this barrier).  The MFMA waves of a
+      // producer block have no DMA of their own to wait for.
+      if constexpr (PROD) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+      } else {
+        wait_all_barrier();
+      }
       if (cc == max(CC - 2, 0)) epi_preload<EPI>(p, ein, m0, n0, wave, lane);
       const bool more = k + 1 < nitems;
       const int cc1 = cc + 1 == CC ? 0 : cc + 1;
-      if (more && cc1 == 0) prep_tile(tk + 1);
-      auto nd = [&](int j) {
+      if constexpr (!PROD) {
+        if (more && cc1 == 0) prep_tile(tk + 1);
+      }
+      auto nd = [&](auto j) {
         if (more && !h.dbg) dma(cc1, st ^ 1, j);
       };
       if (cc == 0) {
@@ -431,7 +470,15 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     }
   };
 
-  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk);
+  auto tiles = [&](auto& prep_tile, auto& dma) {
+    for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, prep_tile, dma);
+  };
+  if constexpr (PROD) {
+    int none = 0;
+    tiles(none, none);
+  } else {
+    stager([&](auto& prep_tile, auto& dma, auto&) { tiles(prep_tile, dma); });
+  }
   if (ntiles > 0) {
     const int m0l = m0_of(ntiles - 1);
 #pragma unroll
@@ -720,18 +767,39 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   return (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
 }
 
+// Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves) for every flavour whose
+// MFMA waves fit the 256 registers two waves per SIMD leave; the fused BN-backward
+// reduction holds z and y for the epilogue and keeps the 4-wave form.  MPA_HALO_PROD=0: off.
+static const bool g_halo_prod = [] {
+  const char* e = getenv("MPA_HALO_PROD");
+  return !(e && atoi(e) == 0);
+}();
+
+template <int EPI, bool PROD>
+static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
+                          hipStream_t s) {
+  const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
+  const dim3 blk(PROD ? 512 : 256);
+  if (wres && full)
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, PROD>), dim3(grid), blk, 0, s, a, h);
+  else if (wres)
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false, PROD>), dim3(grid), blk, 0, s, a, h);
+  else if (full)
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true, PROD>), dim3(grid), blk, 0, s, a, h);
+  else
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false, PROD>), dim3(grid), blk, 0, s, a,
+                       h);
+}
+
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
-  if (wres && full)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true>), dim3(grid), dim3(256), 0, s, a, h);
-  else if (wres)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false>), dim3(grid), dim3(256), 0, s, a, h);
-  else if (full)
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true>), dim3(grid), dim3(256), 0, s, a, h);
-  else
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false>), dim3(grid), dim3(256), 0, s, a, h);
+  if constexpr (EPI == EP_BNRED) {
+    launch_halo_k<EPI, false>(wres, grid, a, h, s);
+  } else {
+    if (g_halo_prod) launch_halo_k<EPI, true>(wres, grid, a, h, s);
+    else launch_halo_k<EPI, false>(wres, grid, a, h, s);
+  }
 }
 
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
