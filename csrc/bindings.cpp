@@ -125,7 +125,7 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
 // reduction of the ReLU(BN) that produced this conv's input (see igemm_rows_dgrad_bnred);
 // then dx = g (masked) and bnred->sums receives [sum g | sum g*xhat].
 struct BnRed {
-  Tensor z, y, mean, rstd, sums;
+  Tensor z, y, mean, rstd, sums, gamma, beta;
 };
 
 static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw,
@@ -194,6 +194,12 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
     a.ep_y = bopt(bnred->y);
     a.ep_mean = fopt(bnred->mean);
     a.ep_rstd = fopt(bnred->rstd);
+    a.ep_gamma = fopt(bnred->gamma);
+    a.ep_beta = fopt(bnred->beta);
+    TORCH_CHECK(a.ep_y, "conv_dgrad_bnred: needs y (the implicit GEMM's ReLU mask)");
+    TORCH_CHECK(!a.ep_gamma == !a.ep_beta, "conv_dgrad_bnred: gamma and beta go together");
+    for (const Tensor* t : {&bnred->mean, &bnred->rstd, &bnred->gamma, &bnred->beta})
+      TORCH_CHECK(!has(*t) || t->numel() == C, "conv_dgrad_bnred: per-channel vector size");
     bnred->sums = torch::empty({2 * C}, dy.options().dtype(torch::kFloat32));
     int k = 0;
     bool empty = false;
@@ -250,11 +256,12 @@ bool conv_bnred_ok(int64_t K, int64_t C) {
 
 std::vector<Tensor> conv_dgrad_bnred(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh,
                                      int64_t sw, int64_t ph, int64_t pw, Tensor wt, Tensor z,
-                                     Tensor y, Tensor mean, Tensor rstd) {
+                                     Tensor y, Tensor mean, Tensor rstd,
+                                     c10::optional<Tensor> gamma, c10::optional<Tensor> beta) {
   CHECK_ACT(z);
   TORCH_CHECK(conv_bnred_ok(w.size(0), w.size(3)), "conv_dgrad_bnred: unsupported shape/engine");
   TORCH_CHECK(wt.defined() && wt.numel() == w.numel(), "conv_dgrad_bnred: needs the transposed weight");
-  BnRed r{z, y, mean, rstd, Tensor()};
+  BnRed r{z, y, mean, rstd, Tensor(), gamma.value_or(Tensor()), beta.value_or(Tensor())};
   Tensor dx = conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt, &r);
   TORCH_CHECK(z.sizes() == dx.sizes(), "conv_dgrad_bnred: z must have dx's shape");
   return {dx, r.sums};
@@ -830,7 +837,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accum") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_bnred_ok", &conv_bnred_ok);
-  m.def("conv_dgrad_bnred", &conv_dgrad_bnred);
+  m.def("conv_dgrad_bnred", &conv_dgrad_bnred, py::arg("dy"), py::arg("w"), py::arg("H"),
+        py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt"),
+        py::arg("z"), py::arg("y"), py::arg("mean"), py::arg("rstd"),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("act_bwd", &act_bwd);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),

@@ -81,6 +81,11 @@ struct IGemmArgs {
   const bf16_raw* ep_y;
   const float* ep_mean;
   const float* ep_rstd;
+  // ep_gamma / ep_beta (optional): the 3x3/s1 halo kernel then recomputes the ReLU mask
+  // from z exactly as bn_fwd_train rounded y (bf16(fma(z, gamma*rstd, fma(-mean,
+  // gamma*rstd, beta))) > 0) and never reads y; the implicit GEMM always reads ep_y
+  const float* ep_gamma;
+  const float* ep_beta;
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
   int beta;               // 1: accumulate, C = acc + C (bf16 read-add-write, one rounding):

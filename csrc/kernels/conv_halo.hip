@@ -51,8 +51,8 @@ constexpr int HB_HBYTES = HB_HPX * 64;          // 36 KiB
 constexpr int HB_WIW = 9;                       // weight DMA instructions per wave per chunk
 constexpr int HB_WBYTES = 9 * HB_BN * 64;       // 36 KiB: [tap][64 cols][32 k]
 constexpr int HB_RED = HB_NW * HB_BN * 2 * 4;   // epilogue cross-wave statistics
-constexpr int HB_COLS = 2 * HB_BN * 4;          // per-column epilogue operands [2][64]
-constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED + HB_COLS;  // 150,016 B
+constexpr int HB_COLS = 4 * HB_BN * 4;          // per-column epilogue operands [4][64]
+constexpr int HB_LDS = 2 * HB_HBYTES + 2 * HB_WBYTES + HB_RED + HB_COLS;  // 150,528 B
 
 struct HaloPlan {
   int w2;               // halo row pitch P: W + 1 (one shared zero column) rounded up to 8
@@ -72,11 +72,11 @@ __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
 enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16 };
 
 // Per-tile operands the epilogue reads from memory (accumulate: the old output; fused
-// BN-backward reduction: z and y), loaded right after the tile's last MFMA chunk so they
-// are in registers long before the epilogue runs - a load issued behind the next item's
-// LDS-DMAs would make the in-order vmcnt wait for those DMAs too.
+// BN-backward reduction: z, whose ReLU mask is recomputed like bn_fwd_train rounded y, so
+// y is never read), loaded at the start of the tile's second-to-last item so they are in
+// registers long before the epilogue runs.
 struct EpiIn {
-  uint2 a[4][4], b[4][4];
+  uint2 a[4][4];
 };
 
 template <int EPI>
@@ -86,7 +86,7 @@ __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) in.a[i][jn] = in.b[i][jn] = make_uint2(0u, 0u);
+      for (int jn = 0; jn < 4; ++jn) in.a[i][jn] = make_uint2(0u, 0u);
   } else {
     const int nl = (lane >> 4) * 4;
 #pragma unroll
@@ -97,8 +97,6 @@ __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m
       for (int jn = 0; jn < 4; ++jn) {
         if constexpr (EPI & EP_BNRED) {
           in.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
-          in.b[i][jn] = p.ep_y ? *(const uint2*)(p.ep_y + orow + jn * 16)
-                               : make_uint2(0x3f803f80u, 0x3f803f80u);
         } else {
           in.a[i][jn] = *(const uint2*)((const bf16_t*)p.C + orow + jn * 16);
         }
@@ -117,21 +115,23 @@ __device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0
 // registers across ALL of the block's tiles (ss/sq), reduced and written once per block by
 // halo_stats_flush.  epi_frag handles fragment (i, jn); the fused form calls it between the
 // next tile's taps (branch-free), the MASKED form after the block's last tile.
+// (BN reduction: cb / cs = mean / rstd, mc / mh = bn_fwd_train's scale / shift)
 template <int EPI, bool FULL>
-__device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, uint2 ia, uint2 ib,
-                                         bool ok, int jn, uint32_t orow, const f32x4& cb,
-                                         const f32x4& cs, float (&ssj)[4], float (&sqj)[4]) {
+__device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, uint2 ia, bool ok,
+                                         int jn, uint32_t orow, const f32x4& cb, const f32x4& cs,
+                                         const f32x4& mc, const f32x4& mh, float (&ssj)[4],
+                                         float (&sqj)[4]) {
   bf16_t* const out = (bf16_t*)p.C;
   float v[4];
   if constexpr (EPI & EP_BNRED) {
-    // dy (bf16-rounded) masked by ReLU(y) > 0; reduction (sum g, sum g * xhat)
-    const uint2 z = ia, y = ib;
+    // dy (bf16-rounded) masked by ReLU(bn(z)) > 0; reduction (sum g, sum g * xhat)
+    const uint2 z = ia;
     const float zr[4] = {lo_f(z.x), hi_f(z.x), lo_f(z.y), hi_f(z.y)};
-    const float yr[4] = {lo_f(y.x), hi_f(y.x), lo_f(y.y), hi_f(y.y)};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float d = bf2f(f2bf(acc[r]));
-      v[r] = ((FULL || ok) && yr[r] > 0.f) ? d : 0.f;
+      const bool live = bf2f(f2bf(__builtin_fmaf(zr[r], mc[r], mh[r]))) > 0.f;
+      v[r] = ((FULL || ok) && live) ? d : 0.f;
       ssj[r] += v[r];
       sqj[r] += v[r] * (zr[r] - cb[r]) * cs[r];
     }
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   char* const hal = smem;
   char* const wst = smem + 2 * HB_HBYTES;
   char* const red = smem + 2 * HB_HBYTES + 2 * HB_WBYTES;
-  float* const cst = (float*)(red + HB_RED);  // [2][64] per-column epilogue operands
+  float* const cst = (float*)(red + HB_RED);  // [4][64] per-column epilogue operands
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -342,8 +342,14 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   if (tid < HB_BN) {
     const float* bsrc = (EPI & EP_BNRED) ? p.ep_mean : p.bias;
     const float* ssrc = (EPI & EP_BNRED) ? p.ep_rstd : p.stats_shift;
-    cst[tid] = bsrc ? bsrc[n0 + tid] : 0.f;
-    cst[HB_BN + tid] = ssrc ? ssrc[n0 + tid] : 0.f;
+    const float b = bsrc ? bsrc[n0 + tid] : 0.f, sv = ssrc ? ssrc[n0 + tid] : 0.f;
+    cst[tid] = b;
+    cst[HB_BN + tid] = sv;
+    if constexpr (EPI & EP_BNRED) {  // the ReLU mask's affine, as bn_fwd_train computed it
+      const float sc = p.ep_gamma[n0 + tid] * sv;
+      cst[2 * HB_BN + tid] = sc;
+      cst[3 * HB_BN + tid] = __builtin_fmaf(-b, sc, p.ep_beta[n0 + tid]);
+    }
   }
   float ss[4][4], sq[4][4];
 #pragma unroll
@@ -366,10 +372,23 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     constexpr bool F = decltype(full)::value;
     const int m = m0e + wave * 64 + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
-    const f32x4 colb = *(const f32x4*)(cst + jn * 16 + jq * 4);
-    const f32x4 cols = *(const f32x4*)(cst + HB_BN + jn * 16 + jq * 4);
-    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], ein.b[i][jn], m < p.M, jn, orow, colb, cols,
-                     ss[jn], sq[jn]);
+    // (BN reduction: volatile, read where used - hoisted out of the tile loop, its four
+    // vectors would hold 64 VGPRs through every MFMA.  Volatile reads in the other
+    // flavours made them 12-30 % slower.)
+    const int c = jn * 16 + jq * 4;
+    f32x4 colb, cols, mc = {0.f, 0.f, 0.f, 0.f}, mh = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI & EP_BNRED) {
+      auto col = [&](int row) { return *(const volatile f32x4*)(cst + row * HB_BN + c); };
+      colb = col(0);
+      cols = col(1);
+      mc = col(2);
+      mh = col(3);
+    } else {
+      colb = *(const f32x4*)(cst + c);
+      cols = *(const f32x4*)(cst + HB_BN + c);
+    }
+    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh, ss[jn],
+                     sq[jn]);
   };
 
   // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + 4 B fragments (the next
@@ -725,7 +744,12 @@ static int halo_pitch(int W) { return (W + 1 + 7) / 8 * 8; }
 // epilogue flavour of a launch; -1: not instantiated (the implicit GEMM runs it)
 static int halo_epi(const IGemmArgs& a) {
   int e = 0;
-  if (a.ep_bnred) return (a.beta || a.relu || a.bias) ? -1 : EP_BNRED;
+  // fused BN reduction: the z-mask form only (y is never read; see EpiIn)
+  if (a.ep_bnred)
+    return (a.beta || a.relu || a.bias || a.ep_y || !a.ep_gamma || !a.ep_beta || !a.ep_mean ||
+            !a.ep_rstd)
+               ? -1
+               : EP_BNRED;
   if (a.relu) e |= EP_RELU;
   if (a.beta) e |= EP_BETA;
   if (a.stats) e |= EP_STATS;
@@ -767,9 +791,8 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   return (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
 }
 
-// Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves) for every flavour whose
-// MFMA waves fit the 256 registers two waves per SIMD leave; the fused BN-backward
-// reduction holds z and y for the epilogue and keeps the 4-wave form.  MPA_HALO_PROD=0: off.
+// Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves; each MFMA wave then has
+// 256 registers, which every flavour fits).  MPA_HALO_PROD=0: 4-wave blocks.
 static const bool g_halo_prod = [] {
   const char* e = getenv("MPA_HALO_PROD");
   return !(e && atoi(e) == 0);
@@ -794,12 +817,8 @@ static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPla
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  if constexpr (EPI == EP_BNRED) {
-    launch_halo_k<EPI, false>(wres, grid, a, h, s);
-  } else {
-    if (g_halo_prod) launch_halo_k<EPI, true>(wres, grid, a, h, s);
-    else launch_halo_k<EPI, false>(wres, grid, a, h, s);
-  }
+  if (g_halo_prod) launch_halo_k<EPI, true>(wres, grid, a, h, s);
+  else launch_halo_k<EPI, false>(wres, grid, a, h, s);
 }
 
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);

@@ -907,10 +907,14 @@ void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* s
   a.stats = slab;
   a.stats_sums = sums;
   int BM, BN, rows;
-  if (a.nphase == 0 && bkc && conv3_halo_ok(a)) {
-    rows = conv3_halo(a, s);
-    slab_reduce(slab, rows, 2 * a.N, sums, false, s);
-    return;
+  if (a.nphase == 0 && bkc) {
+    IGemmArgs t = a;
+    if (t.ep_gamma && t.ep_beta) t.ep_y = nullptr;  // the halo kernel's z-mask form
+    if (conv3_halo_ok(t)) {
+      rows = conv3_halo(t, s);
+      slab_reduce(slab, rows, 2 * a.N, sums, false, s);
+      return;
+    }
   }
   if (a.nphase > 0) {
     rows = plan_phases(a, BM, BN);

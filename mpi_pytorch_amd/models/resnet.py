@@ -16,8 +16,10 @@ from ..ops import functional as Fn
 
 
 # MPA_BN_LINK=1 enables the conv1 -> conv2 BN-backward hand-off (Fn.BNLink).  Off by
-# default: on ResNet-18 / batch 256 it removes 8 reduce passes but the dgrad epilogue's
-# strided z / y reads cost as much (same-box A/B: 11.45 ms off vs 11.50 ms on).
+# default: on ResNet-18 it removes 8 reduce passes (-335 us at batch 512) but the dgrad
+# epilogue that takes them over (z read, ReLU mask recomputed from z, two sums per
+# element) runs with the MFMA units idle, +350 us on the halo kernel alone (round-2
+# same-box A/B: 12.05 ms off vs 12.56 ms on; round 1 at batch 256: 11.45 vs 11.50).
 _LINK = os.environ.get("MPA_BN_LINK", "0") == "1"
 # MPA_GRAD_JOIN=0 restores autograd's separate add of the two input-gradient contributions
 _JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"

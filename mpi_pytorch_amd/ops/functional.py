@@ -79,10 +79,10 @@ class BNLink:
     mask and sums (g, g * x_hat) while the gradient is still in registers - and the
     producer's backward runs only the BN apply pass (no reduce pass, no re-read of dy/y)."""
 
-    __slots__ = ("z", "y", "mean", "rstd", "sums")
+    __slots__ = ("z", "y", "mean", "rstd", "gamma", "beta", "sums")
 
     def __init__(self):
-        self.z = self.y = self.mean = self.rstd = self.sums = None
+        self.z = self.y = self.mean = self.rstd = self.gamma = self.beta = self.sums = None
 
 
 class GradJoin:
@@ -193,7 +193,13 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.join_x = join_x
         ctx.join_res = join_res
         if link_out is not None:
-            link_out.z, link_out.y, link_out.mean, link_out.rstd = z, (y if relu else None), mean, rstd
+            link_out.z, link_out.mean, link_out.rstd = z, mean, rstd
+            # ReLU without a residual: the consumer's halo dgrad recomputes the mask from z
+            # (as the forward rounded y) when the BN is affine and never reads y (the
+            # implicit-GEMM fallback does)
+            zmask = relu and residual is None and gamma is not None and beta is not None
+            link_out.y = y if relu else None
+            link_out.gamma, link_out.beta = (gamma, beta) if zmask else (None, None)
             link_out.sums = None
         return y
 
@@ -235,7 +241,8 @@ class _ConvBNAct(torch.autograd.Function):
                     and k.conv_bnred_ok(w.shape[0], w.shape[3])):
                 dx, li.sums = k.conv_dgrad_bnred(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1],
                                                  sh, sw, ph, pw, wt, li.z,
-                                                 _or_empty(li.y, dz), li.mean, li.rstd)
+                                                 _or_empty(li.y, dz), li.mean, li.rstd,
+                                                 gamma=li.gamma, beta=li.beta)
                 dx = _join_grad(ctx.join_x, dx)
             else:
                 dx = _dgrad_joined(k, ctx.join_x, dz, weight_of(w), ctx.in_hw, conv, wt)

@@ -201,14 +201,21 @@ def conv_bnred_ok(K, C):
     return True
 
 
-def conv_dgrad_bnred(dy, w, H, W, sh, sw, ph, pw, wt, z, y, mean, rstd):
+def conv_dgrad_bnred(dy, w, H, W, sh, sw, ph, pw, wt, z, y, mean, rstd, gamma=None, beta=None):
     """dgrad fused with the backward reduction of the ReLU(BN) that produced the conv
-    input: returns (g = dx * (y > 0), [sum g | sum g * xhat])."""
+    input: returns (g = dx * (y > 0), [sum g | sum g * xhat]).  Without y, the mask is
+    recomputed from z with the forward's affine (gamma, beta) - the halo kernel's form
+    (y is the same mask when it is the forward's output)."""
     dx = conv_dgrad(dy, w, H, W, sh, sw, ph, pw)
     C = dx.shape[-1]
     g = _f(dx).reshape(-1, C)
     if _opt(y) is not None:
         g = g * (_f(y).reshape(-1, C) > 0)
+    elif gamma is not None and beta is not None:
+        sc = gamma.float() * rstd
+        sh_ = beta.float() - mean * sc
+        live = (_f(z).reshape(-1, C) * sc + sh_).to(torch.bfloat16).float() > 0
+        g = g * live
     xhat = (_f(z).reshape(-1, C) - mean) * rstd
     sums = torch.cat([g.sum(0), (g * xhat).sum(0)])
     return g.reshape(dx.shape).to(dx.dtype), sums

@@ -194,6 +194,17 @@ def test_conv_dgrad_fused_bn_reduction(gpu, case):
     dz, _ = C().bn_bwd_apply(g, z, e, mean, rstd, gamma, dg, db, sums, True, False)
     dzr, _ = ref.bn_bwd(dx, z, y, mean, rstd, gamma, dg2, db2, True)
     assert rel(dz, dzr) < 3e-2 and rel(dg, dg2) < 2e-2 and rel(db, db2) < 2e-2
+    # ReLU mask recomputed from z (y not passed): same mask as bn_fwd_train's rounded y
+    beta = torch.randn(Cc, device=gpu) * 0.2
+    sc = gamma * rstd
+    yz = torch.relu(z.float() * sc + (beta - mean * sc)).to(torch.bfloat16)
+    g2, sums2 = C().conv_dgrad_bnred(dy, w, H, W, st, st, ph, pw, wt, z, yz, mean, rstd,
+                                     gamma=gamma, beta=beta)
+    torch.cuda.synchronize()
+    assert rel(g2, (dx.float() * (yz.float() > 0)).to(torch.bfloat16)) < 1e-2
+    gr2, sr2 = ref.conv_dgrad_bnred(dy, w, H, W, st, st, ph, pw, None, z, None, mean, rstd,
+                                    gamma, beta)
+    assert rel(g2, gr2) < 2e-2 and rel(sums2, sr2) < 2e-2
 
 
 HALO_CASES = [
@@ -268,11 +279,20 @@ def test_conv_halo_dgrad(gpu, case):
     mean = torch.randn(Cc, device=gpu) * 0.3
     rstd = torch.rand(Cc, device=gpu) + 0.5
     y = torch.relu(z.float() - 0.2).to(torch.bfloat16)
-    (g, sums), (g0, sums0) = _halo_pair(
-        lambda: C().conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, wt, z, y, mean, rstd))
-    gr, sr = ref.conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, None, z, y, mean, rstd)
-    assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
-    assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+    gamma = torch.rand(Cc, device=gpu) + 0.5
+    beta = torch.randn(Cc, device=gpu) * 0.2
+    sc = gamma * rstd
+    yz = torch.relu(z.float() * sc + (beta - mean * sc)).to(torch.bfloat16)  # forward's y
+    # mask from y (implicit GEMM only) and, given gamma / beta, recomputed from z by the halo
+    # kernel (y is then the implicit GEMM's mask source)
+    for yy, ga, be in ((y, None, None), (yz, gamma, beta)):
+        (g, sums), (g0, sums0) = _halo_pair(
+            lambda: C().conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, wt, z, yy, mean, rstd,
+                                         gamma=ga, beta=be))
+        gr, sr = ref.conv_dgrad_bnred(dy, w, H, W, 1, 1, 1, 1, None, z,
+                                      yy if ga is None else None, mean, rstd, ga, be)
+        assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
+        assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
 
 
 @pytest.mark.parametrize("case", HALO_CASES)
