@@ -30,8 +30,11 @@ sys.path.insert(0, ROOT)
 BASELINE_IMG_S = 8.06  # reference FLOP-equivalent img/s at 224^2 (best, 4 ranks)
 
 
-def _emulate_comm(model, step, spec, dev):
-    """bench.py --emulate-comm: see the flag's help."""
+def _emulate_comm(model, step, spec, dev, reserve=0):
+    """bench.py --emulate-comm: see the flag's help.  ``reserve`` > 0 mimics the comm-aware
+    persistent grids of an overlapped bucket (parallel/ddp.py): the conv kernels enqueued
+    between the emulated collective's launch and the optimizer size their grids to the CUs
+    it leaves free."""
     from mpi_pytorch_amd.ops import _ext
     parts = [float(v) for v in spec.split(":")]
     blocks, us = int(parts[0]), parts[1]
@@ -45,6 +48,8 @@ def _emulate_comm(model, step, spec, dev):
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 _ext.ext().comm_emulator(blocks, 512, lds, us, sink)
+            if reserve > 0:
+                _ext.ext().set_comm_reserve(reserve)
 
     model._mpa_arena.add_listener(on_grad)
     fin = step.bucketer.finish
@@ -52,6 +57,8 @@ def _emulate_comm(model, step, spec, dev):
     def finish():
         fin()
         torch.cuda.current_stream(dev).wait_stream(side)
+        if reserve > 0:
+            _ext.ext().set_comm_reserve(0)
 
     step.bucketer.finish = finish
 
@@ -71,8 +78,17 @@ def main(argv=None):
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"])
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--comm-dtype", default="fp32")
+    p.add_argument("--comm-ctas", type=int, default=None,
+                   help="CTA cap of the overlapped buckets' RCCL communicator and the CUs the "
+                        "persistent conv grids leave it (0 off; default MPA_COMM_CTAS)")
+    p.add_argument("--comm-reserve", type=int, default=0,
+                   help="diagnostics, with --emulate-comm: CUs the persistent conv grids leave "
+                        "to the emulated collective while it is in flight")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")
+    p.add_argument("--timers", action="store_true",
+                   help="per-phase HIP-event times of the timed steps (data / forward / backward "
+                        "/ comm_wait / optimizer) as 'phases_ms' in the JSON line")
     p.add_argument("--static-data", action="store_true",
                    help="debug: reuse one device batch (no data pipeline in the loop)")
     p.add_argument("--emulate-comm", default="",
@@ -96,7 +112,7 @@ def main(argv=None):
     hw = (args.image_size, args.image_size)
     model, opt, step, _ = build_training(args.model, args.classes, dev, world, args.lr,
                                          args.optimizer, bucket_mb=args.bucket_mb,
-                                         comm_dtype=args.comm_dtype)
+                                         comm_dtype=args.comm_dtype, comm_ctas=args.comm_ctas)
     spec = input_spec(model, hw)  # the stem's image layout, written by the preprocess kernel
     data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
                             world=world.world_size, depth=6, threads=4, cpad=spec["cpad"],
@@ -106,7 +122,7 @@ def main(argv=None):
         xs, ys = data.next()
         data.next = lambda: (xs, ys)
     if args.emulate_comm:
-        _emulate_comm(model, step, args.emulate_comm, dev)
+        _emulate_comm(model, step, args.emulate_comm, dev, args.comm_reserve)
     # eager by default: the step is GPU-bound (host runs ahead), graph replay buys nothing
     # measurable and needs a per-step sync for correctness (engine/step.py)
     use_graph = args.graph == "on"
@@ -128,6 +144,8 @@ def main(argv=None):
             lazy.append(step(x, y).clone())
         print("lazy losses:", " ".join("%.3f" % float(v) for v in lazy), file=sys.stderr)
         print("loss_sum/steps: %.4f" % step.mean_loss(), file=sys.stderr)
+    if args.timers and not use_graph:
+        step.enable_timers()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -140,6 +158,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     loss = step.mean_loss()
+    phases = step.timer.summary() if step.timer is not None else None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world.world_size > 1:
         import torch.distributed as dist
@@ -174,6 +193,10 @@ def main(argv=None):
                 "mean_loss": round(loss, 4),
             },
         }
+        if phases is not None:
+            rec["phases_ms"] = phases
+            rec["grad_allreduce_mb"] = round(
+                sum(b["bytes"] for b in step.bucketer.describe()) / 2**20, 2)
         print(json.dumps(rec), flush=True)
     data.close()
     from mpi_pytorch_amd.parallel import shutdown

@@ -156,6 +156,15 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a);
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);
 bool igemm_halo_enabled();
+// Comm-aware persistent grids (conv_halo.hip).  While a data-parallel collective overlaps
+// backward, its CTAs hold CUs that a persistent conv block (146-150 KB of LDS) cannot
+// share; a block whose static tile share is queued behind one starts late and stretches
+// the whole kernel.  The bucketer reserves the collective's CTA count while a bucket is in
+// flight, and the persistent launches (halo fwd/dgrad and wgrad, stem fwd and wgrad) size
+// their grids to the CUs left: active_cus() = CU count - reserve, a multiple of 8 (XCDs).
+void set_comm_reserve(int cus);
+int comm_reserve();
+int active_cus();
 // conv_stem.hip: direct row-staged forward of the 7x7 pixel-pair stem (super-tap layout,
 // 64 output channels); run_rows takes it when conv_stem_ok.  Returns the slab rows written.
 bool conv_stem_ok(const IGemmArgs& a);

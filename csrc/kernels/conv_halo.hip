@@ -38,6 +38,7 @@
 //    GradJoin) after each tile; BN statistics accumulate in registers across all of a
 //    block's tiles and are written once per block.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 #include "igemm_common.h"
@@ -737,6 +738,19 @@ static int num_cus() {
   return n;
 }
 
+// CUs held by an overlapping collective (set by the host between kernel launches, read at
+// launch time: a launch enqueued after a bucket's collective runs after it in stream order)
+static std::atomic<int> g_comm_reserve{0};
+void set_comm_reserve(int cus) { g_comm_reserve.store(std::max(0, cus)); }
+int comm_reserve() { return g_comm_reserve.load(); }
+int active_cus() {
+  const int n = num_cus();
+  const int r = g_comm_reserve.load();
+  if (r <= 0) return n;
+  // whole CUs per XCD: the persistent tile schedules split their blocks XCD-contiguously
+  return std::max(8, (n - r) / 8 * 8);
+}
+
 // halo row pitch: W pixels + one zero column shared by consecutive rows (a row's right
 // border is the next row's left border), rounded up to 8 pixels
 static int halo_pitch(int W) { return (W + 1 + 7) / 8 * 8; }
@@ -844,7 +858,7 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   h.a_bytes = (uint32_t)((int64_t)a.M * a.aC * 2);
   h.b_bytes = (uint32_t)((int64_t)a.N * a.ldb * 2);
   // persistent grid: G8 blocks per XCD, a multiple of tiles_n (fixed column tile per block)
-  int g8 = std::min(std::min(num_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
+  int g8 = std::min(std::min(active_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
   const bool wres = a.tiles_n == 1 && h.cc <= 2;
@@ -898,7 +912,7 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.tiles_m = (a.Mpix + HW_BM - 1) / HW_BM;
   h.kparts = a.Kout / 64;
   h.parts = h.kparts * (a.C / 64);
-  const int G = std::min(num_cus(), HALO_MAX_ROWS);
+  const int G = std::min(active_cus(), HALO_MAX_ROWS);
   h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
   h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);

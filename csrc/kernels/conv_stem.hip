@@ -239,7 +239,7 @@ static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
 int conv_stem(IGemmArgs a, hipStream_t s) {
   // one statistics-slab row per block: the caller's slab holds >= slab_rows_max(M) rows
   if (g_stem_cfg == 1 && (a.M + 127) / 128 >= 512) return launch_stem<4, 4, 2>(a, 512, s);
-  return launch_stem<8, 8, 1>(a, HALO_MAX_ROWS, s);
+  return launch_stem<8, 8, 1>(a, std::min(HALO_MAX_ROWS, active_cus()), s);
 }
 
 // ======================================================================================
@@ -430,7 +430,7 @@ int stem_wgrad(WGradArgs a, hipStream_t s) {
   h.items_img = (a.P + 1) / 2;
   h.items = nimg * h.items_img;
   h.ks = (2 * a.Q + 31) / 32;
-  const int grid = std::max(1, std::min(h.items, HALO_MAX_ROWS));
+  const int grid = std::max(1, std::min(h.items, std::min(HALO_MAX_ROWS, active_cus())));
   switch (h.ks) {
 #define SW_CASE(K) \
   case K: hipLaunchKernelGGL(stem_wgrad_kernel<K>, dim3(grid), dim3(256), 0, s, a, h); break;

@@ -66,12 +66,16 @@ class Config:
     bucket_mb: float = 16.0                # gradient all-reduce bucket size (MiB)
     grad_comm_dtype: str = "fp32"          # fp32 | bf16 (wire dtype of the gradient all-reduce)
     overlap_comm: bool = True              # launch bucket all-reduce during backward
+    grad_comm_ctas: int = -1               # >0: overlapped buckets on a CTA-capped RCCL
+                                           # communicator + comm-aware persistent conv grids
+                                           # (0 off; -1: MPA_COMM_CTAS or the default)
     resume_epoch: bool = True              # honour saved epoch (reference restarts at 0: main.py:142)
     graph: str = "auto"                    # auto | on | off : HIP-graph capture of the train step
     seed: int = 0
     log_file: str = "training.log"
     log_per_rank_files: bool = False       # reference appends all ranks to one file (main.py:32)
     metrics_jsonl: str = ""                # machine-readable per-epoch metrics
+    step_timers: bool = False              # per-phase HIP-event step times in the metrics
     num_workers: int = 2                   # native decode/prefetch threads
     eval_lanes: int = 1                    # predictor lanes in the eval pipeline
     eval_batch: int = 64

@@ -32,12 +32,13 @@ from ..parallel import ParamArena, GradBucketer, sync_params, World
 
 def build_model(name: str, num_classes: int, feature_extract: bool, device: torch.device,
                 world: World, use_pretrained: bool = False, bucket_mb: float = 16.0,
-                overlap: bool = True, comm_dtype: str = "fp32"):
+                overlap: bool = True, comm_dtype: str = "fp32", comm_ctas: Optional[int] = None):
     model, input_size = initialize_model(name, num_classes, feature_extract, use_pretrained)
     model = model.to(device)
     arena = ParamArena(model, device)
     model._mpa_arena = arena
-    model._mpa_bucketer = GradBucketer(arena, world.world_size, bucket_mb, overlap, comm_dtype)
+    model._mpa_bucketer = GradBucketer(arena, world.world_size, bucket_mb, overlap, comm_dtype,
+                                       comm_ctas=comm_ctas)
     return model, input_size
 
 
@@ -51,6 +52,74 @@ def loss_fn(out, labels):
             loss = loss + 0.4 * Fn.cross_entropy(aux, labels)
         return loss
     return Fn.cross_entropy(out, labels)
+
+
+class StepTimer:
+    """Per-step phase times from HIP events on the compute stream:
+
+    * ``data``      - previous step's end to this step's start: the batch hand-off, H2D
+                      copy and preprocess kernel the loader enqueued in between;
+    * ``forward``   - gradient-arena zero, forward and loss;
+    * ``backward``  - backward, with the overlapped bucket all-reduces launched inside it;
+    * ``comm_wait`` - the exposed part of the gradient all-reduce (``GradBucketer.finish``);
+    * ``optimizer`` - the fused optimizer kernel (+ transposed-weight refresh).
+
+    Events are resolved lazily (``summary``), so timing adds no host sync to the step.
+    The reference has only the per-epoch ``MPI.Wtime()`` (``/root/reference/main.py:145,158``).
+    """
+
+    PHASES = ("data", "forward", "backward", "comm_wait", "optimizer")
+    _MAX_PENDING = 64
+
+    def __init__(self):
+        self._pending = []
+        self._cur = None
+        self.reset()
+
+    def reset(self) -> None:
+        self.totals = {k: 0.0 for k in self.PHASES}
+        self.steps = 0
+        self.data_steps = 0
+        self._last_end = None  # e.g. an epoch's checkpoint / validation is no data time
+
+    def mark(self, i: int) -> None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if i == 0:
+            self._cur = [self._last_end, ev]
+        else:
+            self._cur.append(ev)
+            if i == 4:
+                self._last_end = ev
+                self._pending.append(self._cur)
+                self._cur = None
+                if len(self._pending) > self._MAX_PENDING:
+                    self._resolve(self._pending[: self._MAX_PENDING // 2])
+                    del self._pending[: self._MAX_PENDING // 2]
+
+    def _resolve(self, recs) -> None:
+        for rec in recs:
+            rec[-1].synchronize()
+            prev, evs = rec[0], rec[1:]
+            if prev is not None:
+                self.totals["data"] += prev.elapsed_time(evs[0])
+                self.data_steps += 1
+            for k, a, b in zip(self.PHASES[1:], evs[:-1], evs[1:]):
+                self.totals[k] += a.elapsed_time(b)
+            self.steps += 1
+
+    def summary(self, reset: bool = True) -> dict:
+        """Mean milliseconds per step of each phase (plus ``step``) since the last reset."""
+        self._resolve(self._pending)
+        self._pending = []
+        n = max(self.steps, 1)
+        out = {k: round(v / n, 4) for k, v in self.totals.items()}
+        out["data"] = round(self.totals["data"] / max(self.data_steps, 1), 4)
+        out["step"] = round(sum(out[k] for k in self.PHASES), 4)
+        out["steps"] = self.steps
+        if reset:
+            self.reset()
+        return out
 
 
 class TrainStep:
@@ -73,14 +142,32 @@ class TrainStep:
         # execution are exact and equally fast for GPU-bound steps.  Graph mode therefore
         # syncs after each replay unless MPA_GRAPH_UNSAFE=1.
         self._sync_replay = os.environ.get("MPA_GRAPH_UNSAFE", "0") != "1"
+        self.timer: Optional[StepTimer] = None
+
+    def enable_timers(self) -> StepTimer:
+        """Turn on per-phase HIP-event timing of eager steps (GPU only)."""
+        if self.timer is None and self.arena.device.type == "cuda":
+            self.timer = StepTimer()
+        return self.timer
 
     def _eager(self, x, y):
+        t = self.timer if self._graph is None else None
+        if t is not None:
+            t.mark(0)
         self.arena.zero_grad()
         out = self.model(x)
         loss = loss_fn(out, y)
+        if t is not None:
+            t.mark(1)
         loss.backward()
+        if t is not None:
+            t.mark(2)
         self.bucketer.finish()
+        if t is not None:
+            t.mark(3)
         self.opt.step()
+        if t is not None:
+            t.mark(4)
         return loss.detach()
 
     def __call__(self, x, y) -> torch.Tensor:
@@ -116,6 +203,7 @@ class TrainStep:
             return False
         self._static_x = x.clone()
         self._static_y = y.clone()
+        self.timer = None  # replayed steps are not phase-timed
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -132,9 +220,10 @@ class TrainStep:
 def build_training(name: str, num_classes: int, device, world: World, lr: float,
                    optimizer: str = "adam", momentum: float = 0.9, weight_decay: float = 0.0,
                    feature_extract: bool = False, bucket_mb: float = 16.0, overlap: bool = True,
-                   comm_dtype: str = "fp32"):
+                   comm_dtype: str = "fp32", comm_ctas: Optional[int] = None):
     model, input_size = build_model(name, num_classes, feature_extract, device, world,
-                                    bucket_mb=bucket_mb, overlap=overlap, comm_dtype=comm_dtype)
+                                    bucket_mb=bucket_mb, overlap=overlap, comm_dtype=comm_dtype,
+                                    comm_ctas=comm_ctas)
     opt = build_optimizer(optimizer, model, lr, momentum, weight_decay)
     sync_params(model)
     model.train()

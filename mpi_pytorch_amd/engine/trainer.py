@@ -169,7 +169,7 @@ def run_training(cfg: Config) -> dict:
     model, opt, step, _input_size = build_training(
         cfg.MODEL_NAME, cfg.NUM_CLASSES, dev, world, cfg.LR, cfg.optimizer, cfg.momentum,
         cfg.weight_decay, cfg.FEATURE_EXTRACT, cfg.bucket_mb, cfg.overlap_comm,
-        cfg.grad_comm_dtype)
+        cfg.grad_comm_dtype, None if cfg.grad_comm_ctas < 0 else cfg.grad_comm_ctas)
     log.info("_Model Created: {}".format(cfg.MODEL_NAME))
     spec = input_spec(model, out_hw)
     for ld in (train_loader, val_loader):
@@ -188,6 +188,8 @@ def run_training(cfg: Config) -> dict:
     log.info("_Model loaded to {}".format("GPU" if dev.type == "cuda" else "CPU"))
     log.info("_Entering training Loop")
 
+    if cfg.step_timers:
+        step.enable_timers()
     history = []
     # fail fast on a stalled rank (e.g. a peer died inside a collective): SURVEY.md §5.3
     dog = Watchdog(cfg.watchdog_s, rank=rank).start()
@@ -212,6 +214,11 @@ def run_training(cfg: Config) -> dict:
         rec = {"epoch": epoch, "train_loss": tr_loss, "time_s": dt,
                "img_per_s_rank": nimg / dt if dt > 0 else 0.0,
                "img_per_s_global": nimg * size / dt if dt > 0 else 0.0}
+        if step.timer is not None:
+            rec["phase_ms"] = step.timer.summary()
+            if size > 1:
+                rec["grad_allreduce_mb"] = round(
+                    sum(b["bytes"] for b in step.bucketer.describe()) / 2**20, 2)
         if cfg.checksum_every and size > 1:
             rec["replicas_consistent"] = replica_checksum(model)
         if rank == 0:

@@ -21,9 +21,19 @@ Design for MI355X / RCCL over xGMI:
   optimizer kernel's ``grad_scale`` (no extra pass over the gradients).
 * Optional bf16 wire format halves xGMI bytes (cast kernels around the collective).
 * ``world_size == 1`` is a no-op, like ``mpi_tools.py:32-33``.
+* Comm-aware persistent grids (``comm_ctas``, ``MPA_COMM_CTAS``, default 8; 0 = off): the
+  buckets that overlap backward run on a second RCCL communicator capped at ``comm_ctas``
+  CTAs (``ncclConfig_t.maxCTAs``), and while one is in flight the persistent conv kernels size
+  their grids to the CUs the collective leaves free (``_ext.set_comm_reserve``).  Without
+  it an RCCL CTA sits on a CU that a persistent conv block (146-150 KB of LDS) cannot
+  share, and that block's static tile share starts only when another block finishes
+  (``bench.py --emulate-comm``, docs/KERNELS.md §2c).  The 126 MiB head bucket needs only
+  ~35 GB/s of bus bandwidth to hide under a ~7 ms backward, so a few CTAs suffice; the
+  last bucket, which nothing overlaps, keeps the default (uncapped) communicator.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -33,14 +43,58 @@ import torch.nn as nn
 from .arena import ParamArena
 
 
+def _set_reserve(cus: int) -> None:
+    from ..ops import _ext
+    _ext.ext().set_comm_reserve(int(cus))
+
+
+# CTA cap of the overlapped buckets' communicator when neither the caller nor MPA_COMM_CTAS
+# says otherwise.  profiles/comm_reserve_emulated_r2.txt (1 GPU, emulated collective):
+# 8 or 32 CTAs held for 2 / 6 ms of backward cost +0.70 / +1.84 ms per step with static
+# persistent grids, +0.38 / +0.61 ms with the reservation - the straggle depends on how
+# long ANY CU is held, not on how many, so few CTAs plus a reservation is the cheap shape.
+DEFAULT_COMM_CTAS = 8
+
+
+def capped_group(max_ctas: int, device: torch.device):
+    """A second RCCL communicator over all ranks whose collectives use at most ``max_ctas``
+    CTAs (None on non-RCCL backends, or if RCCL rejects the config - checked with one tiny
+    all-reduce, so a failure shows here and not inside backward).  Collective call: every
+    rank must make it."""
+    if device.type != "cuda" or dist.get_backend() != "nccl":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.config.max_ctas = int(max_ctas)
+        g = dist.new_group(ranks=list(range(dist.get_world_size())), backend="nccl",
+                           pg_options=opts)
+        probe = torch.ones(64, device=device)
+        dist.all_reduce(probe, group=g)
+        torch.cuda.synchronize(device)
+        if float(probe[0]) != float(dist.get_world_size()):
+            raise RuntimeError("capped communicator returned %s" % float(probe[0]))
+        return g
+    except Exception as ex:  # keep the default communicator, uncapped grids
+        import sys
+        print("GradBucketer: no CTA-capped communicator (%s); overlapped buckets use the "
+              "default one" % ex, file=sys.stderr)
+        return None
+
+
 class GradBucketer:
     def __init__(self, arena: ParamArena, world_size: int, bucket_mb: float = 16.0,
-                 overlap: bool = True, comm_dtype: str = "fp32", group=None):
+                 overlap: bool = True, comm_dtype: str = "fp32", group=None,
+                 comm_ctas: Optional[int] = None):
         self.arena = arena
         self.world_size = world_size
         self.overlap = overlap
         self.comm_dtype = comm_dtype
         self.group = group
+        if comm_ctas is None:
+            comm_ctas = int(os.environ.get("MPA_COMM_CTAS", DEFAULT_COMM_CTAS))
+        self.comm_ctas = max(int(comm_ctas), 0)
+        self.overlap_group = None
+        self._reserved = False
         cap = max(int(bucket_mb * 1024 * 1024 // 4), 1)
         self.buckets: List[List[nn.Parameter]] = []
         self.ranges: List[tuple] = []
@@ -72,6 +126,8 @@ class GradBucketer:
         self.active = world_size > 1
         if self.active:
             arena.add_listener(self._on_grad)
+            if self.comm_ctas > 0 and self.overlap and len(self.buckets) > 1:
+                self.overlap_group = capped_group(self.comm_ctas, arena.device)
         self.reset()
 
     # ------------------------------------------------------------------------------
@@ -95,13 +151,20 @@ class GradBucketer:
             return
         s, e = self.ranges[bi]
         g = self.arena.grad[s:e]
+        group = self.group
+        if self.overlap_group is not None and bi != len(self.buckets) - 1:
+            # an overlapped bucket: capped communicator, persistent grids give way
+            group = self.overlap_group
+            if not self._reserved:
+                _set_reserve(self.comm_ctas)
+                self._reserved = True
         if self.comm_dtype == "bf16" and g.is_cuda:
             w = g.to(torch.bfloat16)
             self._wire[bi] = w
-            self._works[bi] = dist.all_reduce(w, op=dist.ReduceOp.SUM, group=self.group,
+            self._works[bi] = dist.all_reduce(w, op=dist.ReduceOp.SUM, group=group,
                                               async_op=True)
         else:
-            self._works[bi] = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
+            self._works[bi] = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group,
                                               async_op=True)
 
     def finish(self) -> None:
@@ -119,6 +182,10 @@ class GradBucketer:
                 s, e = self.ranges[bi]
                 self.arena.grad[s:e].copy_(self._wire[bi])
                 self._wire[bi] = None
+        if self._reserved:
+            # kernels enqueued from here on (optimizer, next forward) run after the waits
+            _set_reserve(0)
+            self._reserved = False
         self.reset()
 
     @property

@@ -960,3 +960,67 @@ def test_conv_stem_wgrad_plan(gpu, N, P, Q):
         assert rel(f, gemm) < 1e-4 and rel(f, dwr) < 1e-2
     if forced:
         assert rel(forced[0], forced[1]) < 1e-5
+
+
+@pytest.mark.parametrize("reserve", [8, 40])
+def test_comm_reserve_grids(gpu, reserve):
+    """Comm-aware persistent grids (set_comm_reserve, parallel/ddp.py): with CUs reserved
+    for an overlapping collective, the halo fwd / dgrad / wgrad and the stem fwd / wgrad
+    launch fewer persistent blocks; every output tile is computed the same way (outputs
+    bitwise equal), only the per-block statistics / weight-gradient partials are summed in
+    another order (fp32 rounding)."""
+    torch.manual_seed(41)
+    e = torch.empty(0, device=gpu)
+    full = C().active_cus()
+    assert C().comm_reserve() == 0
+
+    def halo_run(N, H, W, Cc, K):
+        x = bf(N, H, W, Cc, dev=gpu)
+        w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * Cc))
+        wt = w.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+        dy = bf(N, H, W, K, dev=gpu)
+        shift = torch.randn(K, device=gpu) * 0.1
+
+        def run():
+            st = torch.zeros(2, K, device=gpu)
+            y = C().conv_fwd(x, w, e, 1, 1, 1, 1, False, st, shift)
+            dx = C().conv_dgrad(dy, w, H, W, 1, 1, 1, 1, wt)
+            dw = torch.zeros(K, 3, 3, Cc, device=gpu)
+            C().conv_wgrad(dy, x, dw, 1, 1, 1, 1)
+            return y, st, dx, dw
+        return run
+
+    def stem_run(N, P, Q):
+        x = bf(N, 2 * (P - 1) + 7, Q + 3, 8, dev=gpu, scale=0.5)
+        w = bf(64, 7, 4, 8, dev=gpu, scale=0.05)
+        dy = bf(N, P, Q, 64, dev=gpu, scale=0.1)
+        shift = torch.randn(64, device=gpu) * 0.1
+
+        def run():
+            st = torch.empty(2, 64, device=gpu)
+            y = C().conv_fwd(x, w, e, 2, 1, 0, 0, False, st, shift)
+            dw = torch.zeros(64, 7, 4, 8, device=gpu)
+            C().conv_wgrad(dy, x, dw, 2, 1, 0, 0)
+            return y, st, dw
+        return run
+
+    C().igemm_set_halo(1)
+    cases = [halo_run(25, 56, 56, 64, 64), halo_run(52, 14, 14, 256, 512),
+             halo_run(3, 9, 11, 96, 128)]
+    stem = stem_run(8, 112, 112)
+    base = [f() for f in cases] + [stem()]
+    torch.cuda.synchronize()
+    try:
+        C().set_comm_reserve(reserve)
+        assert C().comm_reserve() == reserve
+        assert C().active_cus() == max(8, (full - reserve) // 8 * 8)
+        got = [f() for f in cases] + [stem()]
+        torch.cuda.synchronize()
+    finally:
+        C().set_comm_reserve(0)
+    assert C().active_cus() == full
+    for (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) in zip(base[:3], got[:3]):
+        assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
+        assert rel(s1, s0) < 1e-4 and rel(dw1, dw0) < 1e-4
+    (y0, s0, dw0), (y1, s1, dw1) = base[3], got[3]
+    assert torch.equal(y0, y1) and rel(s1, s0) < 1e-4 and rel(dw1, dw0) < 1e-4

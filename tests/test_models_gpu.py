@@ -72,3 +72,32 @@ def test_resnet18_training_decreases_loss(gpu):
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0] * 0.5, losses
+
+
+def test_step_phase_timers(gpu):
+    """StepTimer (engine/step.py): HIP-event phase times of eager steps resolve without a
+    per-step sync, every phase is non-negative, the compute phases are positive, and the
+    phase sum tracks the host wall clock of the same steps."""
+    import time
+    from mpi_pytorch_amd.optim import build_optimizer as bo
+    from mpi_pytorch_amd.engine.step import TrainStep
+    torch.manual_seed(0)
+    w = World(device=gpu)
+    m, _ = build_model("resnet18", 100, False, gpu, w)
+    step = TrainStep(m, bo("adam", m, 1e-3), w)
+    x = (torch.randn(16, 64, 64, 3, device=gpu) * 0.5).to(torch.bfloat16)
+    y = torch.randint(0, 100, (16,), device=gpu)
+    step(x, y)
+    t = step.enable_timers()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        step(x, y)
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3 / 5
+    s = t.summary()
+    assert s["steps"] == 5
+    assert all(s[k] >= 0.0 for k in t.PHASES)
+    assert s["forward"] > 0 and s["backward"] > 0 and s["optimizer"] > 0
+    assert 0.3 * wall_ms < s["step"] < 1.5 * wall_ms, (s, wall_ms)
+    assert t.summary()["steps"] == 0  # reset
