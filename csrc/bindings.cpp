@@ -831,6 +831,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");
   m.def("igemm_halo_enabled", &mpa::igemm_halo_enabled);
   m.def("igemm_set_stem", &mpa::igemm_set_stem, "direct row-staged 7x7 pixel-pair stem on/off");
+  m.def("preprocess_set_copy", &mpa::preprocess_set_copy,
+        "identity-size preprocess fast path on/off (MPA_PRE_COPY)");
   m.def("set_comm_reserve", &mpa::set_comm_reserve,
         "CUs held by an overlapping collective (persistent conv grids use the rest)");
   m.def("comm_reserve", &mpa::comm_reserve, "current collective CU reservation");

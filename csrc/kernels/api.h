@@ -277,6 +277,7 @@ struct Norm3 {
 struct OutPad {
   int top, bottom, left, right;
 };
+void preprocess_set_copy(int on);  // identity-size fast path on/off (tests, A/B)
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
                 int cpad, OutPad pad, bf16_raw* out, hipStream_t s);
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,

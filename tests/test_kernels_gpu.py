@@ -856,6 +856,26 @@ def test_preprocess_canvas(gpu, mode, cpad, pad):
     assert float(out.float().masked_fill(inner, 0).abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("hw,pad", [((224, 224), (3, 2, 3, 3)), ((37, 20), (3, 3, 3, 3)),
+                                    ((8, 300), (0, 1, 2, 0))])
+def test_preprocess_identity_copy(gpu, hw, pad):
+    """Identity-size training preprocess (preprocess_copy4_kernel): bitwise equal to the
+    bilinear kernel (its weights are exactly 0 / 1 at scale 1), zero border and padding
+    channel; W = 300 makes a row need more than one pass of the 64 lanes."""
+    H, W = hw
+    img = torch.randint(0, 256, (3, H, W, 3), dtype=torch.uint8, device=gpu)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    outs = []
+    for on in (1, 0):
+        C().preprocess_set_copy(on)
+        outs.append(C().preprocess(img, H, W, list(mean), list(std), 0, 4, list(pad)))
+    C().preprocess_set_copy(1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    r = ref.preprocess(img, H, W, mean, std, 0, 4, torch.float32, pad)
+    assert float((outs[0].float() - r).abs().max()) < 0.05
+
+
 def test_dropout(gpu):
     x = torch.ones(1 << 16, device=gpu, dtype=torch.bfloat16)
     y, m = C().dropout_fwd(x, 0.5, 7, 1)
