@@ -284,7 +284,8 @@ std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Ten
   return {dx, gout};
 }
 
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                bool overwrite) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   CHECK_CUDA(dw);
@@ -302,6 +303,7 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t 
   a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
   a.Mpix = N * P * Q;
   a.Ncols = R * S * C;
+  a.overwrite = overwrite ? 1 : 0;
   Tensor slab;
   a.slab = alloc_ws(slab, dy, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   mpa::igemm_wgrad(a, vec_width(K), (C % 8 == 0) ? 8 : 1, cur_stream());
@@ -598,7 +600,7 @@ Tensor linear_dgrad(Tensor dy, Tensor w, c10::optional<Tensor> wt_opt) {
   return dx;
 }
 
-void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
+void linear_wgrad(Tensor dy, Tensor x, Tensor dw, bool overwrite) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   CHECK_CUDA(dw);
@@ -611,6 +613,7 @@ void linear_wgrad(Tensor dy, Tensor x, Tensor dw) {
   a.Kout = Cout; a.C = Cin; a.H = 1; a.W = 1; a.P = 1; a.Q = 1; a.R = 1; a.S = 1;
   a.sh = 1; a.sw = 1; a.ph = 0; a.pw = 0;
   a.Mpix = B; a.Ncols = Cin;
+  a.overwrite = overwrite ? 1 : 0;
   Tensor slab;
   a.slab = alloc_ws(slab, dy, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   mpa::igemm_wgrad(a, vec_width(Cout), (Cin % 8 == 0) ? 8 : 1, cur_stream());
@@ -841,7 +844,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none(),
         py::arg("accum") = py::none());
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("overwrite") = false,
+        "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, py::arg("dy"), py::arg("w"), py::arg("H"),
         py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt"),
@@ -878,7 +883,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adaptive_avgpool_bwd", &adaptive_avgpool_bwd);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("wt") = py::none());
-  m.def("linear_wgrad", &linear_wgrad);
+  m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"),
+        py::arg("overwrite") = false);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("argmax_correct", &argmax_correct);

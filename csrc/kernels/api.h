@@ -113,6 +113,8 @@ struct WGradArgs {
   int Ncols;
   int ktiles_per_split;
   int tiles_n, tiles_total;
+  int overwrite;  // 1: dw holds nothing to keep (first gradient since zero_grad): store, no
+                  // read-modify-write of the fp32 arena
 };
 
 // igemm.hip

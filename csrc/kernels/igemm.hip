@@ -409,12 +409,13 @@ __global__ __launch_bounds__(256, OCC) void igemm_wgrad_kernel(WGradArgs p) {
 
 }
 
-// dw[i] += sum_z slab[z][i].  A block owns 64 float4 columns; its 4 waves sum disjoint
+// dw[i] += sum_z slab[z][i] (dw[i] = ... when overwrite).  A block owns 64 float4 columns; its 4 waves sum disjoint
 // quarters of the splits (4 float4 loads in flight per lane), then reduce through LDS.
 // With ~100 splits of a small layer (ResNet-18 layer1: 64 x 576 outputs) a
 // one-thread-per-column walk over the splits ran at ~0.6 TB/s on 36 blocks.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int S,
-                                                            int64_t n, float* __restrict__ dw) {
+                                                            int64_t n, float* __restrict__ dw,
+                                                            int overwrite) {
   __shared__ f32x4 red[4][64];
   const int64_t n4 = n / 4;
   const int64_t c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   __syncthreads();
   if (g == 0 && c < n4) {
     const int t = threadIdx.x;
-    f32x4 v = ((f32x4*)dw)[c];
+    f32x4 v = overwrite ? f32x4{0.f, 0.f, 0.f, 0.f} : ((f32x4*)dw)[c];
     v += (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
     ((f32x4*)dw)[c] = v;
   }
@@ -444,10 +445,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // any n (split rows not 16-B aligned when n % 4 != 0): one thread per element
 __global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* __restrict__ slab,
                                                                    int S, int64_t n,
-                                                                   float* __restrict__ dw) {
+                                                                   float* __restrict__ dw,
+                                                                   int overwrite) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float a = dw[i];
+    float a = overwrite ? 0.f : dw[i];
     for (int z = 0; z < S; ++z) a += slab[(size_t)z * n + i];
     dw[i] = a;
   }
@@ -1106,14 +1108,16 @@ void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
     const int z = conv3_halo_wgrad(a, s);
     const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 64 == 0: float4 rows
     const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
+                       a.overwrite);
     return;
   }
   if (igemm_engine() >= 1 && stem_wgrad_ok(a)) {  // pixel-pair 7x7 stem: halo-staged
     const int z = stem_wgrad(a, s);
     const int64_t n = (int64_t)a.Kout * a.Ncols;
     const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
+                       a.overwrite);
     return;
   }
   const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
@@ -1144,11 +1148,11 @@ static void wgrad_run_plan(WGradArgs a, int vwa, int vwb, hipStream_t s, int tbm
     if (n % 4 == 0) {  // float4 path: 16-B aligned split rows
       const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
       hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, splits, n,
-                         a.dw);
+                         a.dw, a.overwrite);
     } else {
       const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
       hipLaunchKernelGGL(wgrad_reduce_scalar_kernel, dim3(blocks), dim3(256), 0, s, a.slab,
-                         splits, n, a.dw);
+                         splits, n, a.dw, a.overwrite);
     }
   }
 }

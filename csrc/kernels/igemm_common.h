@@ -398,7 +398,8 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
 // Wgrad engine.  The MFMA is issued with the column (r,s,c) operand first, so lane owns
 // D[n = nb + r][m = lane&15]: four consecutive weight-gradient columns of one output
 // channel -> one 16-B fp32 access per lane.  One split: read-modify-write straight into
-// the fp32 gradient arena.  Several splits: plain stores of this split's partial into the
+// the fp32 gradient arena (a plain store when p.overwrite: the classifier's 132 MB gradient
+// is then written once instead of read and written).  Several splits: plain stores of this split's partial into the
 // slab [z][Kout][Ncols]; wgrad_reduce sums the slab into the arena afterwards.
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
@@ -421,12 +422,12 @@ __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
       float* q = dst + (size_t)m * p.Ncols + n;
       if (vec && n + 3 < p.Ncols) {
         f32x4 v = acc[i][j];
-        if (direct) v += *(const f32x4*)q;
+        if (direct && !p.overwrite) v += *(const f32x4*)q;
         *(f32x4*)q = v;
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (n + r < p.Ncols) q[r] = direct ? q[r] + acc[i][j][r] : acc[i][j][r];
+          if (n + r < p.Ncols) q[r] = (direct && !p.overwrite) ? q[r] + acc[i][j][r] : acc[i][j][r];
       }
     }
   }

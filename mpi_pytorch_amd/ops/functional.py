@@ -65,6 +65,12 @@ def _sink(p: Optional[torch.nn.Parameter], like: torch.Tensor) -> torch.Tensor:
     return s if s is not None else _empty(like)
 
 
+def _fresh(p: torch.nn.Parameter) -> bool:
+    """Whether ``p``'s arena gradient is untouched since zero_grad (consumed by the call)."""
+    a = getattr(p, "_mpa_arena", None)
+    return a.take_fresh(p) if a is not None else False
+
+
 def _done(*ps) -> None:
     for p in ps:
         if p is not None:
@@ -227,7 +233,7 @@ class _ConvBNAct(torch.autograd.Function):
         _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
             conv.fix_grad(w.grad)
             _done(w)
         _done(ctx.bias)
@@ -323,7 +329,7 @@ class _ConvBNReLUPool(torch.autograd.Function):
         _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw)
+            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
             conv.fix_grad(w.grad)
             _done(w)
         _done(ctx.bias)
@@ -371,7 +377,7 @@ class _ConvAct(torch.autograd.Function):
         _done(b)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw)
+            k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
             conv.fix_grad(w.grad)
             _done(w)
         dx = None
@@ -446,7 +452,7 @@ class _LinearAct(torch.autograd.Function):
         g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
         _done(b)
         if w.requires_grad:
-            k.linear_wgrad(g, x, w.grad)
+            k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
             _done(w)
         dx = (k.linear_dgrad(g, weight_of(w), weight_t_of(w)) if ctx.needs_input_grad[0]
               else None)

@@ -77,13 +77,16 @@ def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None, accum=None):
     return _nhwc(gi).to(dy.dtype)
 
 
-def conv_wgrad(dy, x, dw, sh, sw, ph, pw):
+def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False):
     K, R, S, C = dw.shape
     gw = torch.ops.aten.convolution_backward(
         _nchw(_f(dy)).contiguous(), _nchw(_f(x)).contiguous(),
         torch.empty(K, C, R, S, device=dy.device), None, [sh, sw], [ph, pw], [1, 1], False,
         [0, 0], 1, [False, True, False])[1]
-    dw.add_(gw.permute(0, 2, 3, 1))
+    if overwrite:
+        dw.copy_(gw.permute(0, 2, 3, 1))
+    else:
+        dw.add_(gw.permute(0, 2, 3, 1))
 
 
 def act_bwd(dy, y, dbias):
@@ -311,8 +314,11 @@ def linear_dgrad(dy, w, wt=None):
     return (_f(dy) @ _f(w)).to(dy.dtype)
 
 
-def linear_wgrad(dy, x, dw):
-    dw.add_(_f(dy).t() @ _f(x))
+def linear_wgrad(dy, x, dw, overwrite=False):
+    if overwrite:
+        dw.copy_(_f(dy).t() @ _f(x))
+    else:
+        dw.add_(_f(dy).t() @ _f(x))
 
 
 # --------------------------------------------------------------------------- loss / acc

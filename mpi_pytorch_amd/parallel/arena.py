@@ -81,6 +81,9 @@ class ParamArena:
                     p.grad = self.grad[o:o + p.numel()].view_as(p)
                 p._mpa_arena = self
         self._listeners: List[Callable[[nn.Parameter], None]] = []
+        # parameters whose gradient slice still holds the zeros of the last zero_grad():
+        # their first weight-gradient kernel stores instead of read-modify-writing
+        self._fresh = {id(p) for p in trainable}
         self._init_transposed()
         self.sync_shadow()
 
@@ -132,6 +135,17 @@ class ParamArena:
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+        self._fresh = {id(p) for p in self.trainable}
+
+    def take_fresh(self, p: nn.Parameter) -> bool:
+        """True (once per zero_grad) if ``p``'s gradient is still all zeros: the caller's
+        kernel may overwrite it instead of accumulating (the 132 MB classifier gradient is
+        then written, not read and written)."""
+        i = id(p)
+        if i in self._fresh:
+            self._fresh.discard(i)
+            return True
+        return False
 
     def add_listener(self, fn: Callable[[nn.Parameter], None]) -> None:
         self._listeners.append(fn)

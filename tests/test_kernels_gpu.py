@@ -1044,3 +1044,36 @@ def test_comm_reserve_grids(gpu, reserve):
         assert rel(s1, s0) < 1e-4 and rel(dw1, dw0) < 1e-4
     (y0, s0, dw0), (y1, s1, dw1) = base[3], got[3]
     assert torch.equal(y0, y1) and rel(s1, s0) < 1e-4 and rel(dw1, dw0) < 1e-4
+
+
+@pytest.mark.parametrize("kind", ["linear", "halo", "strided", "stem"])
+def test_wgrad_overwrite(gpu, kind):
+    """overwrite=True (the first gradient since zero_grad, ParamArena.take_fresh): the
+    weight gradient is stored over whatever dw held and equals accumulating into zeros;
+    overwrite=False still accumulates."""
+    torch.manual_seed(43)
+    if kind == "linear":
+        dy, x = bf(512, 4096, dev=gpu, scale=0.1), bf(512, 512, dev=gpu)
+        shape = (4096, 512)
+        run = lambda dw, ow: C().linear_wgrad(dy, x, dw, overwrite=ow)
+    elif kind == "stem":
+        x = bf(4, 2 * 27 + 7, 28 + 3, 8, dev=gpu, scale=0.5)
+        dy = bf(4, 28, 28, 64, dev=gpu, scale=0.1)
+        shape = (64, 7, 4, 8)
+        run = lambda dw, ow: C().conv_wgrad(dy, x, dw, 2, 1, 0, 0, overwrite=ow)
+    else:
+        st = 1 if kind == "halo" else 2
+        x = bf(6, 28, 28, 128, dev=gpu)
+        dy = bf(6, 28 // st, 28 // st, 128, dev=gpu, scale=0.1)
+        shape = (128, 3, 3, 128)
+        run = lambda dw, ow: C().conv_wgrad(dy, x, dw, st, st, 1, 1, overwrite=ow)
+    zero = torch.zeros(shape, device=gpu)
+    run(zero, False)
+    junk = torch.randn(shape, device=gpu) * 1e3
+    over = junk.clone()
+    run(over, True)
+    acc = junk.clone()
+    run(acc, False)
+    torch.cuda.synchronize()
+    assert torch.equal(over, zero)
+    assert rel(acc - junk, zero) < 1e-3
