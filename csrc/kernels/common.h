@@ -74,4 +74,27 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return base + i;
 }
 
+// Split-K rows GEMM launches (grid = tiles x 1 x splits) with a multiple of 8 splits place
+// whole splits on one XCD: split z runs on XCD z % 8, so its k-slab of A and B
+// comes from HBM once into that XCD's L2 and every tile of the split reuses it.  With
+// xcd_remap's tile-contiguous placement each k-slab is fetched by every XCD that holds a
+// tile of its row / column (the classifier dgrad, 4 x 4 tiles x 16 splits: 2-4x the HBM
+// bytes; tools/bench_head.py: 74.5 -> 66 us).  Dispatch order is the flattened id
+// L = x + gx * z, XCD = L % 8.  The mapping is a bijection of (x, z), so a wrong guess of
+// the order costs locality, never correctness.  (The split-pixel weight-gradient kernels
+// keep xcd_remap: there the step's autotuned plans came out mixed.)
+__device__ __forceinline__ bool split_major() {
+  return gridDim.z >= 8 && (gridDim.z & 7) == 0 && gridDim.y == 1;
+}
+__device__ __forceinline__ int block_split() {
+  if (!split_major()) return blockIdx.z;
+  const int L = blockIdx.x + gridDim.x * blockIdx.z;
+  return (L & 7) + 8 * ((L >> 3) / gridDim.x);
+}
+__device__ __forceinline__ int block_tile(int tiles_total) {
+  if (!split_major()) return xcd_remap(blockIdx.x, tiles_total);
+  const int L = blockIdx.x + gridDim.x * blockIdx.z;
+  return (L >> 3) % gridDim.x;
+}
+
 }  // namespace mpa

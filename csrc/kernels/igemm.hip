@@ -58,12 +58,12 @@ __global__ __launch_bounds__(256, OCC) void igemm_rows_kernel(IGemmArgs p) {
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  const int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  const int tile = block_tile(p.tiles_total);
   const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
   const int m0 = mt * BM, n0 = nt * BN;
 
   const int ktiles = (p.Ktot + BK - 1) / BK;
-  const int kbeg = blockIdx.z * p.ktiles_per_split;
+  const int kbeg = block_split() * p.ktiles_per_split;
   const int kend = min(ktiles, kbeg + p.ktiles_per_split);
 
   // ---- per-thread A rows (fixed for the whole K loop)

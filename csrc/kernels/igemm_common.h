@@ -187,7 +187,7 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
   const int lane = tid & 63;
   const int nl = (lane >> 4) * 4;
   if constexpr (SPLIT) {
-    float* out = (float*)p.C + (size_t)blockIdx.z * g.M * p.N;
+    float* out = (float*)p.C + (size_t)block_split() * g.M * p.N;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wrow0 + i * 16 + (lane & 15);
@@ -376,7 +376,7 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
         }
       }
       __syncthreads();
-      if (stat_row == 0 && blockIdx.z == 0 && tid < BN && n0 + tid < p.N) {
+      if (stat_row == 0 && block_split() == 0 && tid < BN && n0 + tid < p.N) {
         // start value of the slab reduction that runs after this kernel (no memset)
         p.stats_sums[n0 + tid] = 0.f;
         p.stats_sums[p.N + n0 + tid] = 0.f;

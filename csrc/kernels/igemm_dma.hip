@@ -88,7 +88,7 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  int tile = block_tile(p.tiles_total);
   // merged stride-phase launch: the block's phase sets output geometry, K and taps
   RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow, p.fd_hw, p.fd_ow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
@@ -108,7 +108,7 @@ void igemm_rows_dma_kernel(IGemmArgs p) {
   const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
   const int m0 = mt * BM, n0 = nt * BN;
   const int ktiles = (Ktot + BK - 1) / BK;
-  const int kbeg = blockIdx.z * kps;
+  const int kbeg = block_split() * kps;
   const int kend = min(ktiles, kbeg + kps);
 
   for (int t = tid; t < T; t += NT) {
@@ -285,7 +285,7 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
-  int tile = xcd_remap(blockIdx.x, p.tiles_total);
+  int tile = block_tile(p.tiles_total);
   RowsGeom g{p.M, p.oH, p.oW, p.Poh, p.Pow, p.fd_hw, p.fd_ow};
   int Ktot = p.Ktot, T = p.T, tap0 = 0, kps = p.ktiles_per_split;
   int row_base = 0;  // statistics-slab row of m-tile 0 of this block's phase (dense rows)
@@ -304,7 +304,7 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const int mt = tile / p.tiles_n, nt = tile % p.tiles_n;
   const int m0 = mt * BM, n0 = nt * BN;
   const int ktiles = Ktot / BK;  // aC % 32 == 0 => Ktot % 32 == 0
-  const int kbeg = blockIdx.z * kps;
+  const int kbeg = block_split() * kps;
   const int kend = min(ktiles, kbeg + kps);
   const int aC = p.aC;
 

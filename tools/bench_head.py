@@ -43,10 +43,11 @@ gflop = 2.0 * B * NO * NI / 1e9
 
 rows = [("linear_fwd", lambda: C.linear_fwd(x, w, b, False)),
         ("linear_dgrad", lambda: C.linear_dgrad(dy, w, wt)),
-        ("linear_wgrad", lambda: C.linear_wgrad(dy, x, dw))]
+        ("linear_wgrad", lambda: C.linear_wgrad(dy, x, dw)),
+        ("wgrad_overwr", lambda: C.linear_wgrad(dy, x, dw, overwrite=True))]
 for name, fn in rows:
     t = timeit(fn)
-    print("%-14s %8.1f us  %6.0f TF" % (name, t, gflop / t * 1e-3 * 1e3))
+    print("%-14s %8.1f us  %6.0f TF" % (name, t, gflop / t * 1e3))
 logits = C.linear_fwd(x, w, b, False)[:, :64500]
 loss, lse = C.ce_fwd(logits, labels)
 go = torch.ones(1, device=dev)
@@ -70,6 +71,16 @@ for bm, bn in ((128, 128), (256, 128), (256, 64), (128, 64), (256, 256)):
     print("%3dx%-3d " % (bm, bn) + " | ".join(cells))
 C.igemm_force_tile(0, 0, 0)
 
+print("dgrad sweep (BM x BN / splits, transposed weight): us")
+for bm, bn in ((128, 64), (128, 128), (256, 128), (256, 256), (256, 64)):
+    cells = []
+    for sp in (4, 8, 16, 32, 64):
+        C.igemm_force_tile(bm, bn, sp)
+        cells.append("s%d %6.1f" % (sp, timeit(lambda: C.linear_dgrad(dy, w, wt))))
+    print("%3dx%-3d " % (bm, bn) + " | ".join(cells))
+C.igemm_force_tile(0, 0, 0)
+print("%-14s %8.1f us (auto)" % ("linear_dgrad", timeit(lambda: C.linear_dgrad(dy, w, wt))))
+
 # vendor GEMMs (hipBLASLt through torch) on the same shapes, for comparison
 print("vendor (torch / hipBLASLt):")
 vrows = [("F.linear fwd", lambda: torch.nn.functional.linear(x, w, b.to(torch.bfloat16))),
@@ -82,4 +93,4 @@ except Exception as ex:  # no bf16 -> fp32 mm on this build
 vrows.append(("mm wgrad bf16", lambda: torch.mm(dy.t(), x)))
 for name, fn in vrows:
     t = timeit(fn)
-    print("%-14s %8.1f us  %6.0f TF" % (name, t, gflop / t * 1e-3 * 1e3))
+    print("%-14s %8.1f us  %6.0f TF" % (name, t, gflop / t * 1e3))
