@@ -7,10 +7,11 @@ Design for MI355X / RCCL over xGMI:
 
 * Buckets are cut from the flat fp32 gradient arena (:mod:`.arena`) at parameter
   boundaries, ``bucket_mb`` each (a parameter larger than a bucket gets its own).  The
-  default 16 MiB is sized for the exposed tail: the LAST bucket (layer2..stem) can only
-  start when backward ends, so it is kept small (ResNet-18 @64,500: 126 + 9 + 9.5 + 16 +
-  8.4 MiB), while 8-16 MiB messages still run near RCCL's large-message ring bandwidth
-  on one xGMI link per ring hop.  Since
+  default 16 MiB keeps every bucket's launch close to its last gradient while 8-16 MiB
+  messages still run near RCCL's large-message ring bandwidth on one xGMI link per ring
+  hop (ResNet-18 @64,500: 126 + 9 + 9.5 + 16 + 8.3 MiB + 55 KB).  The final parameters
+  (the stem) get a tiny bucket of their own (``_split_tail``): it is the only collective
+  that can start only when backward ends.  Since
   the arena is in reverse registration order, bucket 0 holds the classifier head, whose
   gradient is produced first; its all-reduce runs under the whole conv backward.
 * Each backward kernel calls ``arena.notify(p)`` after its weight-gradient launch.  When a
@@ -84,7 +85,7 @@ def capped_group(max_ctas: int, device: torch.device):
 class GradBucketer:
     def __init__(self, arena: ParamArena, world_size: int, bucket_mb: float = 16.0,
                  overlap: bool = True, comm_dtype: str = "fp32", group=None,
-                 comm_ctas: Optional[int] = None):
+                 comm_ctas: Optional[int] = None, tail_elems: int = 32768):
         self.arena = arena
         self.world_size = world_size
         self.overlap = overlap
@@ -116,6 +117,7 @@ class GradBucketer:
         if cur:
             self.buckets.append(cur)
             self.ranges.append((start, end))
+        self._split_tail(tail_elems)
         self.bucket_of = {}
         for bi, ps in enumerate(self.buckets):
             for p in ps:
@@ -129,6 +131,29 @@ class GradBucketer:
             if self.comm_ctas > 0 and self.overlap and len(self.buckets) > 1:
                 self.overlap_group = capped_group(self.comm_ctas, arena.device)
         self.reset()
+
+    def _split_tail(self, tail_elems: int) -> None:
+        """Give the last parameters of the arena (the first layers, whose gradients land
+        last - for a ResNet the stem conv + BN, after a ~0.7 ms pool / BN / wgrad backward)
+        a tiny bucket of their own (<= ``tail_elems`` elements), so the bulk of the old last
+        bucket (layer2..layer1, 8.4 MiB for ResNet-18) launches before that stem backward
+        and only a sub-128 KB collective is left exposed after backward."""
+        if tail_elems <= 0 or not self.buckets or len(self.buckets[-1]) < 2:
+            return
+        ps = self.buckets[-1]
+        k, n = len(ps), 0
+        while k > 1:
+            o, e = self.arena.slice_of(ps[k - 1])
+            if n + (e - o) > tail_elems:
+                break
+            n += e - o
+            k -= 1
+        if k == len(ps):
+            return
+        s, e = self.ranges[-1]
+        mid = self.arena.offsets[id(ps[k])]
+        self.buckets[-1:] = [ps[:k], ps[k:]]
+        self.ranges[-1:] = [(s, mid), (mid, e)]
 
     # ------------------------------------------------------------------------------
     def reset(self) -> None:

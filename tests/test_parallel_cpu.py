@@ -153,3 +153,24 @@ def test_watchdog_exits_process_with_stall_code():
                        cwd=root)
     assert r.returncode == 75, (r.returncode, r.stderr[-500:])
     assert "rank 1: no train progress" in r.stderr and "Thread" in r.stderr
+
+
+def test_bucket_layout_resnet18():
+    """GradBucketer on ResNet-18 @64,500: the classifier is bucket 0 (produced first, reduced
+    under the whole conv backward), buckets tile the gradient arena contiguously, and the
+    stem's parameters (their gradients land last, after the pool / BN / stem-wgrad backward)
+    form a tiny final bucket, so layer2..layer1 launch before that stem backward."""
+    from mpi_pytorch_amd.engine import build_model
+    from mpi_pytorch_amd.parallel import World
+    from mpi_pytorch_amd.parallel.ddp import GradBucketer
+    m, _ = build_model("resnet18", 64500, False, torch.device("cpu"), World())
+    a = m._mpa_arena
+    b = GradBucketer(a, 2, 16.0)
+    names = [[a.names[id(p)] for p in ps] for ps in b.buckets]
+    assert names[0] == ["fc.bias", "fc.weight"]
+    assert names[-1] == ["bn1.bias", "bn1.weight", "conv1.weight"]
+    assert b.describe()[-1]["bytes"] < 128 * 1024
+    assert "layer1.0.conv1.weight" in names[-2]
+    assert b.ranges[0][0] == 0 and b.ranges[-1][1] == a.n_train
+    assert all(b.ranges[i][1] == b.ranges[i + 1][0] for i in range(len(b.ranges) - 1))
+    assert sum(len(ps) for ps in b.buckets) == len(a.trainable)
