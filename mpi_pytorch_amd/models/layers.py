@@ -281,7 +281,12 @@ class Linear(nn.Module):
         if in_chw is not None or self.out_store != out_features:
             self.weight._mpa_export = self._exp
             self.weight._mpa_import = self._imp
-        self.weight._mpa_tlayout = (self.out_store, 1, in_features)  # [in][out] copy for dgrad
+        # [in][out] copy for dgrad - except for the wide classifier heads (64,500 classes):
+        # their dgrad (M = batch, N = in, K = 64,512, split-K) reads the forward weight with
+        # transposing LDS loads as fast or faster (tools/bench_head.py: 61.9 vs 65.7 us), and
+        # skipping the copy saves transposing 33 M weights (~24 us) after every update
+        if out_features < 16384:
+            self.weight._mpa_tlayout = (self.out_store, 1, in_features)
         if bias:
             bound = 1 / math.sqrt(in_features)
             b = torch.empty(out_features).uniform_(-bound, bound)

@@ -80,6 +80,8 @@ for bm, bn in ((128, 64), (128, 128), (256, 128), (256, 256), (256, 64)):
     print("%3dx%-3d " % (bm, bn) + " | ".join(cells))
 C.igemm_force_tile(0, 0, 0)
 print("%-14s %8.1f us (auto)" % ("linear_dgrad", timeit(lambda: C.linear_dgrad(dy, w, wt))))
+print("%-14s %8.1f us (auto, forward weight: transposing LDS reads, no [in][out] copy)" % (
+    "linear_dgrad", timeit(lambda: C.linear_dgrad(dy, w))))
 
 # vendor GEMMs (hipBLASLt through torch) on the same shapes, for comparison
 print("vendor (torch / hipBLASLt):")
