@@ -80,6 +80,67 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Padded rows (ld % 8 == 0, 16-B aligned; the 64,500-class head has ld = 64,512): 16-B
+// loads over the whole padded row with columns >= NC masked to -inf, U loads issued before
+// any is consumed.  The unpadded kernel above walked 64,500 columns in 8-B loads, one load
+// per online-LSE step, and streamed ~2.2 TB/s (30 us per 66 MB of logits).
+template <int U>
+__global__ __launch_bounds__(256) void ce_fwd_padded_kernel(const bf16_t* __restrict__ logits,
+                                                             const int64_t* __restrict__ labels,
+                                                             int B, int NC, int ld,
+                                                             float* __restrict__ loss,
+                                                             float* __restrict__ lse_out) {
+  const int row = blockIdx.x;
+  const bf16_t* x = logits + (size_t)row * ld;
+  float m = -INFINITY, s = 0.f;
+  const int nv = ld / 8;
+  for (int i0 = threadIdx.x; i0 < nv; i0 += 256 * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * 256;
+      v[u] = i < nv ? *(const uint4*)(x + (size_t)i * 8) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c0 = (i0 + u * 256) * 8;
+      if (c0 >= NC) continue;
+      float f[8];
+      unpack8(v[u], f);
+      float lm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (c0 + j >= NC) f[j] = -INFINITY;
+        lm = fmaxf(lm, f[j]);
+      }
+      const float mn = fmaxf(m, lm);
+      float acc = s * __expf(m - mn);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += __expf(f[j] - mn);
+      m = mn;
+      s = acc;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    lse_merge(m, s, m2, s2);
+  }
+  __shared__ float sm[4], ss[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; ss[w] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int i = 1; i < 4; ++i) lse_merge(M, S, sm[i], ss[i]);
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const int64_t lab = labels[row];
+    const float picked = (lab >= 0 && lab < NC) ? bf2f(x[lab]) : lse;
+    atomicAdd(loss, (lse - picked) / (float)B);
+  }
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ logits,
                                                       const int64_t* __restrict__ labels,
@@ -146,6 +207,11 @@ __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ 
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s) {
   (void)hipMemsetAsync(loss, 0, sizeof(float), s);
+  if (ld % 8 == 0 && ld >= NC && reinterpret_cast<uintptr_t>(logits) % 16 == 0) {
+    hipLaunchKernelGGL(ce_fwd_padded_kernel<4>, dim3(B), dim3(256), 0, s, logits, labels, B, NC,
+                       ld, loss, lse);
+    return;
+  }
   const int g = NC % 8 == 0 && ld % 8 == 0 ? 8 : (NC % 4 == 0 && ld % 4 == 0 ? 4 : 1);
   if (g == 8)
     hipLaunchKernelGGL(ce_fwd_kernel<8>, dim3(B), dim3(256), 0, s, logits, labels, B, NC, ld, loss,
