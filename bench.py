@@ -86,9 +86,10 @@ def main(argv=None):
                         "to the emulated collective while it is in flight")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")
-    p.add_argument("--timers", action="store_true",
+    p.add_argument("--timers", default="auto", choices=["auto", "on", "off"],
                    help="per-phase HIP-event times of the timed steps (data / forward / backward "
-                        "/ comm_wait / optimizer) as 'phases_ms' in the JSON line")
+                        "/ comm_wait / optimizer) as 'phases_ms' in the JSON line; auto: on for "
+                        "more than one GPU (where comm_wait shows the exposed all-reduce)")
     p.add_argument("--static-data", action="store_true",
                    help="debug: reuse one device batch (no data pipeline in the loop)")
     p.add_argument("--emulate-comm", default="",
@@ -144,7 +145,8 @@ def main(argv=None):
             lazy.append(step(x, y).clone())
         print("lazy losses:", " ".join("%.3f" % float(v) for v in lazy), file=sys.stderr)
         print("loss_sum/steps: %.4f" % step.mean_loss(), file=sys.stderr)
-    if args.timers and not use_graph:
+    timers = args.timers == "on" or (args.timers == "auto" and world.world_size > 1)
+    if timers and not use_graph:
         step.enable_timers()
     torch.cuda.synchronize()
     barrier()

@@ -12,7 +12,7 @@ run() {
   timeout -k 10 180 python bench.py --steps 20 --warmup 5 "$@" 2>/dev/null | tail -1 >> $out || exit 1
   tail -1 $out | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$*', d['ms_per_step'], d.get('phases_ms',''))"
 }
-run --timers
+run --timers on
 run
 for spec in "8:2000" "8:6000" "32:2000" "32:6000"; do
   b=${spec%%:*}
