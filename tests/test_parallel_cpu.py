@@ -111,16 +111,20 @@ def _single(out_dir):
     return grad, m._mpa_arena.master.clone()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-def test_dp_equivalence_gloo(overlap):
+@pytest.mark.parametrize("world,overlap", [(2, True), (2, False), (4, True)])
+def test_dp_equivalence_gloo(world, overlap):
+    """DP over gloo == one process on the whole batch (mean of equal-size per-rank means is
+    the global mean), with the bucketed overlapped all-reduce; world 4 rehearses more ranks
+    than the one-GPU box can hold."""
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, _free_port(), d, overlap), nprocs=2, join=True,
-                           start_method="spawn")
-        r0 = torch.load(os.path.join(d, "r0.pt"))
-        r1 = torch.load(os.path.join(d, "r1.pt"))
+        mp.start_processes(_worker, args=(world, _free_port(), d, overlap), nprocs=world,
+                           join=True, start_method="spawn")
+        rs = [torch.load(os.path.join(d, "r%d.pt" % r)) for r in range(world)]
+        r0 = rs[0]
         # broadcast made replicas identical, and they stay identical
-        assert torch.equal(r0["init"], r1["init"])
-        assert torch.equal(r0["final"], r1["final"])
+        for r in rs[1:]:
+            assert torch.equal(r0["init"], r["init"])
+            assert torch.equal(r0["final"], r["final"])
         grad, final = _single(d)
         assert torch.allclose(r0["grad"], grad, atol=1e-5, rtol=1e-4)
         assert torch.allclose(r0["final"], final, atol=1e-5, rtol=1e-4)
