@@ -68,8 +68,10 @@ def main(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=512,
-                   help="per-GPU batch (profiles/batch_sweep_r18.txt: 256 -> 29.5k, 512 -> 34.0k img/s)")
+    p.add_argument("--batch", type=int, default=1024,
+                   help="per-GPU batch (profiles/batch_sweep_r2.txt: 512 -> 42.9k, 1024 -> 47.1-48.1k, "
+                        "2048 -> 50.5k img/s; 1024 keeps a 21 ms step and halves the all-reduce's "
+                        "share of a data-parallel step)")
     p.add_argument("--model", default="resnet18")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--classes", type=int, default=64500)
