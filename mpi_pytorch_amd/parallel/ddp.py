@@ -128,7 +128,9 @@ class GradBucketer:
         self.active = world_size > 1
         if self.active:
             arena.add_listener(self._on_grad)
-            if self.comm_ctas > 0 and self.overlap and len(self.buckets) > 1:
+            # (the capped communicator spans the whole world: only for the default group)
+            if (self.comm_ctas > 0 and self.overlap and len(self.buckets) > 1
+                    and self.group is None):
                 self.overlap_group = capped_group(self.comm_ctas, arena.device)
         self.reset()
 
