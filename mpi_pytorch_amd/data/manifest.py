@@ -21,6 +21,7 @@ from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
+import torch
 
 try:
     import pandas as pd
@@ -66,10 +67,27 @@ class SyntheticImages:
         if out is None:
             out = np.empty((len(names), H, W, 3), dtype=np.uint8)
         for i, n in enumerate(names):
-            h = zlib.crc32(str(n).encode())
-            r, c = h % H, (h // H) % W
+            r, c = self._offset(n)
             out[i] = self.tex[r:r + H, c:c + W]
         return out
+
+    def _offset(self, name) -> Tuple[int, int]:
+        H, W = self.hw
+        h = zlib.crc32(str(name).encode())
+        return h % H, (h // H) % W
+
+    def load_device(self, names: Sequence[str], device) -> torch.Tensor:
+        """``load(names)`` produced on ``device`` as one gather from a device copy of the
+        texture (bitwise the same images): the training driver's synthetic batches then
+        cost no host copy, pinning or H2D transfer."""
+        device = torch.device(device)
+        if getattr(self, "_tex_dev", None) is None or self._tex_dev.device != device:
+            self._tex_dev = torch.from_numpy(self.tex).to(device)
+        H, W = self.hw
+        rc = torch.tensor([self._offset(n) for n in names], dtype=torch.int64).to(device)
+        rows = (rc[:, 0:1] + torch.arange(H, device=device))[:, :, None]
+        cols = (rc[:, 1:2] + torch.arange(W, device=device))[:, None, :]
+        return self._tex_dev[rows, cols]
 
 
 class FolderImages:

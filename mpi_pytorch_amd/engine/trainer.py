@@ -79,10 +79,21 @@ class ManifestBatches:
 
     def _host(self, idx):
         names = [self.names[i] for i in idx]
+        if self._device_synth:  # images are gathered on the GPU in _to_device
+            return names, torch.from_numpy(self.labels[idx])
         return self.source.load(names), torch.from_numpy(self.labels[idx])
+
+    @property
+    def _device_synth(self) -> bool:
+        return self.device.type == "cuda" and isinstance(self.source, SyntheticImages)
 
     def _to_device(self, imgs, labels):
         cuda = self.device.type == "cuda"
+        if self._device_synth:
+            imgs = self.source.load_device(imgs, self.device)
+            x = Fn.preprocess(imgs, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
+                              self.cpad, out_dtype=torch.float32, pad=self.pad)
+            return x, labels.to(self.device, non_blocking=True)
         if isinstance(imgs, np.ndarray):
             groups = [torch.from_numpy(imgs)]
         else:

@@ -178,3 +178,15 @@ def test_launcher_fail_fast(tmp_path):
     t = time.time()
     rc = launch(2, [sys.executable, str(script)])
     assert rc == 3 and time.time() - t < 30
+
+
+def test_synthetic_images_device_gather_matches_host():
+    """SyntheticImages.load_device (the training driver's GPU-side synthetic batches) gives
+    bitwise the host load's images (checked on the CPU device here)."""
+    from mpi_pytorch_amd.data.manifest import SyntheticImages
+    src = SyntheticImages((37, 23), seed=3)
+    names = ["img_%d.jpg" % i for i in range(11)]
+    host = src.load(names)
+    dev = src.load_device(names, "cpu")
+    assert dev.dtype == torch.uint8 and tuple(dev.shape) == host.shape
+    assert np.array_equal(dev.numpy(), host)
