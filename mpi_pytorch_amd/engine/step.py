@@ -71,7 +71,9 @@ class StepTimer:
     PHASES = ("data", "forward", "backward", "comm_wait", "optimizer")
     _MAX_PENDING = 64
 
-    def __init__(self):
+    def __init__(self, event_factory=None):
+        # HIP timing events; a stand-in factory lets the bookkeeping be tested on the CPU
+        self._event = event_factory or (lambda: torch.cuda.Event(enable_timing=True))
         self._pending = []
         self._cur = None
         self.reset()
@@ -83,7 +85,7 @@ class StepTimer:
         self._last_end = None  # e.g. an epoch's checkpoint / validation is no data time
 
     def mark(self, i: int) -> None:
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = self._event()
         ev.record()
         if i == 0:
             self._cur = [self._last_end, ev]

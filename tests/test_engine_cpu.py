@@ -190,3 +190,40 @@ def test_synthetic_images_device_gather_matches_host():
     dev = src.load_device(names, "cpu")
     assert dev.dtype == torch.uint8 and tuple(dev.shape) == host.shape
     assert np.array_equal(dev.numpy(), host)
+
+
+def test_step_timer_bookkeeping():
+    """StepTimer phase accounting with stand-in events on a fake clock: per-phase means,
+    'data' only between consecutive steps, lazy resolution past _MAX_PENDING steps, and
+    reset (which also forgets the previous step's end)."""
+    from mpi_pytorch_amd.engine.step import StepTimer
+    clock = [0.0]
+
+    class Ev:
+        def record(self):
+            self.t = clock[0]
+
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    t = StepTimer(event_factory=Ev)
+    durs = [1.0, 2.0, 3.0, 0.5, 0.25]  # gap before the step, forward, backward, comm, opt
+    n = StepTimer._MAX_PENDING + 5
+    for _ in range(n):
+        clock[0] += durs[0]
+        for i, d in enumerate(durs[1:]):
+            t.mark(i)
+            clock[0] += d
+        t.mark(4)
+    s = t.summary()
+    assert s["steps"] == n
+    assert s["forward"] == 2.0 and s["backward"] == 3.0
+    assert s["comm_wait"] == 0.5 and s["optimizer"] == 0.25 and s["data"] == 1.0
+    assert s["step"] == 6.75
+    clock[0] += 100.0  # e.g. checkpoint + validation between epochs: not data time
+    t.mark(0); t.mark(1); t.mark(2); t.mark(3); t.mark(4)
+    s = t.summary()
+    assert s["steps"] == 1 and s["data"] == 0.0
