@@ -63,9 +63,13 @@ def _emulate_comm(model, step, spec, dev, reserve=0):
     step.bucketer.finish = finish
 
 
-def main(argv=None):
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU).  Without a launcher environment (WORLD_SIZE unset) "
+                        "bench.py spawns them itself through mpi_pytorch_amd.launch")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: plumbing check of the same code path on host ops (gloo for N>1)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=1024,
@@ -100,18 +104,48 @@ def main(argv=None):
                         "data-parallel all-reduce overlapping backward); the optimizer waits "
                         "for it like for the real collective")
     args = p.parse_args(argv)
+    return args
 
-    from mpi_pytorch_amd.parallel import init_world, barrier, get_world
+
+def _launcher_env() -> bool:
+    """True when a launcher (torchrun, our launch.py, an MPI launcher) already made us a
+    rank of an N-process job."""
+    return any(os.environ.get(k) for k in ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE"))
+
+
+def spawn(argv, nprocs: int) -> int:
+    """``python bench.py --gpus N`` outside a launcher: start N rank processes of this very
+    script (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR=127.0.0.1 set by
+    ``mpi_pytorch_amd.launch``), fail fast if one dies, and return the job's exit code.
+    Nothing here touches the GPU: the parent only waits for its children."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_mpa_launch", os.path.join(ROOT, "mpi_pytorch_amd", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.launch(nprocs, [sys.executable, os.path.abspath(__file__)] + list(argv))
+
+
+def run(args) -> None:
+    from mpi_pytorch_amd.parallel import init_world, barrier
     from mpi_pytorch_amd.engine import build_training
+    from mpi_pytorch_amd.engine.step import markers
     from mpi_pytorch_amd.data import DevicePrefetcher
     from mpi_pytorch_amd.models import input_spec
 
-    world = init_world("cuda")
-    if world.world_size != args.gpus and world.rank == 0:
-        print("warning: --gpus {} but WORLD_SIZE {}".format(args.gpus, world.world_size),
-              file=sys.stderr)
+    cuda = args.device == "cuda"
+    timers = args.timers == "on" or (args.timers == "auto" and args.gpus > 1)
+    world = init_world(args.device, comm_timing=timers and cuda)
+    if world.world_size != args.gpus:
+        raise SystemExit("bench.py: --gpus {} but this job has {} ranks".format(
+            args.gpus, world.world_size))
     torch.manual_seed(0)
     dev = world.device
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
     hw = (args.image_size, args.image_size)
     model, opt, step, _ = build_training(args.model, args.classes, dev, world, args.lr,
                                          args.optimizer, bucket_mb=args.bucket_mb,
@@ -128,7 +162,7 @@ def main(argv=None):
         _emulate_comm(model, step, args.emulate_comm, dev, args.comm_reserve)
     # eager by default: the step is GPU-bound (host runs ahead), graph replay buys nothing
     # measurable and needs a per-step sync for correctness (engine/step.py)
-    use_graph = args.graph == "on"
+    use_graph = args.graph == "on" and cuda
     if use_graph:
         x, y = data.next()
         use_graph = step.capture(x, y)
@@ -147,22 +181,30 @@ def main(argv=None):
             lazy.append(step(x, y).clone())
         print("lazy losses:", " ".join("%.3f" % float(v) for v in lazy), file=sys.stderr)
         print("loss_sum/steps: %.4f" % step.mean_loss(), file=sys.stderr)
-    timers = args.timers == "on" or (args.timers == "auto" and world.world_size > 1)
     if timers and not use_graph:
         step.enable_timers()
-    torch.cuda.synchronize()
+    if timers:
+        step.bucketer.enable_comm_stats()
+    mk = step.markers
+    step.mean_loss()  # the reported loss is the timed steps' mean
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if mk is not None:
+            mk.range_push("data")
         x, y = data.next()
+        if mk is not None:
+            mk.range_pop()
         step(x, y)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     loss = step.mean_loss()
     phases = step.timer.summary() if step.timer is not None else None
+    comm = step.bucketer.comm_stats()
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world.world_size > 1:
         import torch.distributed as dist
@@ -182,7 +224,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_IMG_S, 2),
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic",
             "config": {
                 "model": args.model,
@@ -193,18 +235,31 @@ def main(argv=None):
                 "num_classes": args.classes,
                 "optimizer": args.optimizer,
                 "parallelism": "dp{}".format(world.world_size),
+                "device": args.device,
+                "backend": world.backend,
                 "hip_graph": bool(use_graph),
                 "mean_loss": round(loss, 4),
             },
         }
         if phases is not None:
             rec["phases_ms"] = phases
-            rec["grad_allreduce_mb"] = round(
-                sum(b["bytes"] for b in step.bucketer.describe()) / 2**20, 2)
+        if world.world_size > 1:
+            rec["grad_allreduce_mb"] = step.bucketer.wire_mb()
+            rec["comm_ctas"] = step.bucketer.comm_ctas if step.bucketer.overlap_group else 0
+        if comm is not None:
+            rec["comm"] = comm
         print(json.dumps(rec), flush=True)
     data.close()
     from mpi_pytorch_amd.parallel import shutdown
     shutdown()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus > 1 and not _launcher_env():
+        sys.exit(spawn(argv, args.gpus))
+    run(args)
 
 
 if __name__ == "__main__":

@@ -562,6 +562,10 @@ struct TunedTile {
 };
 static std::mutex g_tune_mu;
 static std::map<std::string, TunedTile> g_tuned;
+// held for a whole tuning pass (scratch growth + candidate launches + timing): a second
+// host thread tuning on the same device must not free the scratch buffer that this
+// thread's candidate kernels are still writing
+static std::mutex g_tune_pass_mu;
 
 static bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -760,6 +764,8 @@ static void tuned_rows_tile(const IGemmArgs& a, bool bkc, int vw, bool allow_spl
   if (!g_tune || (g_force_bm && g_force_bn) || a.M <= 0 || stream_capturing(s)) return;
   const std::string key = rows_key(a, bkc, allow_split);
   if (tuned_lookup(key, tbm, tbn)) return;
+  std::lock_guard<std::mutex> pass(g_tune_pass_mu);
+  if (tuned_lookup(key, tbm, tbn)) return;  // tuned by another thread meanwhile
   const int64_t ws_cap = allow_split ? igemm_ws_floats(a.M, a.N, a.Ktot) : 0;
   const int64_t cbytes = ((int64_t)a.M * std::max(a.ldc, a.N) * 2 + 255) / 256 * 256;
   const int64_t sbytes = (igemm_slab_floats(a.M, a.N) + 2 * a.N) * 4;
@@ -940,7 +946,9 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
     int tbm = 0, tbn = 0;
     if (g_tune && !(g_force_bm && g_force_bn) && !stream_capturing(s)) {
       const std::string key = rows_key(a, bkc, false);
-      if (!tuned_lookup(key, tbm, tbn)) {  // time the merged launch per candidate tile
+      std::unique_lock<std::mutex> pass(g_tune_pass_mu, std::defer_lock);
+      if (!tuned_lookup(key, tbm, tbn) && (pass.lock(), !tuned_lookup(key, tbm, tbn))) {
+        // time the merged launch per candidate tile
         const int64_t hw0 = std::max(1, a.ph[0].oH * a.ph[0].oW);
         const int64_t rows = (a.ph[0].M + hw0 - 1) / hw0 * a.dH * a.dW;  // dx pixels
         const int64_t cbytes = rows * std::max(a.ldc, a.N) * 2;
@@ -1079,6 +1087,8 @@ static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s
   snprintf(k, sizeof k, "wgrad K%d N%d P%d x%dx%dx%d o%dx%d f%dx%d s%d,%d p%d,%d", a.Kout, a.Ncols,
            a.Mpix, a.H, a.W, a.C, a.P, a.Q, a.R, a.S, a.sh, a.sw, a.ph, a.pw);
   const std::string key(k);
+  if (tuned_lookup(key, tbm, tbn)) return;
+  std::lock_guard<std::mutex> pass(g_tune_pass_mu);
   if (tuned_lookup(key, tbm, tbn)) return;
   const int64_t out = (int64_t)a.Kout * a.Ncols;
   const int64_t cap = igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix);

@@ -54,6 +54,28 @@ def loss_fn(out, labels):
     return Fn.cross_entropy(out, labels)
 
 
+class _NoMarkers:
+    """roctx stand-in on hosts without the native extension (CPU runs)."""
+
+    def range_push(self, name: str) -> int:
+        return 0
+
+    def range_pop(self) -> int:
+        return 0
+
+    def mark(self, name: str) -> None:
+        pass
+
+
+def markers():
+    """The roctx API of the native extension (``range_push`` / ``range_pop`` / ``mark``,
+    csrc/runtime/runtime.cpp) - or a no-op stand-in when it is not built (CPU)."""
+    from ..ops import _ext
+    if torch.cuda.is_available() and _ext.available():
+        return _ext.ext()
+    return _NoMarkers()
+
+
 class StepTimer:
     """Per-step phase times from HIP events on the compute stream:
 
@@ -145,6 +167,9 @@ class TrainStep:
         # syncs after each replay unless MPA_GRAPH_UNSAFE=1.
         self._sync_replay = os.environ.get("MPA_GRAPH_UNSAFE", "0") != "1"
         self.timer: Optional[StepTimer] = None
+        # roctx ranges fwd / bwd / comm_wait / opt around the host enqueue of each phase
+        # (rocprofv3 --marker-trace shows them beside the kernels); MPA_ROCTX=1
+        self.markers = markers() if os.environ.get("MPA_ROCTX", "0") == "1" else None
 
     def enable_timers(self) -> StepTimer:
         """Turn on per-phase HIP-event timing of eager steps (GPU only)."""
@@ -154,22 +179,36 @@ class TrainStep:
 
     def _eager(self, x, y):
         t = self.timer if self._graph is None else None
+        m = self.markers
         if t is not None:
             t.mark(0)
+        if m is not None:
+            m.range_push("fwd")
         self.arena.zero_grad()
         out = self.model(x)
         loss = loss_fn(out, y)
         if t is not None:
             t.mark(1)
+        if m is not None:
+            m.range_pop()
+            m.range_push("bwd")
         loss.backward()
         if t is not None:
             t.mark(2)
+        if m is not None:
+            m.range_pop()
+            m.range_push("comm_wait")
         self.bucketer.finish()
         if t is not None:
             t.mark(3)
+        if m is not None:
+            m.range_pop()
+            m.range_push("opt")
         self.opt.step()
         if t is not None:
             t.mark(4)
+        if m is not None:
+            m.range_pop()
         return loss.detach()
 
     def __call__(self, x, y) -> torch.Tensor:

@@ -38,9 +38,10 @@ from ..data.manifest import (read_manifests, synthetic_manifest, SyntheticImages
 from ..data.loader import IMAGENET_MEAN, IMAGENET_STD
 from ..ops import functional as Fn
 from ..parallel import (init_world, get_world, barrier, scatter_object, broadcast_object,
+                        all_gather_object,
                         shard_dataframe, array_split_sizes, replica_checksum)
 from ..parallel.sharding import equal_step_count
-from ..utils.logging import init_logger, MetricsWriter
+from ..utils.logging import init_logger, MetricsWriter, log_rank_lines
 from .step import build_training
 from ..models import input_spec
 
@@ -131,7 +132,7 @@ def _image_source(cfg: Config, names: Sequence[str], src_hw):
 
 
 def run_training(cfg: Config) -> dict:
-    world = init_world(cfg.device, cfg.timeout_s)
+    world = init_world(cfg.device, cfg.timeout_s, comm_timing=cfg.step_timers)
     rank, size = world.rank, world.world_size
     log = init_logger(rank, cfg.log_file, cfg.log_per_rank_files)
     metrics = MetricsWriter(cfg.metrics_jsonl, rank)
@@ -201,6 +202,7 @@ def run_training(cfg: Config) -> dict:
 
     if cfg.step_timers:
         step.enable_timers()
+        step.bucketer.enable_comm_stats()
     history = []
     # fail fast on a stalled rank (e.g. a peer died inside a collective): SURVEY.md §5.3
     dog = Watchdog(cfg.watchdog_s, rank=rank).start()
@@ -215,23 +217,35 @@ def run_training(cfg: Config) -> dict:
             step(x, y)
             nimg += x.shape[0]
             gstep += 1
-            dog.beat(gstep)
+            if dev.type == "cuda":
+                # progress = the step's kernels COMPLETED on the device, not enqueued
+                ev = torch.cuda.Event()
+                ev.record()
+                dog.beat_on(gstep, ev)
+            else:
+                dog.beat(gstep)
         tr_loss = step.mean_loss()
-        dog.beat(gstep)
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        dog.beat(gstep)
         dt = time.perf_counter() - t0
-        log.info("_Epoch: {} | Train Loss: {} | Time: {}".format(epoch, tr_loss, dt))
+        log_rank_lines(log, "_Epoch: {} | Train Loss: {} | Time: {}".format(epoch, tr_loss, dt),
+                       rank, size, all_gather_object, cfg.log_per_rank_files)
         rec = {"epoch": epoch, "train_loss": tr_loss, "time_s": dt,
                "img_per_s_rank": nimg / dt if dt > 0 else 0.0,
                "img_per_s_global": nimg * size / dt if dt > 0 else 0.0}
         if step.timer is not None:
-            rec["phase_ms"] = step.timer.summary()
-            if size > 1:
-                rec["grad_allreduce_mb"] = round(
-                    sum(b["bytes"] for b in step.bucketer.describe()) / 2**20, 2)
+            rec["phases_ms"] = step.timer.summary()
+        if size > 1:
+            rec["grad_allreduce_mb"] = step.bucketer.wire_mb()
+            cs = step.bucketer.comm_stats()
+            if cs is not None:
+                rec["comm"] = cs
         if cfg.checksum_every and size > 1:
             rec["replicas_consistent"] = replica_checksum(model)
+        # rank 0 checkpoints and validates while the others wait at the next collective:
+        # no rank's deadline runs until everyone is past the epoch-end work
+        dog.pause()
         if rank == 0:
             log.info("_Creating a checkpoint at epoch {}".format(epoch))
             save_checkpoint(build_state(epoch, model, opt, tr_loss), epoch, cfg.MODEL_NAME,
@@ -244,7 +258,9 @@ def run_training(cfg: Config) -> dict:
                 log.info("_Epoch: {} | Acc: {}".format(epoch, acc))
         metrics.write(**rec)
         history.append(rec)
-        dog.beat(gstep)
+        if size > 1:
+            barrier()
+        dog.resume()
     dog.stop()
     return {"history": history, "checkpoint": ckpt}
 

@@ -151,6 +151,9 @@ class ParamArena:
         self._listeners.append(fn)
 
     def notify(self, p: nn.Parameter) -> None:
+        # whatever wrote p's gradient, it is no longer all zeros: a later kernel for the
+        # same parameter (tied weights, a second use) must accumulate, not overwrite
+        self._fresh.discard(id(p))
         for fn in self._listeners:
             fn(p)
 

@@ -35,6 +35,7 @@ Design for MI355X / RCCL over xGMI:
 from __future__ import annotations
 
 import os
+import time
 from typing import List, Optional
 
 import torch
@@ -64,6 +65,7 @@ def capped_group(max_ctas: int, device: torch.device):
     rank must make it."""
     if device.type != "cuda" or dist.get_backend() != "nccl":
         return None
+    g, err = None, None
     try:
         opts = dist.ProcessGroupNCCL.Options()
         opts.config.max_ctas = int(max_ctas)
@@ -74,12 +76,23 @@ def capped_group(max_ctas: int, device: torch.device):
         torch.cuda.synchronize(device)
         if float(probe[0]) != float(dist.get_world_size()):
             raise RuntimeError("capped communicator returned %s" % float(probe[0]))
+    except Exception as ex:
+        err = ex
+    # every rank must agree: a rank sending its overlapped buckets to the default group
+    # while the others use the capped one would never match its collectives
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
         return g
-    except Exception as ex:  # keep the default communicator, uncapped grids
-        import sys
-        print("GradBucketer: no CTA-capped communicator (%s); overlapped buckets use the "
-              "default one" % ex, file=sys.stderr)
-        return None
+    import sys
+    print("GradBucketer: no CTA-capped communicator (%s); overlapped buckets use the "
+          "default one" % (err or "failed on another rank"), file=sys.stderr)
+    if g is not None:
+        try:
+            dist.destroy_process_group(g)
+        except Exception:
+            pass
+    return None
 
 
 class GradBucketer:
@@ -125,6 +138,7 @@ class GradBucketer:
         self._pending = [0] * len(self.buckets)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._wire: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
+        self._stats: Optional[list] = None  # (bucket, wire bytes, work, host t0, host t1)
         self.active = world_size > 1
         if self.active:
             arena.add_listener(self._on_grad)
@@ -186,13 +200,12 @@ class GradBucketer:
                 _set_reserve(self.comm_ctas)
                 self._reserved = True
         if self.comm_dtype == "bf16" and g.is_cuda:
-            w = g.to(torch.bfloat16)
-            self._wire[bi] = w
-            self._works[bi] = dist.all_reduce(w, op=dist.ReduceOp.SUM, group=group,
-                                              async_op=True)
-        else:
-            self._works[bi] = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group,
-                                              async_op=True)
+            g = g.to(torch.bfloat16)
+            self._wire[bi] = g
+        self._works[bi] = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        if self._stats is not None and len(self._stats) < self._MAX_STATS:
+            self._stats.append([bi, g.numel() * g.element_size(), self._works[bi],
+                                time.perf_counter(), None])
 
     def finish(self) -> None:
         """Issue any bucket not yet launched, then make the compute stream wait for all."""
@@ -205,6 +218,12 @@ class GradBucketer:
             w = self._works[bi]
             if w is not None:
                 w.wait()
+                if self._stats is not None and not self.arena.grad.is_cuda:
+                    # host backends: wait() returned when the collective did
+                    for rec in self._stats[::-1]:
+                        if rec[2] is w:
+                            rec[4] = time.perf_counter()
+                            break
             if self._wire[bi] is not None:
                 s, e = self.ranges[bi]
                 self.arena.grad[s:e].copy_(self._wire[bi])
@@ -219,7 +238,73 @@ class GradBucketer:
     def grad_scale(self) -> float:
         return 1.0 / self.world_size
 
+    @property
+    def wire_elem_bytes(self) -> int:
+        return 2 if (self.comm_dtype == "bf16" and self.arena.grad.is_cuda) else 4
+
     def describe(self) -> List[dict]:
+        """Bucket layout; ``bytes`` is what each all-reduce actually sends (wire dtype)."""
         return [{"bucket": i, "params": len(ps), "numel": r[1] - r[0],
-                 "bytes": (r[1] - r[0]) * 4}
+                 "bytes": (r[1] - r[0]) * self.wire_elem_bytes}
                 for i, (ps, r) in enumerate(zip(self.buckets, self.ranges))]
+
+    def wire_mb(self) -> float:
+        return round(sum(b["bytes"] for b in self.describe()) / 2**20, 2)
+
+    # ------------------------------------------------------------------ comm statistics
+    _MAX_STATS = 8192
+
+    def enable_comm_stats(self) -> None:
+        """Record every bucket all-reduce of the following steps for :meth:`comm_stats`.
+
+        RCCL: the collective's own duration on its stream, from the start/end events
+        ProcessGroupNCCL records when ``TORCH_NCCL_ENABLE_TIMING=1`` was set before the
+        process group came up (``Work._get_duration``).  Host backends (gloo): launch to
+        completion of ``wait()``.  Nothing is synchronised until :meth:`comm_stats`."""
+        if self.active:
+            self._stats = []
+
+    def comm_stats(self, reset: bool = True) -> Optional[dict]:
+        """Per-bucket mean all-reduce time, algorithm and bus bandwidth (ring all-reduce:
+        busbw = algbw * 2(n-1)/n, the per-link rate nccl-tests reports), plus the totals
+        per step.  Call after the device has been synchronised."""
+        if self._stats is None:
+            return None
+        n = self.world_size
+        per = {}
+        for bi, nbytes, work, t0, t1 in self._stats:
+            ms = None
+            if t1 is not None:
+                ms = (t1 - t0) * 1e3
+            else:
+                try:
+                    ms = float(work._get_duration())
+                except Exception:
+                    ms = None
+            d = per.setdefault(bi, {"bucket": bi, "bytes": nbytes, "ms": [], "n": 0})
+            d["n"] += 1
+            if ms is not None and ms > 0:
+                d["ms"].append(ms)
+        out = []
+        tot_ms, tot_bytes, steps = 0.0, 0, 0
+        for bi in sorted(per):
+            d = per[bi]
+            rec = {"bucket": bi, "mb": round(d["bytes"] / 2**20, 3), "calls": d["n"]}
+            if d["ms"]:
+                ms = sum(d["ms"]) / len(d["ms"])
+                algbw = d["bytes"] / (ms * 1e-3) / 1e9
+                rec.update(ms=round(ms, 4), algbw_gbs=round(algbw, 2),
+                           busbw_gbs=round(algbw * 2.0 * (n - 1) / n, 2))
+                tot_ms += ms
+            tot_bytes += d["bytes"]
+            steps = max(steps, d["n"])
+            out.append(rec)
+        if reset:
+            self._stats = []
+        res = {"world": n, "steps": steps, "buckets": out,
+               "mb_per_step": round(tot_bytes / 2**20, 2),
+               "timed": any("ms" in r for r in out)}
+        if res["timed"]:
+            res["sum_ms_per_step"] = round(tot_ms, 4)
+            res["busbw_gbs"] = round(tot_bytes / (tot_ms * 1e-3) / 1e9 * 2.0 * (n - 1) / n, 2)
+        return res

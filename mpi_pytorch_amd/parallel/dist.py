@@ -57,8 +57,13 @@ def env_rank_info():
 
 
 def init_world(device: str = "auto", timeout_s: float = 1800.0,
-               backend: Optional[str] = None) -> World:
-    """Initialise (idempotently) the process group and pick this rank's device."""
+               backend: Optional[str] = None, comm_timing: bool = False) -> World:
+    """Initialise (idempotently) the process group and pick this rank's device.
+
+    ``comm_timing``: have ProcessGroupNCCL record start/end events around every
+    collective (``TORCH_NCCL_ENABLE_TIMING``), read back by ``GradBucketer.comm_stats``."""
+    if comm_timing:
+        os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     global _WORLD
     if _WORLD is not None:
         return _WORLD

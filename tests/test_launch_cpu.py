@@ -1,0 +1,148 @@
+"""Multi-process launch paths on the CPU (gloo): bench.py's own rank spawning, the
+training driver at world size 2 (per-rank epoch lines in one log), and the watchdog's
+device-completion beats.  Reference: ``mpiexec -n N python -m mpi4py main.py``
+(``/root/reference/README.md:38``), per-rank epoch lines (``main.py:159-160``)."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def test_bench_spawns_ranks_itself(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher environment starts 2 ranks itself and
+    rank 0 prints exactly one JSON line with n_gpus 2 and the per-bucket comm stats."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--image-size", "32", "--batch", "2", "--classes", "10", "--steps", "2",
+           "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=_env(), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["global_batch"] == 4
+    assert rec["steps"] == 2 and rec["warmup"] == 1
+    comm = rec["comm"]
+    assert comm["world"] == 2 and comm["timed"]
+    assert len(comm["buckets"]) >= 2 and all(b["calls"] == 2 for b in comm["buckets"])
+    assert rec["grad_allreduce_mb"] == pytest.approx(comm["mb_per_step"], rel=1e-3)
+    assert "phases_ms" not in rec  # host runs have no HIP-event timers
+
+
+def test_bench_rejects_rank_count_mismatch(tmp_path):
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--image-size", "32", "--batch", "2", "--classes", "10", "--steps", "1",
+           "--warmup", "0"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0 and "ranks" in (r.stderr + r.stdout)
+
+
+def test_training_driver_two_ranks_logs_every_rank(tmp_path):
+    """main.py under the launcher at world size 2: the shared training.log holds both
+    ranks' epoch lines, each with its own rank tag, written whole by rank 0."""
+    log = tmp_path / "training.log"
+    cmd = [sys.executable, "-m", "mpi_pytorch_amd.launch", "-n", "2", "--timeout", "500",
+           os.path.join(ROOT, "main.py"), "--device", "cpu", "--synthetic_images", "16",
+           "--image_size", "32", "--NUM_EPOCHS", "2", "--BATCH_SIZE", "4",
+           "--NUM_CLASSES", "10", "--VALIDATE", "false", "--log_file", str(log),
+           "--CHECKPOINT_DIR", str(tmp_path) + "/ck/", "--step_timers", "true",
+           "--metrics_jsonl", str(tmp_path / "m.jsonl")]
+    env = _env()
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    text = log.read_text()
+    for e in (0, 1):
+        for rk in (0, 1):
+            assert "INFO:Herbarium_R{}:_Epoch: {} | Train Loss: ".format(rk, e) in text, text
+    assert "_Files Received: 8" in text
+    recs = [json.loads(l) for l in (tmp_path / "m.jsonl").read_text().splitlines()]
+    assert {r_["rank"] for r_ in recs} == {0, 1}
+    assert all(r_["comm"]["world"] == 2 for r_ in recs)
+
+
+class _StalledEvent:
+    """A device event that never completes (a GPU stuck in a collective)."""
+
+    def query(self):
+        return False
+
+
+class _DoneEvent:
+    def query(self):
+        return True
+
+
+def test_watchdog_fires_on_stalled_device_while_host_enqueues():
+    from mpi_pytorch_amd.parallel.watchdog import Watchdog
+    hits = []
+    dog = Watchdog(0.3, rank=1, on_timeout=hits.append, poll_s=0.02).start()
+    # the host keeps enqueuing steps (what an async GPU loop does) - none completes
+    t0 = time.monotonic()
+    step = 0
+    while time.monotonic() - t0 < 1.0 and not hits:
+        step += 1
+        dog.beat_on(step, _StalledEvent())
+        time.sleep(0.005)
+    dog.stop()
+    assert hits and "rank 1" in hits[0]
+    assert dog.pending_events() <= Watchdog._MAX_EVENTS + 1
+
+
+def test_watchdog_counts_completed_device_steps():
+    from mpi_pytorch_amd.parallel.watchdog import Watchdog
+    hits = []
+    dog = Watchdog(0.3, rank=0, on_timeout=hits.append, poll_s=0.02).start()
+    t0 = time.monotonic()
+    step = 0
+    while time.monotonic() - t0 < 0.8:
+        step += 1
+        dog.beat_on(step, _DoneEvent())
+        time.sleep(0.01)
+    time.sleep(0.05)
+    assert not hits and dog._step == step
+    # paused: no deadline during the epoch-end checkpoint / validation
+    dog.pause()
+    time.sleep(0.5)
+    assert not hits
+    dog.resume()
+    time.sleep(0.1)
+    assert not hits
+    dog.stop()
+
+
+def test_log_rank_lines_tags_each_rank(tmp_path):
+    from mpi_pytorch_amd.utils.logging import init_logger, log_rank_lines
+    path = tmp_path / "t.log"
+    log = init_logger(0, str(path), stream=False)
+    log_rank_lines(log, "_Epoch: 0 | Train Loss: 1.0 | Time: 2.0", 0, 3,
+                   gather=lambda m: [m, m.replace("2.0", "5.0"), m.replace("2.0", "6.0")])
+    log.info("after")
+    lines = path.read_text().splitlines()
+    assert lines == ["INFO:Herbarium_R0:_Epoch: 0 | Train Loss: 1.0 | Time: 2.0",
+                     "INFO:Herbarium_R1:_Epoch: 0 | Train Loss: 1.0 | Time: 5.0",
+                     "INFO:Herbarium_R2:_Epoch: 0 | Train Loss: 1.0 | Time: 6.0",
+                     "INFO:Herbarium_R0:after"]
+    for h in list(log.handlers):
+        log.removeHandler(h)
+        h.close()
