@@ -653,11 +653,11 @@ std::vector<Tensor> ce_fwd(Tensor logits, Tensor labels) {
   TORCH_CHECK(labels.scalar_type() == torch::kInt64, "labels must be int64");
   const int B = logits.size(0), NC = logits.size(1);
   const c10::OptionalDeviceGuard g(device_of(logits));
-  Tensor loss = torch::empty({1}, logits.options().dtype(torch::kFloat32));
+  Tensor buf = torch::empty({1 + B}, logits.options().dtype(torch::kFloat32));
   Tensor lse = torch::empty({B}, logits.options().dtype(torch::kFloat32));
   mpa::ce_fwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), B, NC, ld,
-              loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
-  return {loss, lse};
+              buf.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
+  return {buf.narrow(0, 0, 1), lse};
 }
 
 // returns dlogits with the same row stride as logits (a view of a zero-padded buffer when
@@ -829,6 +829,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_set_engine", &mpa::igemm_set_engine);
   m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
   m.def("igemm_set_tune", &mpa::igemm_set_tune, "tile autotuner on/off (MPA_TUNE)");
+  m.def("set_deterministic", &mpa::set_deterministic,
+        "fixed-order reductions + no timing-based autotuning (MPA_DETERMINISTIC)");
+  m.def("deterministic", &mpa::deterministic);
   m.def("igemm_tuned_table", &mpa::igemm_tuned_table, "autotuned GEMM tiles so far");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");

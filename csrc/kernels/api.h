@@ -177,6 +177,9 @@ void igemm_set_stem(int on);  // MPA_STEM_DIRECT=0 disables (A/B, tests)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)
 int64_t bn_ws_floats(int M, int C);
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
+// MPA_DETERMINISTIC: fixed-order cross-block reductions, no timing-based tile autotuning
+void set_deterministic(int on);
+bool deterministic();
 // sums [2][C] of (x - shift) and (x - shift)^2 over M rows -> out [mean(C), var(C)]
 // slab [S][2C] of shifted (sum, sumsq) rows -> sums [2C] and out [mean(C), var(C)] (the
 // slab may be folded in place); replaces slab_reduce + stats_finalize
@@ -251,6 +254,9 @@ void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, 
 // loss.hip
 // logits rows have stride ld >= NC (padded heads); ce_bwd writes dlogits with stride ld and
 // zeros in columns NC..ld-1
+void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* row_loss,
+                 float* lse, hipStream_t s);
+// loss: [1 + B] floats (mean at [0], per-row terms after it; fixed-order sum)
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s);
 void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,

@@ -572,9 +572,9 @@ __device__ __forceinline__ float group_sum(const float* red, int t) {
   return v;
 }
 
-__global__ __launch_bounds__(64 * SG) void slab_reduce_kernel(const float* __restrict__ slab,
-                                                               int S, int W,
-                                                               float* __restrict__ out) {
+__global__ __launch_bounds__(64 * SG) void slab_reduce_kernel(float* __restrict__ slab, int S,
+                                                               int W, float* __restrict__ out,
+                                                               int det) {
   __shared__ float red[64 * SG];
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -585,17 +585,41 @@ __global__ __launch_bounds__(64 * SG) void slab_reduce_kernel(const float* __res
   if (g == 0 && w < W) {
     acc = group_sum(red, threadIdx.x);
     if (gridDim.y == 1) out[w] += acc;
+    else if (det) slab[(size_t)blockIdx.y * SG * W + w] = acc;  // a row only this block read
     else atomicAdd(out + w, acc);
   }
 }
 
+// deterministic second pass: out[w] += the blocks' partials, in block order
+__global__ __launch_bounds__(256) void slab_partials_kernel(const float* __restrict__ slab, int gy,
+                                                            int W, float* __restrict__ out) {
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= W) return;
+  float a = 0.f;
+  for (int y = 0; y < gy; ++y) a += slab[(size_t)y * SG * W + w];
+  out[w] += a;
+}
+
+static bool g_det = [] {
+  const char* e = getenv("MPA_DETERMINISTIC");
+  return e && e[0] == '1';
+}();
+void set_deterministic(int on) { g_det = on != 0; }
+bool deterministic() { return g_det; }
+
 // out must hold its starting value (the producer kernels zero it in their first block
-// when the reduction should start from 0; zero_out=true is only a fallback memset)
+// when the reduction should start from 0; zero_out=true is only a fallback memset).
+// Deterministic mode (MPA_DETERMINISTIC=1): the cross-block combine of a multi-block
+// reduction is a fixed-order second pass over per-block partials (stored into the slab
+// rows each block owns) instead of float atomics, whose order varies between launches.
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s) {
   if (zero_out) (void)hipMemsetAsync(out, 0, sizeof(float) * W, s);
   const int gy = std::max(1, std::min(32, (S + 255) / 256));
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 63) / 64, gy), dim3(64 * SG), 0, s, slab, S, W,
-                     out);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((W + 63) / 64, gy), dim3(64 * SG), 0, s,
+                     const_cast<float*>(slab), S, W, out, (int)g_det);
+  if (gy > 1 && g_det)
+    hipLaunchKernelGGL(slab_partials_kernel, dim3((W + 255) / 256), dim3(256), 0, s, slab, gy, W,
+                       out);
 }
 
 int64_t bn_ws_floats(int M, int C) {

@@ -761,7 +761,8 @@ static bool rows_cand_ok(int bm, int bn, int N) {
 // autotuned tile of a rows GEMM (fills tbm / tbn; leaves them 0 to keep the heuristic)
 static void tuned_rows_tile(const IGemmArgs& a, bool bkc, int vw, bool allow_split, hipStream_t s,
                             int& tbm, int& tbn) {
-  if (!g_tune || (g_force_bm && g_force_bn) || a.M <= 0 || stream_capturing(s)) return;
+  if (!g_tune || deterministic() || (g_force_bm && g_force_bn) || a.M <= 0 || stream_capturing(s))
+    return;
   const std::string key = rows_key(a, bkc, allow_split);
   if (tuned_lookup(key, tbm, tbn)) return;
   std::lock_guard<std::mutex> pass(g_tune_pass_mu);
@@ -944,7 +945,7 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
   if (a.nphase <= 0) return;
   if (use_dma(vw) && a.nphase <= MAXPH) {
     int tbm = 0, tbn = 0;
-    if (g_tune && !(g_force_bm && g_force_bn) && !stream_capturing(s)) {
+    if (g_tune && !deterministic() && !(g_force_bm && g_force_bn) && !stream_capturing(s)) {
       const std::string key = rows_key(a, bkc, false);
       std::unique_lock<std::mutex> pass(g_tune_pass_mu, std::defer_lock);
       if (!tuned_lookup(key, tbm, tbn) && (pass.lock(), !tuned_lookup(key, tbm, tbn))) {
@@ -1082,7 +1083,9 @@ static const int kWgradCands[][2] = {{64, 128}, {128, 128}, {64, 256}, {128, 256
 // and a scratch dw, and may not need more split slab than the caller allocated
 static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s, int& tbm,
                              int& tbn) {
-  if (!g_tune || (g_force_bm && g_force_bn) || a.Mpix <= 0 || stream_capturing(s)) return;
+  if (!g_tune || deterministic() || (g_force_bm && g_force_bn) || a.Mpix <= 0 ||
+      stream_capturing(s))
+    return;
   char k[200];
   snprintf(k, sizeof k, "wgrad K%d N%d P%d x%dx%dx%d o%dx%d f%dx%d s%d,%d p%d,%d", a.Kout, a.Ncols,
            a.Mpix, a.H, a.W, a.C, a.P, a.Q, a.R, a.S, a.sh, a.sw, a.ph, a.pw);

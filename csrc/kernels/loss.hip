@@ -40,7 +40,7 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 template <int V>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ logits,
                                                       const int64_t* __restrict__ labels, int B,
-                                                      int NC, int ld, float* __restrict__ loss,
+                                                      int NC, int ld, float* __restrict__ row_loss,
                                                       float* __restrict__ lse_out) {
   const int row = blockIdx.x;
   const bf16_t* x = logits + (size_t)row * ld;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const bf16_t* __restrict__ 
     lse_out[row] = lse;
     const int64_t lab = labels[row];
     const float picked = (lab >= 0 && lab < NC) ? bf2f(x[lab]) : lse;
-    atomicAdd(loss, (lse - picked) / (float)B);
+    row_loss[row] = (lse - picked) / (float)B;
   }
 }
 
@@ -88,7 +88,7 @@ template <int U>
 __global__ __launch_bounds__(256) void ce_fwd_padded_kernel(const bf16_t* __restrict__ logits,
                                                              const int64_t* __restrict__ labels,
                                                              int B, int NC, int ld,
-                                                             float* __restrict__ loss,
+                                                             float* __restrict__ row_loss,
                                                              float* __restrict__ lse_out) {
   const int row = blockIdx.x;
   const bf16_t* x = logits + (size_t)row * ld;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void ce_fwd_padded_kernel(const bf16_t* __rest
     lse_out[row] = lse;
     const int64_t lab = labels[row];
     const float picked = (lab >= 0 && lab < NC) ? bf2f(x[lab]) : lse;
-    atomicAdd(loss, (lse - picked) / (float)B);
+    row_loss[row] = (lse - picked) / (float)B;
   }
 }
 
@@ -204,9 +204,33 @@ __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// loss = sum of the per-row terms in a FIXED order (strided per-thread partial sums, then a
+// fixed tree): bitwise reproducible, unlike one float atomic per row (whose order varies
+// between launches), and one launch like the memset it replaces.
+__global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restrict__ row_loss, int B,
+                                                          float* __restrict__ loss) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) a += row_loss[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0];
+}
+
+// loss: [1 + B] floats - the mean loss at [0], the per-row terms after it
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s) {
-  (void)hipMemsetAsync(loss, 0, sizeof(float), s);
+  float* rows = loss + 1;
+  ce_fwd_rows(logits, labels, B, NC, ld, rows, lse, s);
+  hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, loss);
+}
+
+void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
+                 float* lse, hipStream_t s) {
   if (ld % 8 == 0 && ld >= NC && reinterpret_cast<uintptr_t>(logits) % 16 == 0) {
     hipLaunchKernelGGL(ce_fwd_padded_kernel<4>, dim3(B), dim3(256), 0, s, logits, labels, B, NC,
                        ld, loss, lse);

@@ -1,0 +1,79 @@
+"""Deterministic mode (MPA_DETERMINISTIC / ``_ext.set_deterministic``): fixed-order
+cross-block reductions and no timing-based tile autotuning make a training step a pure
+function of its inputs, so
+
+* two identical steps from identical state are bitwise equal (loss, gradient arena,
+  updated weights), and
+* back-to-back HIP-graph replays of the whole step are bitwise equal to the same number of
+  eager steps (docs/NOTES.md "HIP graph replay").
+
+The reference has no GPU path; its per-step semantics (fwd -> CE -> backward -> Adam,
+``/root/reference/main.py:142-156``) are what both runs execute."""
+import pytest
+import torch
+
+from mpi_pytorch_amd.engine import build_training
+from mpi_pytorch_amd.parallel import World
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def det(gpu):
+    from mpi_pytorch_amd.ops import _ext
+    C = _ext.ext()
+    old = C.deterministic()
+    C.set_deterministic(1)
+    yield gpu
+    C.set_deterministic(int(old))
+
+
+def _train(gpu, seed=0, name="resnet18", nc=100):
+    torch.manual_seed(seed)
+    w = World(device=gpu)
+    model, opt, step, _ = build_training(name, nc, gpu, w, 1e-3)
+    return model, opt, step
+
+
+def _batch(gpu, B=32, hw=64, nc=100, seed=1):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = (torch.randn(B, hw, hw, 8, generator=g) * (torch.arange(8) < 3)).to(gpu, torch.bfloat16)
+    y = torch.randint(0, nc, (B,), generator=g).to(gpu)
+    return x, y
+
+
+def test_two_identical_steps_bitwise(det):
+    gpu = det
+    x, y = _batch(gpu)
+    outs = []
+    for _ in range(2):
+        model, opt, step = _train(gpu)
+        losses = [step(x, y).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        a = model._mpa_arena
+        outs.append((torch.stack(losses).cpu(), a.grad.cpu().clone(), a.master.cpu().clone(),
+                     opt.exp_avg_sq.cpu().clone()))
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+
+
+def test_graph_replays_bitwise_equal_eager(det):
+    """100 back-to-back replays (no host sync between them) == 100 eager steps."""
+    gpu = det
+    x, y = _batch(gpu)
+    n = 100
+    # eager: the capture below runs 2 eager warmup steps before recording
+    model, opt, step = _train(gpu)
+    ref = torch.stack([step(x, y).clone() for _ in range(n + 2)])[2:]
+    torch.cuda.synchronize()
+    ref_master = model._mpa_arena.master.clone()
+    del model, opt, step
+    model, opt, step = _train(gpu)
+    step._sync_replay = False
+    assert step.capture(x, y, warmup=2)
+    got = torch.stack([step(x, y).clone() for _ in range(n)])
+    torch.cuda.synchronize()
+    bad = (got != ref).nonzero()
+    assert bad.numel() == 0, "first diverging replay %d: %s vs %s" % (
+        int(bad[0]), float(got[bad[0]]), float(ref[bad[0]]))
+    assert torch.equal(model._mpa_arena.master, ref_master)
