@@ -723,7 +723,8 @@ void cast_f32_bf16(Tensor x, Tensor y) {
 // ------------------------------------------------------------------------ preprocess
 // pad: (top, bottom, left, right) zero border of the output canvas (empty = none)
 Tensor preprocess(Tensor img, int64_t OH, int64_t OW, std::vector<double> mean,
-                  std::vector<double> stdv, int64_t mode, int64_t cpad, std::vector<int64_t> pad) {
+                  std::vector<double> stdv, int64_t mode, int64_t cpad, std::vector<int64_t> pad,
+                  c10::optional<Tensor> ext) {
   CHECK_CUDA(img);
   CHECK_CONTIG(img);
   TORCH_CHECK(img.scalar_type() == torch::kUInt8 && img.dim() == 4 && img.size(3) == 3,
@@ -739,8 +740,63 @@ Tensor preprocess(Tensor img, int64_t OH, int64_t OW, std::vector<double> mean,
       img, {B, OH + pd.top + pd.bottom, OW + pd.left + pd.right, cpad}, torch::kBFloat16);
   mpa::Norm3 n;
   for (int i = 0; i < 3; ++i) { n.mean[i] = mean[i]; n.std[i] = stdv[i]; }
+  const int* extp = nullptr;
+  if (ext && ext->defined() && ext->numel() > 0) {
+    // per-image extents (h, w) inside the [H][W] pitch; the caller (ops/functional.py)
+    // checked them on its host copy, so no device sync here
+    TORCH_CHECK(mode == 0, "preprocess: extents with mode 0 (mode 1 is preprocess_pil)");
+    CHECK_CUDA((*ext));
+    CHECK_CONTIG((*ext));
+    TORCH_CHECK(ext->scalar_type() == torch::kInt32 && ext->numel() == 2 * (int64_t)B,
+                "preprocess: ext must be int32 [B,2]");
+    extp = ext->data_ptr<int>();
+  }
   mpa::preprocess(img.data_ptr<uint8_t>(), B, H, W, OH, OW, n, mode, cpad, pd, bpm(out),
-                  cur_stream());
+                  cur_stream(), extp);
+  return out;
+}
+
+// PIL-exact bicubic resize + ToTensor + Normalize (data/pil_resize.py builds the tables)
+Tensor preprocess_pil(Tensor img, Tensor ext, Tensor sel, Tensor hb, Tensor hk, int64_t kh,
+                      Tensor vb, Tensor vk, int64_t kv, int64_t OH, int64_t OW,
+                      std::vector<double> mean, std::vector<double> stdv, int64_t cpad,
+                      std::vector<int64_t> pad) {
+  CHECK_CUDA(img);
+  CHECK_CONTIG(img);
+  TORCH_CHECK(img.scalar_type() == torch::kUInt8 && img.dim() == 4 && img.size(3) == 3,
+              "preprocess_pil: expects uint8 [B,H,W,3]");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3 && cpad >= 3, "preprocess_pil: args");
+  TORCH_CHECK(pad.empty() || pad.size() == 4, "preprocess_pil: pad = (top, bottom, left, right)");
+  const int B = img.size(0), Hp = img.size(1), Wp = img.size(2);
+  auto i32 = [&](const Tensor& t, int64_t n, const char* what) {
+    CHECK_CUDA(t);
+    CHECK_CONTIG(t);
+    TORCH_CHECK(t.scalar_type() == torch::kInt32 && t.numel() == n, "preprocess_pil: ", what);
+    return t.data_ptr<int>();
+  };
+  const int* selp = i32(sel, 2 * (int64_t)B, "sel [B,2]");
+  TORCH_CHECK(hb.numel() % (2 * OW) == 0 && vb.numel() % (2 * OH) == 0, "preprocess_pil: bounds");
+  const int64_t nw = hb.numel() / (2 * OW), nh = vb.numel() / (2 * OH);
+  const int* hbp = i32(hb, nw * 2 * OW, "hb");
+  const int* hkp = i32(hk, nw * OW * kh, "hk");
+  const int* vbp = i32(vb, nh * 2 * OH, "vb");
+  const int* vkp = i32(vk, nh * OH * kv, "vk");
+  // (the window of every table entry lies inside its image's extent and every extent inside
+  // the pitch: data/pil_resize.TableCache checks that on the host copies it builds, so this
+  // launch path never syncs the device)
+  const int* extp = has(ext) ? i32(ext, 2 * (int64_t)B, "ext [B,2]") : nullptr;
+  mpa::OutPad pd{0, 0, 0, 0};
+  if (pad.size() == 4) pd = mpa::OutPad{(int)pad[0], (int)pad[1], (int)pad[2], (int)pad[3]};
+  TORCH_CHECK(pd.top >= 0 && pd.bottom >= 0 && pd.left >= 0 && pd.right >= 0, "preprocess_pil: pad");
+  const c10::OptionalDeviceGuard g(device_of(img));
+  Tensor out = empty_like_shape(
+      img, {B, OH + pd.top + pd.bottom, OW + pd.left + pd.right, cpad}, torch::kBFloat16);
+  Tensor tmp = torch::empty({(int64_t)B * Hp * OW}, img.options().dtype(torch::kInt32));
+  mpa::Norm3 n;
+  for (int i = 0; i < 3; ++i) { n.mean[i] = mean[i]; n.std[i] = stdv[i]; }
+  mpa::preprocess_pil(img.data_ptr<uint8_t>(), B, Hp, Wp, extp, selp, hbp, hkp, (int)kh, vbp, vkp,
+                      (int)kv, (int)OH, (int)OW, n, (int)cpad, pd,
+                      reinterpret_cast<uint32_t*>(tmp.data_ptr<int>()), bpm(out), cur_stream());
   return out;
 }
 
@@ -895,9 +951,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("transpose_krsc", &transpose_krsc);
+  m.def("preprocess_pil", &preprocess_pil, "PIL-exact bicubic resize + ToTensor + Normalize");
   m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
         py::arg("std"), py::arg("mode"), py::arg("cpad"),
-        py::arg("pad") = std::vector<int64_t>{});
+        py::arg("pad") = std::vector<int64_t>{}, py::arg("ext") = py::none());
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("concat_channels", &concat_channels);

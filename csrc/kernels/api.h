@@ -286,8 +286,16 @@ struct OutPad {
   int top, bottom, left, right;
 };
 void preprocess_set_copy(int on);  // identity-size fast path on/off (tests, A/B)
+// ext (optional): per-image source extents [B][2] = (h, w) inside the [H][W] pitch (mode 0)
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
-                int cpad, OutPad pad, bf16_raw* out, hipStream_t s);
+                int cpad, OutPad pad, bf16_raw* out, hipStream_t s, const int* ext = nullptr);
+// PIL-exact bicubic (eval transform): per-image extents ext [B][2] (h, w) inside the
+// [Hp][Wp] pitch (nullptr: all full), per-image table selectors sel [B][2]; tmp holds
+// B * Hp * OW RGBx words
+void preprocess_pil(const uint8_t* img, int B, int Hp, int Wp, const int* ext, const int* sel,
+                    const int* hb, const int* hk, int kh, const int* vb, const int* vk, int kv,
+                    int OH, int OW, Norm3 nrm, int cpad, OutPad pd, uint32_t* tmp, bf16_raw* out,
+                    hipStream_t s);
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,
                  bf16_raw* y, uint8_t* mask, hipStream_t s);
 void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,

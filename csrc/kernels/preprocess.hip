@@ -64,7 +64,7 @@ constexpr int PP_MAXW = 1344;  // 2 x 8 staged rows x 1344 px x 3 B = 63 KiB of 
 template <bool STAGED, int VEC, int CPAD>
 __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
     const uint8_t* __restrict__ img, int B, int H, int W, int OH, int OW,
-    Norm3 nrm, int cpad_rt, OutPad pd, bf16_t* __restrict__ out) {
+    Norm3 nrm, int cpad_rt, OutPad pd, bf16_t* __restrict__ out, const int* __restrict__ ext) {
   const int cpad = CPAD ? CPAD : cpad_rt;
   extern __shared__ __attribute__((aligned(16))) uint8_t srow[];  // [PP_ROWS][2][rb]
   const float* mean = nrm.mean;
@@ -73,11 +73,9 @@ __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
   const float o0 = mean[0] / stdv[0], o1 = mean[1] / stdv[1], o2 = mean[2] / stdv[2];
   const int ohp = OH + pd.top + pd.bottom, owp = OW + pd.left + pd.right;
   const int ngroups = (ohp + PP_ROWS - 1) / PP_ROWS;  // row groups per image
-  const float sh = (float)H / OH, sw = (float)W / OW;
-  const int rb = W * 3;                     // source row bytes
+  const int rb = W * 3;                     // source row bytes (the slot pitch)
   const int rbp = (rb + 15) & ~15;          // staged row pitch
   constexpr int vec = VEC;
-  const int per = rb / vec;  // vectors per source row
   // work items (image, row group), strided over a grid of at most ~2k blocks: per-wave
   // start-up (kernel arguments, the normalisation divides) is paid once per block
   for (int item = blockIdx.x; item < B * ngroups; item += gridDim.x) {
@@ -85,11 +83,16 @@ __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
     const int row0 = (item - b * ngroups) * PP_ROWS;
     const int nrows = min(PP_ROWS, ohp - row0);
     const uint8_t* base = img + (size_t)b * H * W * 3;
+    // this image's extent inside the [H][W] pitch (real images of different sizes share
+    // one padded slot); the full pitch when ext is null
+    const int ih = ext ? ext[2 * b] : H, iw = ext ? ext[2 * b + 1] : W;
+    const float sh = (float)ih / OH, sw = (float)iw / OW;
+    const int per = (iw * 3 + vec - 1) / vec;  // vectors per staged source row
     auto tap_rows = [&](int r, int& y0, int& y1, float& ly) {
       const int oy = row0 + r - pd.top;
       const float sy = fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
-      y0 = min((int)sy, H - 1);
-      y1 = min(y0 + 1, H - 1);
+      y0 = min((int)sy, ih - 1);
+      y1 = min(y0 + 1, ih - 1);
       ly = sy - y0;
     };
     if constexpr (STAGED) {  // phase 1: every (row, tap) source row; 4 loads in flight per
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(256) void preprocess_bilinear_kernel(
           continue;
         }
         const float sx = fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
-        const int x0 = min((int)sx, W - 1), x1 = min(x0 + 1, W - 1);
+        const int x0 = min((int)sx, iw - 1), x1 = min(x0 + 1, iw - 1);
         const float lx = sx - x0;
         float c[3];
 #pragma unroll
@@ -317,6 +320,99 @@ __global__ void dropout_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
     dx[i] = mask[i] ? f2bf(bf2f(dy[i]) * scale) : (bf16_t)0;
 }
 
+// ---------------------------------------------------------------- PIL-exact bicubic (eval)
+// Pillow's 8-bpc resampler (evaluation_pipeline.py:89 -> data/pil_resize.py): integer
+// tables (22-bit fixed point) built on the host exactly as Pillow builds them, a horizontal
+// pass rounded + clipped to uint8, then a vertical pass over that uint8 image, then
+// ToTensor/Normalize in fp32 with torchvision's operation order.  Every image b of the batch
+// has its own source extent ext[b] = (h, w) inside the [Hp][Wp] slot pitch (real JPEGs of
+// different sizes decoded into one padded ring slot) and its own tables sel[b] = (width
+// table, height table).  The output equals PIL's uint8 image exactly before normalisation.
+constexpr int PIL_PREC = 22;
+
+__device__ __forceinline__ int pil_clip8(int v) { return min(max(v >> PIL_PREC, 0), 255); }
+
+// tmp[b][y][ox] (RGBx, 4 B) for the rows y < h_b: one thread per output column
+__global__ __launch_bounds__(256) void pil_hpass_kernel(const uint8_t* __restrict__ img, int Hp,
+                                                        int Wp, const int* __restrict__ ext,
+                                                        const int* __restrict__ sel,
+                                                        const int* __restrict__ hb,
+                                                        const int* __restrict__ hk, int kh, int OW,
+                                                        uint32_t* __restrict__ tmp) {
+  const int b = blockIdx.z, y = blockIdx.y;
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x;
+  const int h = ext ? ext[2 * b] : Hp;
+  if (y >= h || ox >= OW) return;
+  const int tab = sel[2 * b];
+  const int xmin = hb[2 * (tab * OW + ox)], xs = hb[2 * (tab * OW + ox) + 1];
+  const int* k = hk + (size_t)(tab * OW + ox) * kh;
+  const uint8_t* p = img + (((size_t)b * Hp + y) * Wp + xmin) * 3;
+  int s0 = 1 << (PIL_PREC - 1), s1 = s0, s2 = s0;
+  for (int t = 0; t < xs; ++t) {
+    const int kt = k[t];
+    s0 += (int)p[3 * t] * kt;
+    s1 += (int)p[3 * t + 1] * kt;
+    s2 += (int)p[3 * t + 2] * kt;
+  }
+  tmp[((size_t)b * Hp + y) * OW + ox] =
+      (uint32_t)pil_clip8(s0) | ((uint32_t)pil_clip8(s1) << 8) | ((uint32_t)pil_clip8(s2) << 16);
+}
+
+// one block per canvas row (blockIdx.x) of image blockIdx.y; threads over its pixels
+__global__ __launch_bounds__(256) void pil_vpass_kernel(const uint32_t* __restrict__ tmp, int Hp,
+                                                        const int* __restrict__ sel,
+                                                        const int* __restrict__ vb,
+                                                        const int* __restrict__ vk, int kv, int OH,
+                                                        int OW, Norm3 nrm, int cpad, OutPad pd,
+                                                        bf16_t* __restrict__ out) {
+  const CanvasRow cr = canvas_row(pd, OH, OW, cpad, out);
+  const int b = blockIdx.y, oy = cr.oy;
+  int ymin = 0, ys = 0;
+  const int* k = nullptr;
+  if (!cr.border) {
+    const int tab = sel[2 * b + 1];
+    ymin = vb[2 * (tab * OH + oy)];
+    ys = vb[2 * (tab * OH + oy) + 1];
+    k = vk + (size_t)(tab * OH + oy) * kv;
+  }
+  for (int px = threadIdx.x; px < cr.owp; px += blockDim.x) {
+    const int ox = px - pd.left;
+    bf16_t* o = cr.out + (size_t)px * cpad;
+    if (cr.border || (unsigned)ox >= (unsigned)OW) {
+      store_px(o, 0.f, 0.f, 0.f, cpad);
+      continue;
+    }
+    const uint32_t* col = tmp + ((size_t)b * Hp + ymin) * OW + ox;
+    int s0 = 1 << (PIL_PREC - 1), s1 = s0, s2 = s0;
+    for (int t = 0; t < ys; ++t) {
+      const uint32_t v = col[(size_t)t * OW];
+      const int kt = k[t];
+      s0 += (int)(v & 255u) * kt;
+      s1 += (int)((v >> 8) & 255u) * kt;
+      s2 += (int)((v >> 16) & 255u) * kt;
+    }
+    // ToTensor (u8 / 255) then Normalize ((x - mean) / std), each step in fp32
+    const float c0 = ((float)pil_clip8(s0) / 255.f - nrm.mean[0]) / nrm.std[0];
+    const float c1 = ((float)pil_clip8(s1) / 255.f - nrm.mean[1]) / nrm.std[1];
+    const float c2 = ((float)pil_clip8(s2) / 255.f - nrm.mean[2]) / nrm.std[2];
+    store_px(o, c0, c1, c2, cpad);
+  }
+}
+
+void preprocess_pil(const uint8_t* img, int B, int Hp, int Wp, const int* ext, const int* sel,
+                    const int* hb, const int* hk, int kh, const int* vb, const int* vk, int kv,
+                    int OH, int OW, Norm3 nrm, int cpad, OutPad pd, uint32_t* tmp, bf16_raw* out,
+                    hipStream_t s) {
+  if (B <= 0) return;
+  const int tx = OW >= 256 ? 256 : std::max(64, (OW + 63) / 64 * 64);
+  hipLaunchKernelGGL(pil_hpass_kernel, dim3((OW + tx - 1) / tx, Hp, B), dim3(tx), 0, s, img, Hp,
+                     Wp, ext, sel, hb, hk, kh, OW, tmp);
+  const int ohp = OH + pd.top + pd.bottom, owp = OW + pd.left + pd.right;
+  const dim3 block(owp >= 256 ? 256 : std::max(64, (owp + 63) / 64 * 64));
+  hipLaunchKernelGGL(pil_vpass_kernel, dim3(ohp, B), block, 0, s, tmp, Hp, sel, vb, vk, kv, OH,
+                     OW, nrm, cpad, pd, (bf16_t*)out);
+}
+
 static int blocks_n(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
 }
@@ -329,10 +425,10 @@ static int g_pre_copy = [] {
 void preprocess_set_copy(int on) { g_pre_copy = on; }
 
 void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 nrm, int mode,
-                int cpad, OutPad pd, bf16_raw* out, hipStream_t s) {
+                int cpad, OutPad pd, bf16_raw* out, hipStream_t s, const int* ext) {
   if (B <= 0) return;  // bicubic: gridDim.y = images (<= 65535)
   const int ohp = OH + pd.top + pd.bottom, owp = OW + pd.left + pd.right;
-  if (mode == 0 && g_pre_copy && H == OH && W == OW && cpad == 4 && W % 4 == 0 &&
+  if (mode == 0 && !ext && g_pre_copy && H == OH && W == OW && cpad == 4 && W % 4 == 0 &&
       reinterpret_cast<uintptr_t>(img) % 4 == 0 && (int64_t)B * ohp < (1ll << 30)) {
     hipLaunchKernelGGL(preprocess_copy4_kernel, dim3((B * ohp + 3) / 4), dim3(256), 0, s, img, B,
                        H, W, nrm, pd, out);
@@ -347,7 +443,7 @@ void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 n
     const int vec = (rb % 16 == 0 && ia % 16 == 0) ? 16 : (rb % 4 == 0 && ia % 4 == 0) ? 4 : 1;
 #define PP_LAUNCH(ST, V, CP, L)                                                                 \
   hipLaunchKernelGGL((preprocess_bilinear_kernel<ST, V, CP>), grid, dim3(256), L, s, img, B, H, \
-                     W, OH, OW, nrm, cpad, pd, out)
+                     W, OH, OW, nrm, cpad, pd, out, ext)
 #define PP_CPAD(ST, V, L)                                      \
   do {                                                         \
     if (cpad == 4) PP_LAUNCH(ST, V, 4, L);                     \

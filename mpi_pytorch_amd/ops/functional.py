@@ -24,6 +24,7 @@ from __future__ import annotations
 import os
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import ref
@@ -628,13 +629,52 @@ def count_correct(logits, labels, count: torch.Tensor) -> None:
 
 
 def preprocess(img_u8, out_hw, mean, std, mode: int = 0, cpad: int = 3,
-               out_dtype=torch.bfloat16, pad=None):
+               out_dtype=torch.bfloat16, pad=None, extents=None):
     """u8 [B,H,W,3] -> resized, normalized NHWC with ``cpad`` channels, optionally on a
     zero-bordered canvas ``pad`` = (top, bottom, left, right) (the pre-padded input layout
-    of a pixel-pair stem, ``models.layers.Conv2d.input_spec``)."""
+    of a pixel-pair stem, ``models.layers.Conv2d.input_spec``).
+
+    mode 0: bilinear, no antialias (the train transform, main.py:62-65); mode 1: PIL-exact
+    bicubic (the eval transform, evaluation_pipeline.py:89, data/pil_resize.py); mode 2:
+    float antialiased bicubic (torch ``F.interpolate(antialias=True)`` semantics).
+    ``extents`` (host int [B, 2]): image b occupies rows [0, h_b) and columns [0, w_b) of
+    its slot (real images of different sizes decoded into one padded batch)."""
     k = K(img_u8)
     pad = list(pad) if pad else []
+    if extents is not None:
+        extents = np.asarray(extents, dtype=np.int64).reshape(-1, 2)
+        B, Hp, Wp = img_u8.shape[:3]
+        if extents.shape[0] != B or (extents < 1).any() or (extents[:, 0] > Hp).any() \
+                or (extents[:, 1] > Wp).any():
+            raise ValueError("preprocess: extents %s do not fit the [%d, %d] slot pitch"
+                             % (extents.tolist(), Hp, Wp))
     if img_u8.is_cuda:
-        return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad, pad)
+        if mode == 1:  # PIL-exact bicubic (the eval transform)
+            tc = _PIL_TABLES.get(img_u8.device)
+            if tc is None:
+                from ..data.pil_resize import TableCache
+                tc = _PIL_TABLES[img_u8.device] = TableCache(img_u8.device)
+            B, Hp, Wp = img_u8.shape[:3]
+            ext = extents if extents is not None else np.tile([[Hp, Wp]], (B, 1))
+            e, sel, hb, hk, kh, vb, vk, kv = tc.tables(ext, tuple(out_hw), (Hp, Wp))
+            return k.preprocess_pil(img_u8, e if extents is not None else _empty_i32(img_u8),
+                                    sel, hb, hk, kh, vb, vk, kv, out_hw[0], out_hw[1],
+                                    list(mean), list(std), cpad, pad)
+        ext = None
+        if extents is not None:
+            ext = torch.from_numpy(extents.astype(np.int32)).to(img_u8.device, non_blocking=True)
+        return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad, pad,
+                            ext)
     return k.preprocess(img_u8, out_hw[0], out_hw[1], list(mean), list(std), mode, cpad,
-                        out_dtype, pad)
+                        out_dtype, pad, extents)
+
+
+_PIL_TABLES = {}
+
+
+def _empty_i32(t: torch.Tensor) -> torch.Tensor:
+    key = (t.device, torch.int32)
+    e = _EMPTY.get(key)
+    if e is None:
+        e = _EMPTY[key] = torch.empty(0, device=t.device, dtype=torch.int32)
+    return e

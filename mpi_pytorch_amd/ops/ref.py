@@ -375,23 +375,36 @@ def sgd_step(master, grad, buf, shadow, step_t, lr, momentum, dampening, wd, nes
 
 
 # ------------------------------------------------------------------------ preprocessing
-def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype, pad=None):
+def preprocess(img_u8, oh, ow, mean, std, mode, cpad, out_dtype, pad=None, extents=None):
     """u8 NHWC [B,H,W,3] -> normalized NHWC [B,oh,ow,cpad] (zero padded channels), on a
     zero-bordered canvas when pad = (top, bottom, left, right).
 
     mode 0: bilinear, no antialias  (train path: ToTensor -> Resize on tensor, main.py:62-65)
-    mode 1: bicubic with antialias  (eval path: PIL resize, evaluation_pipeline.py:89)
+    mode 1: PIL bicubic (antialiased, 8-bit fixed point) -> u8 -> ToTensor -> Normalize
+            (eval path, evaluation_pipeline.py:89,116-122): data/pil_resize.py, bit-exact
+            with PIL.Image.resize
+    mode 2: float bicubic with antialias (F.interpolate semantics)
+    extents: image b occupies [:h_b, :w_b] of its slot.
     """
-    x = _nchw(img_u8.float() / 255.0)
-    if (oh, ow) != tuple(x.shape[-2:]):
-        if mode == 0:
-            x = F.interpolate(x, size=(oh, ow), mode="bilinear", align_corners=False)
-        else:
-            x = F.interpolate(x, size=(oh, ow), mode="bicubic", align_corners=False,
-                              antialias=True)
-    m = torch.tensor(mean, device=x.device).view(1, 3, 1, 1)
-    s = torch.tensor(std, device=x.device).view(1, 3, 1, 1)
-    x = _nhwc((x - m) / s)
+    if extents is not None:
+        parts = [preprocess(img_u8[b:b + 1, :int(h), :int(w)], oh, ow, mean, std, mode, cpad,
+                            out_dtype, pad) for b, (h, w) in enumerate(extents)]
+        return torch.cat(parts, 0)
+    if mode == 1:
+        from ..data import pil_resize
+        x = torch.from_numpy(pil_resize.reference(img_u8.cpu().numpy(), (oh, ow), mean, std))
+        x = x.to(img_u8.device)
+    else:
+        x = _nchw(img_u8.float() / 255.0)
+        if (oh, ow) != tuple(x.shape[-2:]):
+            if mode == 0:
+                x = F.interpolate(x, size=(oh, ow), mode="bilinear", align_corners=False)
+            else:
+                x = F.interpolate(x, size=(oh, ow), mode="bicubic", align_corners=False,
+                                  antialias=True)
+        m = torch.tensor(mean, device=x.device).view(1, 3, 1, 1)
+        s = torch.tensor(std, device=x.device).view(1, 3, 1, 1)
+        x = _nhwc((x - m) / s)
     if cpad > 3:
         x = F.pad(x, (0, cpad - 3))
     if pad:

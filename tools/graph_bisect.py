@@ -28,7 +28,7 @@ HW = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 60
 NC = int(os.environ.get("NC", "100"))
 gpu = torch.device("cuda", 0)
-_ext.ext().set_deterministic(1)
+_ext.ext().set_deterministic(int(os.environ.get("DET", "1")))
 g = torch.Generator().manual_seed(1)
 x = (torch.randn(B, HW, HW, 8, generator=g) * (torch.arange(8) < 3)).to(gpu, torch.bfloat16)
 y = torch.randint(0, NC, (B,), generator=g).to(gpu)
@@ -36,7 +36,8 @@ y = torch.randint(0, NC, (B,), generator=g).to(gpu)
 
 def fresh():
     torch.manual_seed(0)
-    return build_training(os.environ.get("MODEL", "resnet18"), NC, gpu, World(device=gpu), 1e-3)
+    return build_training(os.environ.get("MODEL", "resnet18"), NC, gpu, World(device=gpu),
+                          1e-3)[:3]
 
 
 def checksum(model):
@@ -114,9 +115,10 @@ def run_fwd_graph(sep, n, with_bwd):
             torch.cuda.current_stream().synchronize()
     torch.cuda.synchronize()
     v, c = torch.stack(vals), torch.stack(sums)
-    # BN running stats drift between replays but batch statistics (train mode) do not
-    # depend on them: every replay must reproduce the first bitwise
-    return first_diff(v, v[:1].expand_as(v)), first_diff(c, c[:1].expand_as(c)), v
+    # the BN running mean drifts between replays and the conv epilogues take their
+    # statistics around it (docs/NOTES.md "BN statistics without cancellation"), so replays
+    # agree to rounding, not bitwise: report the spread
+    return float((v - v[0]).abs().max()), float(((c - c[0]).abs() / c[0].abs()).max()), v
 
 
 print("batch %d hw %d replays %d deterministic %d" % (B, HW, R, _ext.ext().deterministic()),
@@ -124,9 +126,9 @@ print("batch %d hw %d replays %d deterministic %d" % (B, HW, R, _ext.ext().deter
 for with_bwd in (False, True):
     for sep in ("none", "event", "sync"):
         fl, fc, v = run_fwd_graph(sep, R, with_bwd)
-        print("%-7s sep=%-5s first differing replay: loss %d  grad/weights %d   (loss[0] %.6f, "
-              "nan %d)" % ("fwdbwd" if with_bwd else "fwd", sep, fl, fc, float(v[0]),
-                           int(torch.isnan(v).sum())), flush=True)
+        print("%-7s sep=%-5s spread over replays: loss %.3g  grad/weights (rel) %.3g   "
+              "(loss[0] %.6f, nan %d)" % ("fwdbwd" if with_bwd else "fwd", sep, fl, fc,
+                                          float(v[0]), int(torch.isnan(v).sum())), flush=True)
 ref_l, ref_c = eager_ref(R + 2)
 ref_l, ref_c = ref_l[2:], ref_c[2:]
 for sep in ("none", "event", "sync"):
