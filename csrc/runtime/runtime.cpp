@@ -1,14 +1,22 @@
 // Native host runtime: the data path the reference runs serially in Python
-// (DataLoader with num_workers=0, main.py:102; GetData.__getitem__, data_loader.py:29-37).
+// (DataLoader with num_workers=0, main.py:102; GetData.__getitem__, data_loader.py:29-37;
+// the eval pipeline's read stage, evaluation_pipeline.py:53-71).
 //
-// BatchRing: a bounded ring of pinned (hipHostMalloc) batch slots filled by C++ producer
-// threads, consumed by the training loop, which issues one async H2D copy per batch on a
-// dedicated copy stream and hands the slot back once that copy's event has completed.
-// Producers never hold the GIL.  Two producer modes:
-//   * synthetic: deterministic pseudo-random uint8 HWC images + uniform labels
+// BatchRing: a bounded ring of pinned (hipHostMalloc) batch slots filled by producers,
+// consumed by the training loop / eval pipeline, which issue one async H2D copy per batch on
+// a dedicated copy stream and hand the slot back once that copy's event has completed.
+// Every slot carries uint8 images [B][H][W][3] (H x W is the PITCH: an image may occupy only
+// its top-left extent, ext[b] = (h, w), so real JPEGs of different sizes share one slot and
+// one preprocess launch), int64 labels [B], the batch index and the valid image count.
+// Consumers receive batches in batch-index order (start_index, start_index + stride, ...),
+// whatever order the producers finish them in, so data order is deterministic.
+// Producer modes (native ones never hold the GIL):
+//   * synthetic: deterministic pseudo-random uint8 images + uniform labels per batch index
 //     (BASELINE.json: synthetic data, no Herbarium images offline);
+//   * window: image i of a manifest is the window of a shared uint8 texture at offs[i]
+//     (data/manifest.SyntheticImages, bitwise), label labels[i]; batches 0..ceil(N/B)-1;
 //   * external: Python (PIL decode threads) writes decoded images into a slot obtained
-//     with acquire_empty()/commit() - the same ring feeds the GPU preprocess kernel.
+//     with acquire_empty() and hands it over with commit(id, batch_index, count).
 //
 // Markers: roctx ranges so rocprofv3 --marker-trace shows step phases.
 #include "runtime.h"
@@ -38,7 +46,9 @@ inline uint64_t splitmix(uint64_t& x) {
 struct Slot {
   uint8_t* img = nullptr;    // pinned [B,H,W,3]
   int64_t* labels = nullptr; // pinned [B]
+  int32_t* ext = nullptr;    // pinned [B,2] (h, w) of each image inside the pitch
   int64_t batch_index = -1;
+  int count = 0;             // valid images (the last batch of a manifest may be short)
 };
 
 class BatchRing {
@@ -46,8 +56,10 @@ class BatchRing {
   BatchRing(int batch, int H, int W, int64_t num_classes, int depth, int threads, uint64_t seed,
             int64_t start_index, int64_t stride, bool synthetic)
       : B_(batch), H_(H), W_(W), nc_(num_classes), seed_(seed), next_index_(start_index),
-        stride_(stride), synthetic_(synthetic) {
+        next_consume_(start_index), stride_(stride), synthetic_(synthetic),
+        threads_(std::max(1, threads)) {
     TORCH_CHECK(depth >= 2, "BatchRing depth must be >= 2");
+    TORCH_CHECK(batch >= 1 && H >= 1 && W >= 1 && stride >= 1, "BatchRing: bad geometry");
     slots_.resize(depth);
     const size_t img_bytes = (size_t)B_ * H_ * W_ * 3;
     for (auto& s : slots_) {
@@ -58,10 +70,13 @@ class BatchRing {
       TORCH_CHECK(hipHostMalloc(&p, sizeof(int64_t) * B_, hipHostMallocDefault) == hipSuccess,
                   "hipHostMalloc failed");
       s.labels = (int64_t*)p;
+      TORCH_CHECK(hipHostMalloc(&p, sizeof(int32_t) * 2 * B_, hipHostMallocDefault) == hipSuccess,
+                  "hipHostMalloc failed");
+      s.ext = (int32_t*)p;
     }
     for (int i = 0; i < depth; ++i) empty_.push_back(i);
     if (synthetic_) {
-      for (int t = 0; t < std::max(1, threads); ++t) workers_.emplace_back([this] { produce(); });
+      for (int t = 0; t < threads_; ++t) workers_.emplace_back([this] { produce(); });
     }
   }
 
@@ -78,18 +93,54 @@ class BatchRing {
     workers_.clear();
   }
 
-  // consumer: block until a filled slot is available (releases the GIL while waiting)
+  // window mode: image i = tex[offs[i,0] : +H, offs[i,1] : +W], label labels[i]
+  void set_window_source(torch::Tensor tex, torch::Tensor offs, torch::Tensor labels) {
+    TORCH_CHECK(!synthetic_ && workers_.empty() && !window_, "BatchRing: source already set");
+    TORCH_CHECK(tex.device().is_cpu() && tex.scalar_type() == torch::kUInt8 && tex.dim() == 3 &&
+                    tex.size(2) == 3 && tex.is_contiguous(),
+                "set_window_source: tex must be a contiguous CPU uint8 [TH, TW, 3]");
+    TORCH_CHECK(offs.device().is_cpu() && offs.scalar_type() == torch::kInt64 && offs.dim() == 2 &&
+                    offs.size(1) == 2 && offs.is_contiguous(),
+                "set_window_source: offs must be CPU int64 [N, 2]");
+    TORCH_CHECK(labels.device().is_cpu() && labels.scalar_type() == torch::kInt64 &&
+                    labels.numel() == offs.size(0) && labels.is_contiguous(),
+                "set_window_source: labels must be CPU int64 [N]");
+    const int64_t TH = tex.size(0), TW = tex.size(1);
+    auto o = offs.accessor<int64_t, 2>();
+    for (int64_t i = 0; i < offs.size(0); ++i)  // every window inside the texture
+      TORCH_CHECK(o[i][0] >= 0 && o[i][1] >= 0 && o[i][0] + H_ <= TH && o[i][1] + W_ <= TW,
+                  "set_window_source: window ", i, " outside the texture");
+    tex_ = tex;
+    offs_ = offs;
+    wlabels_ = labels;
+    n_items_ = offs.size(0);
+    window_ = true;
+    for (int t = 0; t < threads_; ++t) workers_.emplace_back([this] { produce(); });
+  }
+
+  int64_t num_batches() const { return window_ ? (n_items_ + B_ - 1) / B_ : -1; }
+
+  // consumer: block until the NEXT batch (in batch-index order) is filled; releases the GIL
   std::tuple<int, torch::Tensor, torch::Tensor, int64_t> acquire() {
-    int id;
+    int id = -1;
     {
       pybind11::gil_scoped_release nogil;
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return !ready_.empty() || stopping_; });
-      TORCH_CHECK(!ready_.empty(), "BatchRing stopped");
-      id = ready_.front();
-      ready_.pop_front();
+      cv_.wait(lk, [&] { return find_ready() >= 0 || stopping_; });
+      id = find_ready();
+      TORCH_CHECK(id >= 0, "BatchRing stopped");
+      for (auto it = ready_.begin(); it != ready_.end(); ++it)
+        if (*it == id) { ready_.erase(it); break; }
+      next_consume_ += stride_;
     }
     return {id, view_img(id), view_labels(id), slots_[id].batch_index};
+  }
+
+  // (valid image count, pinned int32 [B,2] extents) of an acquired slot
+  std::tuple<int, torch::Tensor> info(int id) {
+    TORCH_CHECK(id >= 0 && id < (int)slots_.size(), "BatchRing: bad slot");
+    auto opt = torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true);
+    return {slots_[id].count, torch::from_blob(slots_[id].ext, {B_, 2}, opt)};
   }
 
   void release(int id) {
@@ -101,7 +152,7 @@ class BatchRing {
   }
 
   // external producer API (real-data mode): grab an empty slot, fill it, commit
-  std::tuple<int, torch::Tensor, torch::Tensor> acquire_empty() {
+  std::tuple<int, torch::Tensor, torch::Tensor, torch::Tensor> acquire_empty() {
     int id;
     {
       pybind11::gil_scoped_release nogil;
@@ -111,13 +162,21 @@ class BatchRing {
       id = empty_.front();
       empty_.pop_front();
     }
-    return {id, view_img(id), view_labels(id)};
+    auto opt = torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true);
+    return {id, view_img(id), view_labels(id), torch::from_blob(slots_[id].ext, {B_, 2}, opt)};
   }
 
-  void commit(int id, int64_t batch_index) {
+  void commit(int id, int64_t batch_index, int count) {
+    TORCH_CHECK(id >= 0 && id < (int)slots_.size(), "BatchRing: bad slot");
+    TORCH_CHECK(count >= 0 && count <= B_, "BatchRing: count outside [0, batch]");
+    for (int b = 0; b < count; ++b)
+      TORCH_CHECK(slots_[id].ext[2 * b] >= 1 && slots_[id].ext[2 * b] <= H_ &&
+                      slots_[id].ext[2 * b + 1] >= 1 && slots_[id].ext[2 * b + 1] <= W_,
+                  "BatchRing.commit: image ", b, " extent outside the slot pitch");
     {
       std::lock_guard<std::mutex> lk(mu_);
       slots_[id].batch_index = batch_index;
+      slots_[id].count = count;
       ready_.push_back(id);
     }
     cv_.notify_all();
@@ -126,6 +185,12 @@ class BatchRing {
   int depth() const { return (int)slots_.size(); }
 
  private:
+  int find_ready() const {  // the slot holding batch next_consume_, or -1
+    for (int id : ready_)
+      if (slots_[id].batch_index == next_consume_) return id;
+    return -1;
+  }
+
   torch::Tensor view_img(int id) {
     auto opt = torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true);
     return torch::from_blob(slots_[id].img, {B_, H_, W_, 3}, opt);
@@ -133,6 +198,13 @@ class BatchRing {
   torch::Tensor view_labels(int id) {
     auto opt = torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true);
     return torch::from_blob(slots_[id].labels, {B_}, opt);
+  }
+
+  void full_extents(Slot& s) {
+    for (int b = 0; b < B_; ++b) {
+      s.ext[2 * b] = H_;
+      s.ext[2 * b + 1] = W_;
+    }
   }
 
   void fill_synthetic(Slot& s, int64_t bidx) {
@@ -149,7 +221,29 @@ class BatchRing {
       }
       for (size_t i = n64 * 8; i < per_img; ++i) s.img[per_img * b + i] = (uint8_t)(x >> (i & 7));
     }
+    full_extents(s);
     s.batch_index = bidx;
+    s.count = B_;
+  }
+
+  void fill_window(Slot& s, int64_t bidx) {
+    const int64_t i0 = bidx * B_;
+    const int n = (int)std::min<int64_t>(B_, n_items_ - i0);
+    const uint8_t* tex = tex_.data_ptr<uint8_t>();
+    const int64_t TW = tex_.size(1);
+    const int64_t* off = offs_.data_ptr<int64_t>();
+    const int64_t* lab = wlabels_.data_ptr<int64_t>();
+    const size_t row = (size_t)W_ * 3;
+    for (int b = 0; b < n; ++b) {
+      const int64_t r0 = off[2 * (i0 + b)], c0 = off[2 * (i0 + b) + 1];
+      uint8_t* dst = s.img + (size_t)b * H_ * row;
+      for (int y = 0; y < H_; ++y)
+        std::memcpy(dst + (size_t)y * row, tex + ((r0 + y) * TW + c0) * 3, row);
+      s.labels[b] = lab[i0 + b];
+    }
+    full_extents(s);
+    s.batch_index = bidx;
+    s.count = n;
   }
 
   void produce() {
@@ -160,18 +254,17 @@ class BatchRing {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return !empty_.empty() || stopping_; });
         if (stopping_) return;
+        bidx = next_index_;
+        if (window_ && bidx * B_ >= n_items_) return;  // manifest exhausted
         id = empty_.front();
         empty_.pop_front();
-        bidx = next_index_;
         next_index_ += stride_;
       }
-      fill_synthetic(slots_[id], bidx);
+      if (window_) fill_window(slots_[id], bidx);
+      else fill_synthetic(slots_[id], bidx);
       {
         std::lock_guard<std::mutex> lk(mu_);
-        // keep batches in order: insert sorted by batch index
-        auto it = ready_.begin();
-        while (it != ready_.end() && slots_[*it].batch_index < bidx) ++it;
-        ready_.insert(it, id);
+        ready_.push_back(id);
       }
       cv_.notify_all();
     }
@@ -181,16 +274,22 @@ class BatchRing {
     for (auto& s : slots_) {
       if (s.img) (void)hipHostFree(s.img);
       if (s.labels) (void)hipHostFree(s.labels);
+      if (s.ext) (void)hipHostFree(s.ext);
       s.img = nullptr;
       s.labels = nullptr;
+      s.ext = nullptr;
     }
   }
 
   int B_, H_, W_;
   int64_t nc_;
   uint64_t seed_;
-  int64_t next_index_, stride_;
+  int64_t next_index_, next_consume_, stride_;
   bool synthetic_;
+  int threads_;
+  bool window_ = false;
+  torch::Tensor tex_, offs_, wlabels_;
+  int64_t n_items_ = 0;
   std::vector<Slot> slots_;
   std::deque<int> empty_, ready_;
   std::mutex mu_;
@@ -211,7 +310,11 @@ void register_bindings(pybind11::module_& m) {
       .def("acquire", &BatchRing::acquire)
       .def("release", &BatchRing::release)
       .def("acquire_empty", &BatchRing::acquire_empty)
-      .def("commit", &BatchRing::commit)
+      .def("commit", &BatchRing::commit, pybind11::arg("id"), pybind11::arg("batch_index"),
+           pybind11::arg("count"))
+      .def("info", &BatchRing::info)
+      .def("set_window_source", &BatchRing::set_window_source)
+      .def("num_batches", &BatchRing::num_batches)
       .def("stop", &BatchRing::stop)
       .def("depth", &BatchRing::depth);
   m.def("range_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); });

@@ -77,10 +77,12 @@ class DevicePrefetcher:
 
     def _recycle(self, force: bool = False) -> None:
         keep = []
-        for slot, ev in self._pending:
-            if force or ev.query():
-                if force:
-                    ev.synchronize()
+        depth = self.ring.depth()
+        for k, (slot, ev) in enumerate(self._pending):
+            # never hold every slot: the ring could then produce nothing and acquire()
+            # would wait forever - wait for the oldest copies instead
+            if force or ev.query() or len(self._pending) - k >= depth - 1:
+                ev.synchronize()
                 self.ring.release(slot)
             else:
                 keep.append((slot, ev))

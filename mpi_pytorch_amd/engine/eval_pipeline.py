@@ -9,26 +9,31 @@ passes from the checkpoint (:132-159); the per-predictor ``corrects / dataset_si
 SUM-reduced to rank 0 (:196) which logs ``Accuracy is ...`` (:199).  Needs >= 4 ranks.
 
 Here, on one MI355X:
-  stage 0  read/decode   host threads (PIL decode, or deterministic synthetic pixels) fill
-                         batches of uint8 images;
-  stage 1  transfer      pinned host -> HBM copy on a copy stream (event-ordered);
-  stage 2  resize+norm   the preprocess kernel (bicubic+antialias, mode 1, exactly the
-                         eval transform) on a preprocess stream, waiting on stage 1's event;
+  stage 0  read/decode   the native ``BatchRing`` (csrc/runtime): C++ threads copy each
+                         manifest row's synthetic image (a texture window,
+                         ``SyntheticImages``) into pinned slots, or PIL decode threads write
+                         real JPEGs into a slot (each image at its own extent inside the
+                         slot pitch); slots come back to the consumer in batch order;
+  stage 1  transfer      pinned slot -> HBM copy on a copy stream (event-ordered); the slot
+                         returns to the ring once its copy event has completed;
+  stage 2  resize+norm   the PIL-exact preprocess kernels (mode 1, bit-exact with PIL's
+                         uint8 resize, per-image extents) on a preprocess stream;
   stage 3  predict       ``lanes`` predictor lanes, each a HIP stream running a *batched*
                          eval forward + fused argmax/correct-count; each batch goes to a
                          lane chosen at random (reference behaviour) or round-robin.
 Stages overlap through events; ring depth bounds the in-flight batches (the end-of-stream
-sentinel is simply the end of the batch list).  Accuracy = sum over lanes of
-correct_lane / dataset_size, like the reference's reduce.  With several GPUs each rank
-takes an ``array_split`` shard and the per-rank partial accuracies are SUM-reduced
-(RCCL) - predictor fan-out across GPUs.
+sentinel is the ring's batch count).  Accuracy = sum over lanes of correct_lane /
+dataset_size, like the reference's reduce.  With several GPUs each rank takes an
+``array_split`` shard and the per-rank partial accuracies are SUM-reduced (RCCL) -
+predictor fan-out across GPUs.  The CPU path runs the same stages without streams.
 """
 from __future__ import annotations
 
 import os
 import time
+import threading
 from concurrent.futures import ThreadPoolExecutor
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -113,35 +118,28 @@ class StreamPipeline:
         return buf
 
     def _preprocess(self, imgs):
-        if isinstance(imgs, np.ndarray):
-            groups = [torch.from_numpy(imgs)]
-        else:
-            groups = [torch.from_numpy(np.ascontiguousarray(a))[None] for a in imgs]
-        outs = []
-        for g in groups:
-            if self.cuda:
-                g = self._staging(g)
-                with torch.cuda.stream(self.copy_stream):
-                    gd = g.to(self.device, non_blocking=True)
-                    copied = torch.cuda.Event()
-                    copied.record(self.copy_stream)
-                self._last_slot[1] = copied  # pinned slot free once this copy is done
-                self.prep_stream.wait_stream(self.copy_stream)
-                with torch.cuda.stream(self.prep_stream):
-                    gd.record_stream(self.prep_stream)
-                    outs.append(Fn.preprocess(gd, self.out_hw, IMAGENET_MEAN, IMAGENET_STD,
-                                              self.mode, self.cpad, pad=self.pad))
-            else:
-                outs.append(Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD,
-                                          self.mode, self.cpad, out_dtype=torch.float32,
-                                          pad=self.pad))
-        if self.cuda:
-            with torch.cuda.stream(self.prep_stream):
-                x = outs[0] if len(outs) == 1 else torch.cat(outs, 0)
-                ev = torch.cuda.Event()
-                ev.record(self.prep_stream)
-            return x, ev
-        return (outs[0] if len(outs) == 1 else torch.cat(outs, 0)), None
+        ext = None
+        if not isinstance(imgs, np.ndarray):  # decoded images of different sizes: one
+            imgs, ext = pad_batch(imgs)        # padded batch + extents, ONE preprocess
+        g = torch.from_numpy(imgs)
+        if not self.cuda:
+            return Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
+                                 self.cpad, out_dtype=torch.float32, pad=self.pad,
+                                 extents=ext), None
+        g = self._staging(g)
+        with torch.cuda.stream(self.copy_stream):
+            gd = g.to(self.device, non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record(self.copy_stream)
+        self._last_slot[1] = copied  # pinned slot free once this copy is done
+        self.prep_stream.wait_stream(self.copy_stream)
+        with torch.cuda.stream(self.prep_stream):
+            gd.record_stream(self.prep_stream)
+            x = Fn.preprocess(gd, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
+                              self.cpad, pad=self.pad, extents=ext)
+            ev = torch.cuda.Event()
+            ev.record(self.prep_stream)
+        return x, ev
 
     @torch.no_grad()
     def run(self, batches) -> List[int]:
@@ -171,6 +169,132 @@ class StreamPipeline:
             for s in self.lane_streams:
                 s.synchronize()
         return [int(c.item()) for c in self.counts]
+
+
+
+    @torch.no_grad()
+    def run_ring(self, ring, nbatches: int) -> List[int]:
+        """GPU stages fed by a native ``BatchRing``: no per-batch host copy, pinning or
+        Python image work on the consumer thread.  Returns per-lane correct counts."""
+        pending = []   # (slot, copy event): the slot returns to the ring once copied
+        inflight = []  # lane completion events (bounds the batches in flight)
+        depth = ring.depth()
+        for i in range(nbatches):
+            keep = []
+            for k, (slot, ev) in enumerate(pending):
+                if ev.query() or len(pending) - k >= depth - 1:
+                    ev.synchronize()
+                    ring.release(slot)
+                else:
+                    keep.append((slot, ev))
+            pending = keep
+            slot, img_h, lab_h, _bidx = ring.acquire()
+            n, ext_h = ring.info(slot)
+            ext = ext_h[:n].numpy().copy()
+            uniform = bool((ext[:, 0] == img_h.shape[1]).all() and (ext[:, 1] == img_h.shape[2]).all())
+            with torch.cuda.stream(self.copy_stream):
+                img_d = img_h[:n].to(self.device, non_blocking=True)
+                lab_d = lab_h[:n].to(self.device, non_blocking=True)
+                copied = torch.cuda.Event()
+                copied.record(self.copy_stream)
+            pending.append((slot, copied))
+            self.prep_stream.wait_event(copied)
+            with torch.cuda.stream(self.prep_stream):
+                img_d.record_stream(self.prep_stream)
+                x = Fn.preprocess(img_d, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
+                                  self.cpad, pad=self.pad, extents=None if uniform else ext)
+                prepped = torch.cuda.Event()
+                prepped.record(self.prep_stream)
+            lane = self._lane_for(i)
+            s = self.lane_streams[lane]
+            s.wait_event(prepped)
+            with torch.cuda.stream(s):
+                x.record_stream(s)
+                lab_d.record_stream(s)
+                out = self.model(x)
+                Fn.count_correct(out, lab_d, self.counts[lane])
+                done = torch.cuda.Event()
+                done.record(s)
+            inflight.append(done)
+            if len(inflight) >= self.depth:
+                inflight.pop(0).synchronize()
+            self.seen[lane] += n
+        for slot, ev in pending:
+            ev.synchronize()
+            ring.release(slot)
+        for s in self.lane_streams:
+            s.synchronize()
+        return [int(c.item()) for c in self.counts]
+
+
+def pad_batch(imgs):
+    """A list of uint8 HWC images of different sizes -> one zero-padded [B, Hmax, Wmax, 3]
+    batch and the per-image extents [B, 2] (each image at the top-left of its slot)."""
+    H = max(a.shape[0] for a in imgs)
+    W = max(a.shape[1] for a in imgs)
+    buf = np.zeros((len(imgs), H, W, 3), dtype=np.uint8)
+    for b, a in enumerate(imgs):
+        buf[b, :a.shape[0], :a.shape[1]] = a
+    return buf, np.array([a.shape[:2] for a in imgs], dtype=np.int64)
+
+
+def make_ring(names: Sequence[str], labels: Sequence[int], batch: int, source, num_classes: int,
+              depth: int = 8, threads: int = 4, pitch=None):
+    """Stage 0 on the native ring for one manifest shard.  ``SyntheticImages``: window mode
+    (C++ threads, bitwise ``source.load``).  ``FolderImages``: PIL decode threads write each
+    image into its slot at its own extent (``pitch`` = the largest image, from the
+    manifest's height/width columns when given).  Returns (ring, number of batches)."""
+    from ..ops import _ext
+    nb = (len(names) + batch - 1) // batch
+    if isinstance(source, SyntheticImages):
+        H, W = source.hw
+        ring = _ext.ext().BatchRing(batch, H, W, num_classes, depth, threads, 0, 0, 1, False)
+        offs = torch.tensor([source._offset(n) for n in names], dtype=torch.int64).view(-1, 2)
+        ring.set_window_source(torch.from_numpy(source.tex), offs,
+                               torch.as_tensor(np.asarray(labels, dtype=np.int64)))
+        return ring, nb
+    if pitch is None:
+        raise ValueError("make_ring: real images need the slot pitch (max height, width)")
+    ring = _ext.ext().BatchRing(batch, int(pitch[0]), int(pitch[1]), num_classes, depth, threads,
+                                0, 0, 1, False)
+    _feed_external(ring, list(names), np.asarray(labels, dtype=np.int64), batch, source, threads)
+    return ring, nb
+
+
+def _feed_external(ring, names, labels, batch, source, threads: int) -> None:
+    """PIL decode threads for real images: each takes the next batch index, an empty slot,
+    decodes its images straight into the slot (top-left, extent recorded) and commits it.
+    The ring hands batches to the consumer in index order."""
+    nb = (len(names) + batch - 1) // batch
+    lock = threading.Lock()
+    nxt = [0]
+
+    def worker():
+        from PIL import Image
+        while True:
+            with lock:
+                bi = nxt[0]
+                nxt[0] += 1
+            if bi >= nb:
+                return
+            try:
+                slot, img, lab, ext = ring.acquire_empty()
+            except RuntimeError:  # ring stopped
+                return
+            a = img.numpy()
+            e = ext.numpy()
+            lo, hi = bi * batch, min((bi + 1) * batch, len(names))
+            for b, j in enumerate(range(lo, hi)):
+                with Image.open(os.path.join(source.root, names[j])) as im:
+                    arr = np.asarray(im.convert("RGB"))
+                h, w = min(arr.shape[0], a.shape[1]), min(arr.shape[1], a.shape[2])
+                a[b, :h, :w] = arr[:h, :w]
+                e[b] = (h, w)
+                lab.numpy()[b] = labels[j]
+            ring.commit(slot, bi, hi - lo)
+
+    for _ in range(max(1, threads)):
+        threading.Thread(target=worker, name="mpa-decode", daemon=True).start()
 
 
 def _batches(names, labels, batch: int, source, prefetch: int = 2):
@@ -213,7 +337,19 @@ def run_pipeline(cfg: Config, ckpt_path: Optional[str] = None, max_images: int =
     pipe = StreamPipeline(model, world.device, out_hw, cfg.eval_lanes, assign=cfg.eval_assign,
                           seed=cfg.seed + world.rank)
     t0 = time.perf_counter()
-    counts = pipe.run(_batches(names, labels, cfg.eval_batch, source))
+    if world.device.type == "cuda":
+        pitch = None
+        if isinstance(source, FolderImages):
+            pitch = (int(shard["height"].max()), int(shard["width"].max())) \
+                if {"height", "width"} <= set(shard.columns) else (1024, 1024)
+        ring, nb = make_ring(names, labels, cfg.eval_batch, source, cfg.NUM_CLASSES,
+                             threads=max(2, cfg.num_workers), pitch=pitch)
+        try:
+            counts = pipe.run_ring(ring, nb)
+        finally:
+            ring.stop()
+    else:
+        counts = pipe.run(_batches(names, labels, cfg.eval_batch, source))
     dt = time.perf_counter() - t0
     acc_local = 0.0
     for lane, c in enumerate(counts):
@@ -230,16 +366,17 @@ def run_pipeline(cfg: Config, ckpt_path: Optional[str] = None, max_images: int =
 
 @torch.no_grad()
 def plain_eval(model, names, labels, batch, source, device, out_hw, mode=1) -> int:
-    """Non-pipelined batched evaluation (oracle for the pipeline tests)."""
+    """Non-pipelined batched evaluation (oracle for the pipeline tests): host batches,
+    one preprocess call per batch in the model's input layout (images of different sizes
+    padded into one batch with extents), forward, correct count."""
+    spec = input_spec(model, out_hw)
     correct = torch.zeros(1, dtype=torch.int64, device=device)
     for imgs, lab in _batches(names, labels, batch, source):
-        if isinstance(imgs, np.ndarray):
-            g = torch.from_numpy(imgs).to(device)
-            x = Fn.preprocess(g, out_hw, IMAGENET_MEAN, IMAGENET_STD, mode, 8,
-                              out_dtype=torch.float32)
-        else:
-            x = torch.cat([Fn.preprocess(torch.from_numpy(a)[None].to(device), out_hw,
-                                         IMAGENET_MEAN, IMAGENET_STD, mode, 8,
-                                         out_dtype=torch.float32) for a in imgs], 0)
+        ext = None
+        if not isinstance(imgs, np.ndarray):
+            imgs, ext = pad_batch(imgs)
+        g = torch.from_numpy(imgs).to(device)
+        x = Fn.preprocess(g, out_hw, IMAGENET_MEAN, IMAGENET_STD, mode, spec["cpad"],
+                          out_dtype=torch.float32, pad=spec["pad"], extents=ext)
         Fn.count_correct(model(x), lab.to(device), correct)
     return int(correct.item())

@@ -95,17 +95,17 @@ class ManifestBatches:
             x = Fn.preprocess(imgs, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
                               self.cpad, out_dtype=torch.float32, pad=self.pad)
             return x, labels.to(self.device, non_blocking=True)
-        if isinstance(imgs, np.ndarray):
-            groups = [torch.from_numpy(imgs)]
-        else:
-            groups = [torch.from_numpy(np.ascontiguousarray(a))[None] for a in imgs]
-        outs = []
-        for g in groups:
-            if cuda:
-                g = g.pin_memory().to(self.device, non_blocking=True)
-            outs.append(Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode,
-                                      self.cpad, out_dtype=torch.float32, pad=self.pad))
-        x = outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+        ext = None
+        if not isinstance(imgs, np.ndarray):
+            # decoded JPEGs of different sizes: one padded batch with per-image extents,
+            # so ONE pinned H2D copy and ONE preprocess launch per batch
+            from .eval_pipeline import pad_batch
+            imgs, ext = pad_batch(imgs)
+        g = torch.from_numpy(imgs)
+        if cuda:
+            g = g.pin_memory().to(self.device, non_blocking=True)
+        x = Fn.preprocess(g, self.out_hw, IMAGENET_MEAN, IMAGENET_STD, self.mode, self.cpad,
+                          out_dtype=torch.float32, pad=self.pad, extents=ext)
         y = labels.to(self.device, non_blocking=cuda)
         return x, y
 
