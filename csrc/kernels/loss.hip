@@ -13,6 +13,7 @@
 // backward writes zeros into the padding columns of dlogits.
 #include "common.h"
 #include "api.h"
+#include <cstdlib>
 #include <algorithm>
 
 namespace mpa {
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ 
 // fixed tree): bitwise reproducible, unlike one float atomic per row (whose order varies
 // between launches), and one launch like the memset it replaces.
 __global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restrict__ row_loss, int B,
-                                                          float* __restrict__ loss) {
+                                                          float* __restrict__ loss, int accumulate) {
   __shared__ float red[256];
   float a = 0.f;
   for (int i = threadIdx.x; i < B; i += 256) a += row_loss[i];
@@ -218,15 +219,28 @@ __global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restric
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss = red[0];
+  if (threadIdx.x == 0) {
+    if (accumulate) atomicAdd(loss, red[0]);
+    else *loss = red[0];
+  }
 }
+
+// Diagnostics only (MPA_DIAG_CE_MEMSET=1): the round-2 form of the loss - a memset of the
+// scalar followed by an atomic accumulation into it - for the HIP-graph replay A/B of
+// tools/graph_bisect.py (docs/NOTES.md "HIP graph replay")
+static bool g_diag_memset = [] {
+  const char* e = getenv("MPA_DIAG_CE_MEMSET");
+  return e && e[0] == '1';
+}();
 
 // loss: [1 + B] floats - the mean loss at [0], the per-row terms after it
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s) {
   float* rows = loss + 1;
+  if (g_diag_memset) (void)hipMemsetAsync(loss, 0, sizeof(float), s);
   ce_fwd_rows(logits, labels, B, NC, ld, rows, lse, s);
-  hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, loss);
+  hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, loss,
+                     (int)g_diag_memset);
 }
 
 void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
