@@ -160,12 +160,10 @@ class TrainStep:
         self._static_x = None
         self._static_y = None
         self._static_loss = None
-        # Measured on ROCm 7.2 / MI355X: back-to-back replays of the full-step graph with
-        # no host sync in between intermittently corrupt training state (NaN / 1e30
-        # losses, docs/NOTES.md "HIP graph replay"), while synced replays and eager
-        # execution are exact and equally fast for GPU-bound steps.  Graph mode therefore
-        # syncs after each replay unless MPA_GRAPH_UNSAFE=1.
-        self._sync_replay = os.environ.get("MPA_GRAPH_UNSAFE", "0") != "1"
+        # Back-to-back replays need no host sync: in deterministic mode 100 replays equal
+        # 100 eager steps bitwise (tests/test_determinism_gpu.py, tools/graph_bisect.py;
+        # docs/NOTES.md "HIP graph replay").  MPA_GRAPH_SYNC=1 restores a sync per replay.
+        self._sync_replay = os.environ.get("MPA_GRAPH_SYNC", "0") == "1"
         self.timer: Optional[StepTimer] = None
         # roctx ranges fwd / bwd / comm_wait / opt around the host enqueue of each phase
         # (rocprofv3 --marker-trace shows them beside the kernels); MPA_ROCTX=1
