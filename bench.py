@@ -91,6 +91,10 @@ def parse_args(argv=None):
                    help="diagnostics, with --emulate-comm: CUs the persistent conv grids leave "
                         "to the emulated collective while it is in flight")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--small-batch", type=int, default=128,
+                   help="after the headline measurement, also time --steps steps at this "
+                        "per-GPU batch (the reference's utils.py:40 BATCH_SIZE), eager and - "
+                        "on one GPU - HIP-graph replayed; reported as 'small_batch' (0: off)")
     p.add_argument("--print-losses", action="store_true", help="debug: sync + print each loss")
     p.add_argument("--timers", default="auto", choices=["auto", "on", "off"],
                    help="per-phase HIP-event times of the timed steps (data / forward / backward "
@@ -124,6 +128,30 @@ def spawn(argv, nprocs: int) -> int:
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod.launch(nprocs, [sys.executable, os.path.abspath(__file__)] + list(argv))
+
+
+def _timed(step, data, args, world, sync) -> float:
+    """Whole-job img/s of ``args.steps`` steps after ``args.warmup`` warm-up steps, bracketed
+    like the headline measurement (barrier + device sync, max time over ranks)."""
+    from mpi_pytorch_amd.parallel import barrier
+    for _ in range(max(args.warmup, 2)):
+        x, y = data.next()
+        step(x, y)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x, y = data.next()
+        step(x, y)
+    sync()
+    barrier()
+    sync()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=world.device)
+    if world.world_size > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return args.steps * data.batch * world.world_size / float(t.item())
 
 
 def run(args) -> None:
@@ -212,6 +240,21 @@ def run(args) -> None:
     dt = float(t.item())
     imgs = args.steps * args.batch * world.world_size
     value = imgs / dt
+    small = None
+    if args.small_batch and args.small_batch != args.batch and cuda and not args.emulate_comm:
+        step.timer = None
+        step.bucketer._stats = None
+        data.close()
+        data = DevicePrefetcher(dev, args.small_batch, hw, hw, args.classes, seed=4321,
+                                rank=world.rank, world=world.world_size, depth=6, threads=2,
+                                cpad=spec["cpad"], pad=spec["pad"])
+        small = {"per_gpu_batch": args.small_batch,
+                 "eager_img_per_s": round(_timed(step, data, args, world, sync), 1)}
+        if world.world_size == 1:
+            x, y = data.next()
+            if step.capture(x, y):
+                small["graph_img_per_s"] = round(_timed(step, data, args, world, sync), 1)
+        step.mean_loss()
     if world.rank == 0:
         rec = {
             "metric": "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X",
@@ -248,6 +291,8 @@ def run(args) -> None:
             rec["comm_ctas"] = step.bucketer.comm_ctas if step.bucketer.overlap_group else 0
         if comm is not None:
             rec["comm"] = comm
+        if small is not None:
+            rec["small_batch"] = small
         print(json.dumps(rec), flush=True)
     data.close()
     from mpi_pytorch_amd.parallel import shutdown

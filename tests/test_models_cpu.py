@@ -251,3 +251,33 @@ def test_pixel_pair_stem_state_dict_roundtrip():
     conv.load_state_dict({"weight": w})
     assert torch.equal(conv.state_dict()["weight"], w)
     assert tuple(conv.weight.shape) == (8, 7, 4, 8)
+
+
+def test_whole_model_gradients_are_shattered_in_fp32():
+    """Why model-level gradient DIRECTION cannot be a tight GPU check (docs/NOTES.md
+    "Numerics", utils/parity.py): on the CPU, in fp32, rounding only the input image to bf16
+    already turns ResNet-34's weight gradient by cos ~0.94 (Inception-v3 ~0.4), while 1e-6
+    noise leaves it at 0.9995.  The GPU tests therefore compare per unit, teacher-forced
+    (tests/test_layer_parity_gpu.py)."""
+    from mpi_pytorch_amd.engine import build_model, loss_fn
+    from mpi_pytorch_amd.parallel import World
+    torch.manual_seed(0)
+    m, _ = build_model("resnet34", 40, False, torch.device("cpu"), World())
+    torch.manual_seed(1)
+    x = torch.randn(4, 64, 64, 3) * 0.5
+    y = torch.randint(0, 40, (4,))
+
+    def grad(xx):
+        m._mpa_arena.grad.zero_()
+        for mod in m.modules():
+            if getattr(mod, "running_mean", None) is not None:
+                mod.running_mean.zero_()
+                mod.running_var.fill_(1.0)
+        loss_fn(m(xx), y).backward()
+        return m._mpa_arena.grad.clone()
+
+    g0 = grad(x)
+    cos = lambda a, b: float(F.cosine_similarity(a, b, dim=0))
+    c_bf16 = cos(g0, grad(x.to(torch.bfloat16).float()))
+    c_tiny = cos(g0, grad(x * (1 + 1e-6 * torch.randn_like(x))))
+    assert c_tiny > 0.999 and c_bf16 < 0.99, (c_tiny, c_bf16)
