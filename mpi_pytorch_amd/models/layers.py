@@ -436,25 +436,38 @@ class FusedSequential(nn.Sequential):
     Conv(no bias)->BN[->ReLU] => conv_bn_act; Conv->ReLU => conv_act(relu); Linear->ReLU
     => linear_act(relu)."""
 
-    def forward(self, x):
+    def groups(self):
+        """The fused execution groups: (first index, end index, kind) over the children."""
         mods = list(self._modules.values())
-        i = 0
-        n = len(mods)
+        out, i, n = [], 0, len(mods)
         while i < n:
             m = mods[i]
             nxt = mods[i + 1] if i + 1 < n else None
             nxt2 = mods[i + 2] if i + 2 < n else None
             if isinstance(m, Conv2d) and isinstance(nxt, BatchNorm2d):
-                relu = isinstance(nxt2, ReLU)
-                x = Fn.conv_bn_act(x, m, nxt, relu=relu)
-                i += 3 if relu else 2
-            elif isinstance(m, (Conv2d, Linear)) and isinstance(nxt, ReLU):
-                x = m(x, relu=True)
-                i += 2
-            elif isinstance(m, BatchNorm2d) and isinstance(nxt, ReLU):
-                x = m(x, relu=True)
-                i += 2
+                k = 3 if isinstance(nxt2, ReLU) else 2
+                out.append((i, i + k, "conv_bn_relu" if k == 3 else "conv_bn"))
+            elif isinstance(m, (Conv2d, Linear, BatchNorm2d)) and isinstance(nxt, ReLU):
+                k = 2
+                out.append((i, i + 2, "relu"))
             else:
-                x = m(x)
-                i += 1
+                k = 1
+                out.append((i, i + 1, "plain"))
+            i += k
+        return out
+
+    def run_group(self, g, x):
+        """Execute fused group ``g`` = (first, end, kind) of :meth:`groups` on ``x``."""
+        mods = list(self._modules.values())
+        i, _e, kind = g
+        if kind.startswith("conv_bn"):
+            return Fn.conv_bn_act(x, mods[i], mods[i + 1], relu=kind == "conv_bn_relu")
+        if kind == "relu":
+            return mods[i](x, relu=True)
+        return mods[i](x)
+
+    def forward(self, x):
+        run = self.run_group
+        for g in self.groups():
+            x = run(g, x)
         return x

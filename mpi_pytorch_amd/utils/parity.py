@@ -73,6 +73,29 @@ def unit_modules(model: nn.Module) -> List[Tuple[str, nn.Module]]:
     return out
 
 
+def _tapped_groups(name: str, fs, rec: Dict):
+    """An instance-level ``run_group`` for a FusedSequential that records every group with
+    parameters as unit ``name[first:end]`` (input / output values and gradients)."""
+    cls_run = type(fs).run_group
+    mods = list(fs._modules.values())
+
+    def run_group(g, x):
+        i0, i1, kind = g
+        if not any(p.requires_grad for mm in mods[i0:i1] for p in mm.parameters()):
+            return cls_run(fs, g, x)
+        key = "%s[%d:%d]" % (name, i0, i1)
+        r = rec.setdefault(key, {"calls": 0, "group": g, "fs": name, "fs_mod": fs,
+                                 "kind": kind})
+        r["calls"] += 1
+        bx, by = [], []
+        r["x"], r["gx"] = x.detach().clone(), bx
+        out = cls_run(fs, g, _Tap.apply(x, bx))
+        r["y"], r["gy"] = out.detach().clone(), by
+        return _Tap.apply(out, by)
+
+    return run_group
+
+
 def _cos(a: torch.Tensor, b: torch.Tensor) -> float:
     a, b = a.double().flatten(), b.double().flatten()
     na, nb = float(a.norm()), float(b.norm())
@@ -122,7 +145,14 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             return _Tap.apply(out, box)
         return fn
 
+    from ..models.layers import FusedSequential
+    patched = []
     for name, m in units:
+        if isinstance(m, FusedSequential):
+            # a fused stack (VGG / AlexNet): every fused group with parameters is a unit
+            patched.append(m)
+            m.run_group = _tapped_groups(name, m, rec)
+            continue
         hooks.append(m.register_forward_pre_hook(pre(name)))
         hooks.append(m.register_forward_hook(post(name)))
     try:
@@ -135,24 +165,38 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
     finally:
         for h in hooks:
             h.remove()
+        for m in patched:
+            del m.run_group
     g_gpu = arena.grad.detach().cpu()
     out = []
-    for name, m in units:
-        r = rec.get(name)
-        if r is None or r["calls"] != 1 or not r["gy"]:
+    plain = {name: m for name, m in units}
+    for name in list(rec.keys()):
+        r = rec[name]
+        if r["calls"] != 1 or not r.get("gy"):
             continue  # not reached (e.g. aux head in eval) or reused
-        mc = cpu_mods[name]
         ac = model_cpu._mpa_arena
         ac.zero_grad()
-        if isinstance(r["x"], list):
-            xc = torch.cat([t.float().cpu() for t in r["x"]], -1).requires_grad_(True)
-            yc = mc([xc])
-            gx_gpu = torch.cat([b[0].float().cpu() if b else torch.zeros_like(t.float().cpu())
-                                for b, t in zip(r["gx"], r["x"])], -1)
-        else:
+        if "group" in r:  # a fused group of a FusedSequential stack
+            fs_g, fs_c = r["fs_mod"], cpu_mods[r["fs"]]
+            i0, i1, _k = r["group"]
+            m = nn.ModuleList(list(fs_g._modules.values())[i0:i1])
+            mc = nn.ModuleList(list(fs_c._modules.values())[i0:i1])
             xc = r["x"].float().cpu().requires_grad_(True)
-            yc = mc(xc)
+            yc = fs_c.run_group(r["group"], xc)
             gx_gpu = r["gx"][0].float().cpu() if r["gx"] else None
+        else:
+            m = plain[name]
+            mc = cpu_mods[name]
+            if isinstance(r["x"], list):
+                xc = torch.cat([t.float().cpu() for t in r["x"]], -1).requires_grad_(True)
+                yc = mc([xc])
+                gx_gpu = torch.cat([b[0].float().cpu() if b else
+                                    torch.zeros_like(t.float().cpu())
+                                    for b, t in zip(r["gx"], r["x"])], -1)
+            else:
+                xc = r["x"].float().cpu().requires_grad_(True)
+                yc = mc(xc)
+                gx_gpu = r["gx"][0].float().cpu() if r["gx"] else None
         yg = r["y"].float().cpu()
         if yc.shape != yg.shape:  # padded head columns etc.: compare the common slice
             yg = yg[..., :yc.shape[-1]]
@@ -169,7 +213,7 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             oc, ec = ac.slice_of(p_c)
             pg.append(g_gpu[o:e])
             pc.append(g_cpu[oc:ec])
-        row = {"unit": name, "type": type(m).__name__,
+        row = {"unit": name, "type": r.get("kind", type(m).__name__),
                "y_cos": _cos(yg, yc.detach()), "y_ratio": _ratio(yg, yc.detach())}
         if gx_gpu is not None and xc.grad is not None and r["x"] is not None and \
                 getattr(r["x"] if not isinstance(r["x"], list) else r["x"][0], "dtype",
