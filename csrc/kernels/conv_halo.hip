@@ -805,6 +805,12 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   return (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
 }
 
+// MPA_HALO_WRES=0: no resident-weight variant (A/B of the 64-channel layers)
+static const bool g_halo_wres = [] {
+  const char* e = getenv("MPA_HALO_WRES");
+  return !(e && atoi(e) == 0);
+}();
+
 // Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves; each MFMA wave then has
 // 256 registers, which every flavour fits).  MPA_HALO_PROD=0: 4-wave blocks.
 static const bool g_halo_prod = [] {
@@ -861,7 +867,7 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   int g8 = std::min(std::min(active_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
-  const bool wres = a.tiles_n == 1 && h.cc <= 2;
+  const bool wres = g_halo_wres && a.tiles_n == 1 && h.cc <= 2;
   switch (halo_epi(a)) {
     case 0: launch_halo<0>(wres, grid, a, h, s); break;
     case EP_BETA: launch_halo<EP_BETA>(wres, grid, a, h, s); break;
