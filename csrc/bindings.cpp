@@ -849,6 +849,45 @@ Tensor concat_channels(std::vector<Tensor> xs) {
   return y;
 }
 
+// G[..., off:off+C] (+)= src  (G fp32 [..., Ctot], src bf16 [..., C], same leading dims)
+void chan_accum(Tensor g, int64_t off, Tensor src, bool assign) {
+  CHECK_ACT(src);
+  CHECK_CUDA(g);
+  CHECK_CONTIG(g);
+  CHECK_F32(g);
+  const int64_t ctot = g.size(-1), cs = src.size(-1);
+  TORCH_CHECK(g.dim() == src.dim() && g.numel() / ctot == src.numel() / cs,
+              "chan_accum: leading dims differ");
+  TORCH_CHECK(ctot % 8 == 0 && cs % 8 == 0 && off % 8 == 0 && off >= 0 && off + cs <= ctot,
+              "chan_accum: channel range outside G (multiples of 8 required)");
+  const int64_t pixels = src.numel() / cs;
+  TORCH_CHECK(pixels * (cs / 8) < (int64_t(1) << 31), "chan_accum: too large");
+  const c10::OptionalDeviceGuard gd(device_of(g));
+  if (pixels > 0)
+    mpa::chan_accum(g.data_ptr<float>(), (int)ctot, (int)off, bp(src), (int)cs, (int)pixels, assign,
+                    cur_stream());
+}
+
+// bf16 copy of G[..., off:off+C]
+Tensor chan_extract(Tensor g, int64_t off, int64_t cs) {
+  CHECK_CUDA(g);
+  CHECK_CONTIG(g);
+  CHECK_F32(g);
+  const int64_t ctot = g.size(-1);
+  TORCH_CHECK(ctot % 8 == 0 && cs % 8 == 0 && off % 8 == 0 && off >= 0 && off + cs <= ctot && cs > 0,
+              "chan_extract: channel range outside G (multiples of 8 required)");
+  const int64_t pixels = g.numel() / ctot;
+  TORCH_CHECK(pixels * (cs / 8) < (int64_t(1) << 31), "chan_extract: too large");
+  const c10::OptionalDeviceGuard gd(device_of(g));
+  std::vector<int64_t> shape(g.sizes().begin(), g.sizes().end());
+  shape.back() = cs;
+  Tensor out = torch::empty(shape, g.options().dtype(torch::kBFloat16));
+  if (pixels > 0)
+    mpa::chan_extract(g.data_ptr<float>(), (int)ctot, (int)off, bpm(out), (int)cs, (int)pixels,
+                      cur_stream());
+  return out;
+}
+
 std::vector<Tensor> split_channels(Tensor dy, std::vector<int64_t> sizes) {
   CHECK_ACT(dy);
   TORCH_CHECK(dy.dim() >= 2 && !sizes.empty(), "split_channels: dy must be [..., C]");
@@ -951,6 +990,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("transpose_krsc", &transpose_krsc);
+  m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
+  m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");
   m.def("preprocess_pil", &preprocess_pil, "PIL-exact bicubic resize + ToTensor + Normalize");
   m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
         py::arg("std"), py::arg("mode"), py::arg("cpad"),

@@ -246,6 +246,12 @@ void adaptive_avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P,
 
 // concat.hip (NHWC channel concat / split; every segment's channels % 8 == 0)
 constexpr int CAT_MAXSEG = 32;
+// fp32 gradient buffer G [pixels][ldg]: G[:, off:off+cs] (+)= src (bf16 [pixels][cs]) /
+// dst = bf16(G[:, off:off+cs]); ldg, off, cs multiples of 8
+void chan_accum(float* g, int ldg, int off, const bf16_raw* src, int cs, int pixels, bool assign,
+                hipStream_t s);
+void chan_extract(const float* g, int ldg, int off, bf16_raw* dst, int cs, int pixels,
+                  hipStream_t s);
 void concat_channels(const bf16_raw* const* xs, const int* chans, int nseg, int pixels,
                      int ctotal, bf16_raw* y, hipStream_t s);
 void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, int ctotal,

@@ -78,4 +78,62 @@ void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, 
   launch(true, dxs, chans, nseg, pixels, ctotal, const_cast<bf16_raw*>(dy), s);
 }
 
+// ------------------------------------------------------- fp32 channel-range accumulator
+// A dense block's gradient buffer G [pixels][ldg] (fp32): every layer's input gradient
+// (bf16, channels [0, cs) of the block's joined features) is ADDED into G's first cs
+// channels, and each layer reads its output gradient back as a bf16 channel range - one
+// launch per layer instead of autograd's split + one elementwise add per earlier feature
+// (models/densenet.py).  8 channels per thread (16-B bf16 / 32-B fp32 vectors).
+__global__ void __launch_bounds__(256) chan_accum_kernel(float* __restrict__ g, int ldg8, int off8,
+                                                         const bf16_raw* __restrict__ src, int cs8,
+                                                         int pixels, int assign) {
+  const unsigned n = (unsigned)pixels * (unsigned)cs8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned px = i / (unsigned)cs8, v = i - px * (unsigned)cs8;
+    const uint4 b = reinterpret_cast<const uint4*>(src)[i];
+    float4* d = reinterpret_cast<float4*>(g + ((int64_t)px * ldg8 + off8 + v) * 8);
+    const float4 lo = make_float4(__uint_as_float(b.x << 16), __uint_as_float(b.x & 0xffff0000u),
+                                  __uint_as_float(b.y << 16), __uint_as_float(b.y & 0xffff0000u));
+    const float4 hi = make_float4(__uint_as_float(b.z << 16), __uint_as_float(b.z & 0xffff0000u),
+                                  __uint_as_float(b.w << 16), __uint_as_float(b.w & 0xffff0000u));
+    if (assign) {
+      d[0] = lo;
+      d[1] = hi;
+    } else {
+      float4 a = d[0], c = d[1];
+      d[0] = make_float4(a.x + lo.x, a.y + lo.y, a.z + lo.z, a.w + lo.w);
+      d[1] = make_float4(c.x + hi.x, c.y + hi.y, c.z + hi.z, c.w + hi.w);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) chan_extract_kernel(const float* __restrict__ g, int ldg8,
+                                                           int off8, bf16_raw* __restrict__ dst,
+                                                           int cs8, int pixels) {
+  const unsigned n = (unsigned)pixels * (unsigned)cs8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned px = i / (unsigned)cs8, v = i - px * (unsigned)cs8;
+    const float4* s4 = reinterpret_cast<const float4*>(g + ((int64_t)px * ldg8 + off8 + v) * 8);
+    const float4 a = s4[0], c = s4[1];
+    reinterpret_cast<uint4*>(dst)[i] = make_uint4(pack2(a.x, a.y), pack2(a.z, a.w),
+                                                  pack2(c.x, c.y), pack2(c.z, c.w));
+  }
+}
+
+static int chan_grid(int64_t work) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 8192));
+}
+
+void chan_accum(float* g, int ldg, int off, const bf16_raw* src, int cs, int pixels, bool assign,
+                hipStream_t s) {
+  hipLaunchKernelGGL(chan_accum_kernel, dim3(chan_grid((int64_t)pixels * cs / 8)), dim3(256), 0, s,
+                     g, ldg / 8, off / 8, src, cs / 8, pixels, assign ? 1 : 0);
+}
+
+void chan_extract(const float* g, int ldg, int off, bf16_raw* dst, int cs, int pixels,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(chan_extract_kernel, dim3(chan_grid((int64_t)pixels * cs / 8)), dim3(256), 0,
+                     s, g, ldg / 8, off / 8, dst, cs / 8, pixels);
+}
+
 }  // namespace mpa

@@ -6,6 +6,8 @@ kernel over the concatenated features (channel concat = last-dim concat in NHWC)
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -31,6 +33,11 @@ class _DenseLayer(nn.Module):
         return self.conv2(x)
 
 
+# MPA_DENSE_BLOCK_GRAD=0: plain autograd through the per-layer concats (one split and one
+# elementwise add per earlier feature and layer) instead of the block-level accumulator
+_BLOCK_GRAD = os.environ.get("MPA_DENSE_BLOCK_GRAD", "1") == "1"
+
+
 class _DenseBlock(nn.ModuleDict):
     def __init__(self, num_layers, num_input_features, bn_size, growth_rate):
         super().__init__()
@@ -40,10 +47,66 @@ class _DenseBlock(nn.ModuleDict):
                                         bn_size))
 
     def forward(self, x):
+        if _BLOCK_GRAD and self.training and torch.is_grad_enabled() and x.requires_grad:
+            params = [p for p in self.parameters() if p.requires_grad]
+            return _DenseBlockGrad.apply(x, self, *params)
         feats = [x]
         for layer in self.values():
             feats.append(layer(feats))
         return Fn.cat_channels(feats)
+
+
+class _DenseBlockGrad(torch.autograd.Function):
+    """A dense block whose backward sums every feature's gradient in ONE fp32 buffer.
+
+    Each feature feeds every later layer (through that layer's input concat) and the
+    block output, so plain autograd splits each layer's input gradient into per-feature
+    pieces and adds them feature by feature: O(L^2) small split / add launches per block
+    (535 ATen adds per DenseNet-121 step).  Here the forward runs each layer on a leaf
+    copy of its concatenated input (its own small autograd graph, kept for backward), and
+    the backward walks the layers in reverse with G = the block gradient [..., C_total] in
+    fp32: layer i's output gradient is read from G's channels of feature i
+    (``chan_extract``), its graph is back-propagated, and its input gradient is added to
+    G's first C_i channels (``chan_accum``, one launch).  Parameter gradients land in the
+    flat arena from the layers' own kernels, as in every other model."""
+
+    @staticmethod
+    def forward(ctx, x, block, *params):
+        feats = [x.detach()]
+        recs = []
+        with torch.enable_grad():
+            for layer in block.values():
+                inp = Fn.cat_channels(feats) if len(feats) > 1 else feats[0]
+                inp = inp.detach().requires_grad_(True)
+                out = layer([inp])
+                recs.append((inp, out))
+                feats.append(out.detach())
+        ctx.recs = recs
+        ctx.sizes = [f.shape[-1] for f in feats]
+        ctx.nparams = len(params)
+        return Fn.cat_channels(feats)
+
+    @staticmethod
+    def backward(ctx, gy):
+        k = Fn.K(gy)
+        gy = gy.contiguous()
+        ctot = gy.shape[-1]
+        g = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
+        k.chan_accum(g, 0, gy, True)
+        offs = []
+        o = 0
+        for c in ctx.sizes:
+            offs.append(o)
+            o += c
+        for i in range(len(ctx.recs) - 1, -1, -1):
+            inp, out = ctx.recs[i]
+            g_out = k.chan_extract(g, offs[i + 1], ctx.sizes[i + 1]).to(out.dtype)
+            torch.autograd.backward(out, g_out)
+            if inp.grad is not None:
+                k.chan_accum(g, 0, inp.grad, False)
+            ctx.recs[i] = None
+        dx = k.chan_extract(g, 0, ctx.sizes[0]).to(gy.dtype)
+        return (dx, None) + (None,) * ctx.nparams
 
 
 class _Transition(nn.Sequential):

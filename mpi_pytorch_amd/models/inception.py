@@ -10,6 +10,7 @@ through the same implicit-GEMM engine via its tap table.
 """
 from __future__ import annotations
 
+import os
 from collections import namedtuple
 
 import torch
@@ -17,6 +18,9 @@ import torch.nn as nn
 
 from .layers import (Conv2d, BatchNorm2d, Linear, MaxPool2d, AdaptiveAvgPool2d, Dropout)
 from ..ops import functional as Fn
+
+# MPA_GRAD_JOIN=0: autograd's elementwise adds sum the branch gradients of a block input
+_JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
 
 InceptionOutputs = namedtuple("InceptionOutputs", ["logits", "aux_logits"])
 
@@ -27,20 +31,30 @@ class BasicConv2d(nn.Module):
         self.conv = Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False)
         self.bn = BatchNorm2d(out_channels, eps=0.001)
 
-    def forward(self, x):
-        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True)
+    def forward(self, x, join=None):
+        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True, join_x=join)
 
 
-def _avg3(x):
-    return Fn.avg_pool2d(x, (3, 3), (1, 1), (1, 1), False, True)
+def _avg3(x, join=None):
+    return Fn.avg_pool2d(x, (3, 3), (1, 1), (1, 1), False, True, join=join)
 
 
-def _max3s2(x):
-    return Fn.max_pool2d(x, (3, 3), (2, 2), (0, 0), False)
+def _max3s2(x, join=None):
+    return Fn.max_pool2d(x, (3, 3), (2, 2), (0, 0), False, join=join)
 
 
 def _cat(xs):
     return Fn.cat_channels(xs)
+
+
+def _join(mod, x, n, join=None):
+    """The GradJoin of an input read by ``n`` branches (None outside training); a parent
+    passes its own join when x has consumers outside this block (Mixed_6e -> aux head)."""
+    if join is not None:
+        return join
+    if _JOIN and mod.training and torch.is_grad_enabled() and x.requires_grad:
+        return Fn.GradJoin(n)
+    return None
 
 
 class InceptionA(nn.Module):
@@ -54,11 +68,12 @@ class InceptionA(nn.Module):
         self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, padding=1)
         self.branch_pool = BasicConv2d(in_channels, pool_features, 1)
 
-    def forward(self, x):
-        b1 = self.branch1x1(x)
-        b5 = self.branch5x5_2(self.branch5x5_1(x))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
-        bp = self.branch_pool(_avg3(x))
+    def forward(self, x, join=None):
+        j = _join(self, x, 4, join)
+        b1 = self.branch1x1(x, j)
+        b5 = self.branch5x5_2(self.branch5x5_1(x, j))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)))
+        bp = self.branch_pool(_avg3(x, j))
         return _cat([b1, b5, b3, bp])
 
 
@@ -70,10 +85,11 @@ class InceptionB(nn.Module):
         self.branch3x3dbl_2 = BasicConv2d(64, 96, 3, padding=1)
         self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, stride=2)
 
-    def forward(self, x):
-        b3 = self.branch3x3(x)
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
-        return _cat([b3, bd, _max3s2(x)])
+    def forward(self, x, join=None):
+        j = _join(self, x, 3, join)
+        b3 = self.branch3x3(x, j)
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)))
+        return _cat([b3, bd, _max3s2(x, j)])
 
 
 class InceptionC(nn.Module):
@@ -91,14 +107,15 @@ class InceptionC(nn.Module):
         self.branch7x7dbl_5 = BasicConv2d(c7, 192, (1, 7), padding=(0, 3))
         self.branch_pool = BasicConv2d(in_channels, 192, 1)
 
-    def forward(self, x):
-        b1 = self.branch1x1(x)
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x)))
-        bd = self.branch7x7dbl_1(x)
+    def forward(self, x, join=None):
+        j = _join(self, x, 4, join)
+        b1 = self.branch1x1(x, j)
+        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, j)))
+        bd = self.branch7x7dbl_1(x, j)
         for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
                   self.branch7x7dbl_5):
             bd = m(bd)
-        bp = self.branch_pool(_avg3(x))
+        bp = self.branch_pool(_avg3(x, j))
         return _cat([b1, b7, bd, bp])
 
 
@@ -112,12 +129,13 @@ class InceptionD(nn.Module):
         self.branch7x7x3_3 = BasicConv2d(192, 192, (7, 1), padding=(3, 0))
         self.branch7x7x3_4 = BasicConv2d(192, 192, 3, stride=2)
 
-    def forward(self, x):
-        b3 = self.branch3x3_2(self.branch3x3_1(x))
-        b7 = self.branch7x7x3_1(x)
+    def forward(self, x, join=None):
+        j = _join(self, x, 3, join)
+        b3 = self.branch3x3_2(self.branch3x3_1(x, j))
+        b7 = self.branch7x7x3_1(x, j)
         for m in (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4):
             b7 = m(b7)
-        return _cat([b3, b7, _max3s2(x)])
+        return _cat([b3, b7, _max3s2(x, j)])
 
 
 class InceptionE(nn.Module):
@@ -133,14 +151,19 @@ class InceptionE(nn.Module):
         self.branch3x3dbl_3b = BasicConv2d(384, 384, (3, 1), padding=(1, 0))
         self.branch_pool = BasicConv2d(in_channels, 192, 1)
 
-    def forward(self, x):
-        b1 = self.branch1x1(x)
-        b3 = self.branch3x3_1(x)
-        b3 = _cat([self.branch3x3_2a(b3), self.branch3x3_2b(b3)])
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x))
-        bd = _cat([self.branch3x3dbl_3a(bd), self.branch3x3dbl_3b(bd)])
-        bp = self.branch_pool(_avg3(x))
-        return _cat([b1, b3, bd, bp])
+    def forward(self, x, join=None):
+        j = _join(self, x, 4, join)
+        b1 = self.branch1x1(x, j)
+        b3 = self.branch3x3_1(x, j)
+        j3 = _join(self, b3, 2)  # b3 and bd each feed a (1x3) and a (3x1) conv
+        b3a, b3b = self.branch3x3_2a(b3, j3), self.branch3x3_2b(b3, j3)
+        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, j))
+        jd = _join(self, bd, 2)
+        bda, bdb = self.branch3x3dbl_3a(bd, jd), self.branch3x3dbl_3b(bd, jd)
+        bp = self.branch_pool(_avg3(x, j))
+        # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
+        # as one flat concat, which copies every branch once instead of twice
+        return _cat([b1, b3a, b3b, bda, bdb, bp])
 
 
 class InceptionAux(nn.Module):
@@ -153,8 +176,8 @@ class InceptionAux(nn.Module):
         self.fc.stddev = 0.001
         self.avgpool = AdaptiveAvgPool2d((1, 1))
 
-    def forward(self, x):
-        x = Fn.avg_pool2d(x, (5, 5), (3, 3), (0, 0), False, True)
+    def forward(self, x, join=None):
+        x = Fn.avg_pool2d(x, (5, 5), (3, 3), (0, 0), False, True, join=join)
         x = self.conv1(self.conv0(x))
         x = self.avgpool(x).reshape(x.shape[0], -1)
         return self.fc(x)
@@ -165,6 +188,7 @@ class Inception3(nn.Module):
         super().__init__()
         self.aux_logits = aux_logits
         self.transform_input = False
+        self.cross_join = True
         self.Conv2d_1a_3x3 = BasicConv2d(3, 32, 3, stride=2)
         self.Conv2d_2a_3x3 = BasicConv2d(32, 32, 3)
         self.Conv2d_2b_3x3 = BasicConv2d(32, 64, 3, padding=1)
@@ -200,8 +224,15 @@ class Inception3(nn.Module):
             x = m(x)
         aux = None
         if self.AuxLogits is not None and self.training:
-            aux = self.AuxLogits(x)
-        for m in (self.Mixed_7a, self.Mixed_7b, self.Mixed_7c):
+            # Mixed_6e's output feeds the aux head's pool and Mixed_7a's three branches
+            # (cross_join = False keeps the two modules' input gradients apart, for the
+            # per-unit parity check of utils/parity.py)
+            j = _join(self.Mixed_7a, x, 4) if self.cross_join else None
+            aux = self.AuxLogits(x, j)
+            x = self.Mixed_7a(x, j)
+        else:
+            x = self.Mixed_7a(x)
+        for m in (self.Mixed_7b, self.Mixed_7c):
             x = m(x)
         x = self.avgpool(x).reshape(x.shape[0], -1)
         x = self.dropout(x)

@@ -93,27 +93,37 @@ class BNLink:
 
 
 class GradJoin:
-    """Two gradient contributions to ONE activation, summed without a separate add pass.
+    """Several gradient contributions to ONE activation, summed without separate add passes.
 
     A residual block's input x feeds two ops (conv1 and the shortcut: identity or the
-    downsample conv), so autograd would sum two bf16 gradients with an elementwise add -
-    a full extra read/read/write sweep of the activation per block.  Instead both ops hold
-    the same join.  Whichever backward runs first PARKS its contribution here and returns
-    None for x: an already computed tensor (the identity shortcut's BN gradient), or, for
-    a dgrad, the deferred launch itself.  The second op then produces the sum: one dgrad
-    writes fresh, the other accumulates into it in its GEMM epilogue
-    (``conv_dgrad(..., accum=)``: fp32 add, one rounding).  The fresh one is chosen to be a
-    dgrad that covers every pixel, so a 1x1/s2 downsample (three of four stride phases
-    without taps) never needs a zero fill.  Independent of autograd's execution order."""
+    downsample conv); an Inception block's input feeds three or four branches (1x1 convs
+    and a pool).  Autograd would sum those bf16 gradients with elementwise adds - a full
+    extra read/read/write sweep of the activation per extra consumer.  Instead all
+    consumers hold the same join, created with ``expected`` = their number.  Each backward
+    that runs hands its contribution to the join and returns None for x, except the LAST
+    one, which returns the sum: a computed tensor (a pool or BN gradient) becomes the
+    running partial, a dgrad is parked as the deferred launch itself and later either
+    writes fresh or accumulates into the partial in its GEMM epilogue
+    (``conv_dgrad(..., accum=)``: fp32 add, one rounding per contribution).  A fresh write is
+    given to a dgrad that covers every pixel, so a 1x1/s2 downsample (three of four stride
+    phases without taps) never needs a zero fill.  Independent of autograd's execution
+    order (autograd runs x's producer only after every consumer's backward)."""
 
-    __slots__ = ("partial",)
+    __slots__ = ("partial", "expected", "arrived")
 
-    def __init__(self):
+    def __init__(self, expected: int = 2):
         self.partial = None
+        self.expected = int(expected)
+        self.arrived = 0
 
     def take(self):
         p, self.partial = self.partial, None
         return p
+
+    def arrive(self) -> bool:
+        """Count one contribution; True when it is the last."""
+        self.arrived += 1
+        return self.arrived >= self.expected
 
 
 class _Deferred:
@@ -128,16 +138,21 @@ class _Deferred:
 
 def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
     """Offer a computed contribution ``t`` to ``join``; returns what the op hands back to
-    autograd."""
+    autograd (the sum if it is the last contribution, else None)."""
     if join is None or t is None:
         return t
+    last = join.arrive()
     prev = join.take()
     if prev is None:
-        join.partial = t
-        return None
-    if isinstance(prev, _Deferred):
-        return prev.run(t)  # the parked dgrad accumulates into t
-    return prev.add_(t)  # two computed tensors (not produced by the ResNet blocks)
+        acc = t
+    elif isinstance(prev, _Deferred):
+        acc = prev.run(t)  # the parked dgrad accumulates into t
+    else:
+        acc = prev.add_(t)  # two computed tensors (no zoo model produces this pair)
+    if last:
+        return acc
+    join.partial = acc
+    return None
 
 
 def _dgrad_full(conv, in_hw) -> bool:
@@ -148,7 +163,7 @@ def _dgrad_full(conv, in_hw) -> bool:
 
 
 def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
-    """conv dgrad, summed with the join's other contribution (see GradJoin)."""
+    """conv dgrad, summed with the join's other contributions (see GradJoin)."""
     sh, sw, ph, pw = conv.kgeom
 
     def run(acc):
@@ -156,16 +171,25 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
 
     if join is None:
         return run(None)
+    last = join.arrive()
     prev = join.take()
     full = _dgrad_full(conv, in_hw)
     if prev is None:
+        if last:
+            return run(None)
         join.partial = _Deferred(run, full)
         return None
     if isinstance(prev, _Deferred):
         if full or not prev.full:
-            return prev.run(run(None))
-        return run(prev.run(None))
-    return run(prev)
+            acc = prev.run(run(None))
+        else:
+            acc = run(prev.run(None))
+    else:
+        acc = run(prev)
+    if last:
+        return acc
+    join.partial = acc
+    return None
 
 
 class _ConvBNAct(torch.autograd.Function):
@@ -487,9 +511,10 @@ def linear_act(x, lin, relu: bool = False):
 # ================================================================================= pools
 class _MaxPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, cfg):
+    def forward(ctx, x, cfg, join=None):
         y, idx = K(x).maxpool_fwd(x, *cfg)
         ctx.cfg = cfg
+        ctx.join = join
         ctx.hw = (x.shape[1], x.shape[2])
         ctx.save_for_backward(idx)
         return y
@@ -498,33 +523,38 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         dx = K(dy).maxpool_bwd(dy.contiguous(), idx, ctx.hw[0], ctx.hw[1], *ctx.cfg)
-        return dx, None
+        return _join_grad(ctx.join, dx), None, None
 
 
-def max_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False):
+def max_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False,
+               join: Optional[GradJoin] = None):
+    """``join``: the input's other consumers share it (see GradJoin)."""
     cfg = (kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], bool(ceil_mode))
     if torch.is_grad_enabled() and x.requires_grad:
-        return _MaxPool.apply(x, cfg)
+        return _MaxPool.apply(x, cfg, join)
     return K(x).maxpool_fwd(x, *cfg)[0]
 
 
 class _AvgPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, cfg):
+    def forward(ctx, x, cfg, join=None):
         ctx.cfg = cfg
+        ctx.join = join
         ctx.hw = (x.shape[1], x.shape[2])
         return K(x).avgpool_fwd(x, *cfg)
 
     @staticmethod
     def backward(ctx, dy):
-        return K(dy).avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1], *ctx.cfg), None
+        dx = K(dy).avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1], *ctx.cfg)
+        return _join_grad(ctx.join, dx), None, None
 
 
-def avg_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False, count_include_pad=True):
+def avg_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False, count_include_pad=True,
+               join: Optional[GradJoin] = None):
     cfg = (kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], bool(ceil_mode),
            bool(count_include_pad))
     if torch.is_grad_enabled() and x.requires_grad:
-        return _AvgPool.apply(x, cfg)
+        return _AvgPool.apply(x, cfg, join)
     return K(x).avgpool_fwd(x, *cfg)
 
 

@@ -434,5 +434,17 @@ def split_channels(dy, sizes):
     return [t.contiguous() for t in torch.split(dy, list(sizes), dim=-1)]
 
 
+def chan_accum(g, off, src, assign):
+    cs = src.shape[-1]
+    if assign:
+        g[..., off:off + cs] = src.float()
+    else:
+        g[..., off:off + cs] += src.float()
+
+
+def chan_extract(g, off, cs):
+    return g[..., off:off + cs].clone()
+
+
 def relu_fwd(x):
     return torch.relu(x)

@@ -155,6 +155,10 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             continue
         hooks.append(m.register_forward_pre_hook(pre(name)))
         hooks.append(m.register_forward_hook(post(name)))
+    # a GradJoin spanning two units would hand one unit the other's input gradient
+    cross = getattr(model_gpu, "cross_join", None)
+    if cross is not None:
+        model_gpu.cross_join = False
     try:
         arena = model_gpu._mpa_arena
         arena.zero_grad()
@@ -167,6 +171,8 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             h.remove()
         for m in patched:
             del m.run_group
+        if cross is not None:
+            model_gpu.cross_join = cross
     g_gpu = arena.grad.detach().cpu()
     out = []
     plain = {name: m for name, m in units}
