@@ -662,13 +662,34 @@ std::vector<Tensor> ce_fwd(Tensor logits, Tensor labels) {
 
 // returns dlogits with the same row stride as logits (a view of a zero-padded buffer when
 // the logits are padded)
-Tensor ce_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor grad_out) {
+// out[0] = (or +=, accumulate) weight * mean CE and acc[0] += the same (acc optional);
+// returns the per-row log-sum-exp for the backward
+Tensor ce_fwd_weighted(Tensor logits, Tensor labels, Tensor out, Tensor acc, double weight,
+                       bool accumulate) {
+  const int ld = logits_ld(logits);
+  CHECK_CUDA(labels);
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64, "labels must be int64");
+  CHECK_CUDA(out);
+  CHECK_F32(out);
+  TORCH_CHECK(out.numel() >= 1, "ce_fwd_weighted: out must hold one float");
+  const int B = logits.size(0), NC = logits.size(1);
+  TORCH_CHECK(labels.numel() == B, "ce_fwd_weighted: one label per row");
+  const c10::OptionalDeviceGuard g(device_of(logits));
+  Tensor rows = torch::empty({B}, logits.options().dtype(torch::kFloat32));
+  Tensor lse = torch::empty({B}, logits.options().dtype(torch::kFloat32));
+  mpa::ce_fwd_weighted(bp(logits), labels.contiguous().data_ptr<int64_t>(), B, NC, ld,
+                       out.data_ptr<float>(), fopt_mut(acc), (float)weight, accumulate,
+                       rows.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
+  return lse;
+}
+
+Tensor ce_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor grad_out, double weight) {
   const int ld = logits_ld(logits);
   const int B = logits.size(0), NC = logits.size(1);
   const c10::OptionalDeviceGuard g(device_of(logits));
   Tensor d = torch::empty({B, ld}, logits.options());
   mpa::ce_bwd(bp(logits), labels.contiguous().data_ptr<int64_t>(), fopt(lse), fopt(grad_out), B,
-              NC, ld, bpm(d), cur_stream());
+              NC, ld, bpm(d), cur_stream(), (float)weight);
   return ld == NC ? d : d.narrow(1, 0, NC);
 }
 
@@ -701,7 +722,7 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor shadow, Tensor step, double
                 momentum, dampening, wd, nesterov ? 1 : 0, gs, cur_stream());
 }
 
-void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles) {
+void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles, Tensor step_inc) {
   CHECK_CUDA(w);
   CHECK_CUDA(wt);
   CHECK_CUDA(seg);
@@ -709,7 +730,24 @@ void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles) {
               "transpose_krsc: seg [n][6] int64");
   const c10::OptionalDeviceGuard g(device_of(w));
   mpa::transpose_krsc(bp(w), bpm(wt), seg.contiguous().data_ptr<int64_t>(), (int)seg.size(0),
-                      (int)total_tiles, cur_stream());
+                      (int)total_tiles, cur_stream(), fopt_mut(step_inc));
+}
+
+void zero_f32(Tensor t) {
+  CHECK_CUDA(t);
+  CHECK_CONTIG(t);
+  CHECK_F32(t);
+  TORCH_CHECK(t.numel() % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "zero_f32: numel % 4 == 0 and 16-B alignment required");
+  const c10::OptionalDeviceGuard g(device_of(t));
+  mpa::zero_f32(t.data_ptr<float>(), t.numel(), cur_stream());
+}
+
+void step_inc(Tensor step) {
+  CHECK_CUDA(step);
+  CHECK_F32(step);
+  const c10::OptionalDeviceGuard g(device_of(step));
+  mpa::step_inc(step.data_ptr<float>(), cur_stream());
 }
 
 void cast_f32_bf16(Tensor x, Tensor y) {
@@ -984,12 +1022,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"),
         py::arg("overwrite") = false);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ce_bwd", &ce_bwd);
+  m.def("ce_bwd", &ce_bwd, py::arg("logits"), py::arg("labels"), py::arg("lse"),
+        py::arg("grad_out"), py::arg("weight") = 1.0);
+  m.def("ce_fwd_weighted", &ce_fwd_weighted);
   m.def("argmax_correct", &argmax_correct);
   m.def("adam_step", &adam_step);
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
-  m.def("transpose_krsc", &transpose_krsc);
+  m.def("transpose_krsc", &transpose_krsc, py::arg("w"), py::arg("wt"), py::arg("seg"),
+        py::arg("total_tiles"), py::arg("step_inc") = torch::Tensor());
+  m.def("zero_f32", &zero_f32, "t.zero_() on the native path");
+  m.def("step_inc", &step_inc);
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
   m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");
   m.def("preprocess_pil", &preprocess_pil, "PIL-exact bicubic resize + ToTensor + Normalize");

@@ -266,7 +266,14 @@ void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, i
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s);
 void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,
-            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s);
+            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s,
+            float weight = 1.f);
+void ce_fwd_weighted(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
+                     float* out, float* acc, float weight, bool accumulate, float* rows,
+                     float* lse, hipStream_t s);
+// fp32 t[0:n) = 0 (n % 4 == 0, 16-B aligned); step[0] += 1
+void zero_f32(float* t, int64_t n, hipStream_t s);
+void step_inc(float* step, hipStream_t s);
 void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
                     int64_t* count, hipStream_t s);
 
@@ -279,8 +286,9 @@ void sgd_step(float* p, const float* g, float* buf, bf16_raw* shadow, const floa
               float grad_scale, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s);
 // wt[c][t][k] = w[k][t][c] per segment (src_off, dst_off, K, RS, C, first_tile) of seg
+// step_inc (optional): the optimizer's step counter, incremented by the same launch
 void transpose_krsc(const bf16_raw* w, bf16_raw* wt, const int64_t* seg, int nseg,
-                    int total_tiles, hipStream_t s);
+                    int total_tiles, hipStream_t s, float* step_inc = nullptr);
 
 // preprocess.hip
 struct Norm3 {

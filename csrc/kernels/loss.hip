@@ -147,8 +147,9 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const bf16_t* __restrict__ 
                                                       const int64_t* __restrict__ labels,
                                                       const float* __restrict__ lse,
                                                       const float* __restrict__ grad_out, int B,
-                                                      int NC, int ld, bf16_t* __restrict__ dlogits) {
-  const float scale = grad_out[0] / (float)B;
+                                                      int NC, int ld, bf16_t* __restrict__ dlogits,
+                                                      float weight) {
+  const float scale = grad_out[0] * weight / (float)B;
   const int nv = ld / V;  // whole padded row: columns >= NC get zero gradient
   const int64_t total = (int64_t)B * nv;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
@@ -209,7 +210,8 @@ __global__ __launch_bounds__(256) void argmax_kernel(const bf16_t* __restrict__ 
 // fixed tree): bitwise reproducible, unlike one float atomic per row (whose order varies
 // between launches), and one launch like the memset it replaces.
 __global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restrict__ row_loss, int B,
-                                                          float* __restrict__ loss, int accumulate) {
+                                                          float* __restrict__ loss, int accumulate,
+                                                          float weight, float* __restrict__ acc) {
   __shared__ float red[256];
   float a = 0.f;
   for (int i = threadIdx.x; i < B; i += 256) a += row_loss[i];
@@ -220,8 +222,11 @@ __global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restric
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (accumulate) atomicAdd(loss, red[0]);
-    else *loss = red[0];
+    const float v = weight * red[0];
+    if (accumulate == 2) atomicAdd(loss, v);  // (diagnostics: MPA_DIAG_CE_MEMSET)
+    else if (accumulate) *loss += v;
+    else *loss = v;
+    if (acc) *acc += v;  // the trainer's running loss sum (one host sync per epoch)
   }
 }
 
@@ -240,7 +245,17 @@ void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld
   if (g_diag_memset) (void)hipMemsetAsync(loss, 0, sizeof(float), s);
   ce_fwd_rows(logits, labels, B, NC, ld, rows, lse, s);
   hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, loss,
-                     (int)g_diag_memset);
+                     g_diag_memset ? 2 : 0, 1.f, (float*)nullptr);
+}
+
+// out[0] = (or +=) weight * mean CE; acc[0] += the same (when acc is set).  rows: B floats of
+// scratch.  Several heads (Inception's main + 0.4 * aux) sum into one loss this way.
+void ce_fwd_weighted(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
+                     float* out, float* acc, float weight, bool accumulate, float* rows,
+                     float* lse, hipStream_t s) {
+  ce_fwd_rows(logits, labels, B, NC, ld, rows, lse, s);
+  hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, out,
+                     accumulate ? 1 : 0, weight, acc);
 }
 
 void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
@@ -263,19 +278,20 @@ void ce_fwd_rows(const bf16_raw* logits, const int64_t* labels, int B, int NC, i
 }
 
 void ce_bwd(const bf16_raw* logits, const int64_t* labels, const float* lse,
-            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s) {
+            const float* grad_out, int B, int NC, int ld, bf16_raw* dlogits, hipStream_t s,
+            float weight) {
   const int V = (ld % 8 == 0) ? 8 : (ld % 4 == 0 ? 4 : 1);
   const int64_t total = (int64_t)B * (ld / V);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
   if (V == 8)
     hipLaunchKernelGGL(ce_bwd_kernel<8>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, ld, dlogits);
+                       grad_out, B, NC, ld, dlogits, weight);
   else if (V == 4)
     hipLaunchKernelGGL(ce_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, ld, dlogits);
+                       grad_out, B, NC, ld, dlogits, weight);
   else
     hipLaunchKernelGGL(ce_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, logits, labels, lse,
-                       grad_out, B, NC, ld, dlogits);
+                       grad_out, B, NC, ld, dlogits, weight);
 }
 
 void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,

@@ -111,6 +111,8 @@ void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(cast_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, x, y, n4);
 }
 
+static void step_inc_launch(float* step, hipStream_t s);
+
 // ------------------------------------------------------------ transposed weight shadow
 // wt[c][t][k] = w[k][t][c] for every registered conv / linear weight, from the bf16 shadow
 // the optimizer just wrote: dgrad then reads its B operand K-contiguous, exactly like the
@@ -119,7 +121,11 @@ void cast_f32_bf16(const float* x, bf16_raw* y, int64_t n, hipStream_t s) {
 __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __restrict__ w,
                                                               bf16_t* __restrict__ wt,
                                                               const int64_t* __restrict__ seg,
-                                                              int nseg, int total_tiles) {
+                                                              int nseg, int total_tiles,
+                                                              float* __restrict__ step_inc) {
+  // the optimizer kernel that read the step counter has completed (stream order): count
+  // the step here instead of in a launch of its own
+  if (step_inc && blockIdx.x == 0 && threadIdx.x == 0) *step_inc += 1.f;
   // 64 (k) x 64 (c) tile, rows of eight 16-B chunks; chunk q of row r is stored at
   // position q ^ ((r >> 3) & 7), so the store phase's column gathers (8 lanes per k-row
   // group, one k-row from each of 8 row groups) hit 8 distinct chunk positions: no bank
@@ -172,10 +178,33 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __res
 }
 
 void transpose_krsc(const bf16_raw* w, bf16_raw* wt, const int64_t* seg, int nseg,
-                    int total_tiles, hipStream_t s) {
-  if (nseg <= 0 || total_tiles <= 0) return;
+                    int total_tiles, hipStream_t s, float* step_inc) {
+  if (nseg <= 0 || total_tiles <= 0) {
+    if (step_inc) step_inc_launch(step_inc, s);
+    return;
+  }
   hipLaunchKernelGGL(transpose_krsc_kernel, dim3(total_tiles), dim3(256), 0, s, w, wt, seg, nseg,
-                     total_tiles);
+                     total_tiles, step_inc);
 }
+
+// ------------------------------------------------------------------------ small helpers
+__global__ __launch_bounds__(256) void zero_f32_kernel(float4* __restrict__ t, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x)
+    t[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void step_inc_kernel(float* step) { *step += 1.f; }
+
+void zero_f32(float* t, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  if (n4 > 0)
+    hipLaunchKernelGGL(zero_f32_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, (float4*)t, n4);
+}
+
+static void step_inc_launch(float* step, hipStream_t s) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+}
+void step_inc(float* step, hipStream_t s) { step_inc_launch(step, s); }
 
 }  // namespace mpa

@@ -42,16 +42,15 @@ def build_model(name: str, num_classes: int, feature_extract: bool, device: torc
     return model, input_size
 
 
-def loss_fn(out, labels):
+def loss_fn(out, labels, acc=None):
     """CE; Inception's train-mode (logits, aux) uses loss + 0.4 * aux_loss (the documented
-    fix of the reference's broken Inception path)."""
+    fix of the reference's broken Inception path), one fused native op.
+    ``acc``: device scalar the loss is also added to (the trainer's running sum)."""
     if isinstance(out, (tuple, InceptionOutputs)):
         logits, aux = out[0], out[1]
-        loss = Fn.cross_entropy(logits, labels)
-        if aux is not None:
-            loss = loss + 0.4 * Fn.cross_entropy(aux, labels)
-        return loss
-    return Fn.cross_entropy(out, labels)
+        heads = [(aux, 0.4)] if aux is not None else None
+        return Fn.cross_entropy(logits, labels, acc=acc, heads=heads)
+    return Fn.cross_entropy(out, labels, acc=acc)
 
 
 class _NoMarkers:
@@ -154,7 +153,11 @@ class TrainStep:
         self.arena: ParamArena = model._mpa_arena
         self.bucketer: GradBucketer = model._mpa_bucketer
         self.opt.grad_scale = 1.0 / world.world_size
-        self.loss_sum: Optional[torch.Tensor] = None
+        dev = self.arena.device
+        # running loss sum, added to by the loss kernel itself (graph-safe: fixed address,
+        # reset in place) - one host sync per epoch; the backward seed is a constant
+        self.loss_sum = torch.zeros(4, dtype=torch.float32, device=dev)
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.steps = 0
         self._graph = None
         self._static_x = None
@@ -184,13 +187,13 @@ class TrainStep:
             m.range_push("fwd")
         self.arena.zero_grad()
         out = self.model(x)
-        loss = loss_fn(out, y)
+        loss = loss_fn(out, y, acc=self.loss_sum)
         if t is not None:
             t.mark(1)
         if m is not None:
             m.range_pop()
             m.range_push("bwd")
-        loss.backward()
+        loss.backward(self._one)
         if t is not None:
             t.mark(2)
         if m is not None:
@@ -223,15 +226,12 @@ class TrainStep:
         return loss
 
     def _accumulate(self, loss):
-        if self.loss_sum is None:
-            self.loss_sum = torch.zeros((), dtype=torch.float32, device=loss.device)
-        self.loss_sum += loss.float()
-        self.steps += 1
+        self.steps += 1  # (the loss kernel already added the loss to self.loss_sum)
 
     def mean_loss(self, reset: bool = True) -> float:
-        v = float(self.loss_sum.item()) / max(self.steps, 1) if self.loss_sum is not None else 0.0
+        v = float(self.loss_sum[0].item()) / max(self.steps, 1) if self.steps else 0.0
         if reset:
-            self.loss_sum = None
+            Fn.K(self.loss_sum).zero_f32(self.loss_sum)
             self.steps = 0
         return v
 

@@ -633,24 +633,47 @@ def dropout(x, p: float, training: bool):
 
 # ========================================================================= cross-entropy
 class _CrossEntropy(torch.autograd.Function):
+    """sum_h weight_h * CE(logits_h, labels) as ONE native op: each head's fused
+    log-softmax + NLL kernel adds its weighted mean into the loss scalar (and into the
+    trainer's running loss sum ``acc``), the backward scales each head's softmax gradient
+    by its weight - no elementwise ATen ops for Inception's ``loss + 0.4 * aux_loss``."""
+
     @staticmethod
-    def forward(ctx, logits, labels):
-        loss, lse = K(logits).ce_fwd(logits, labels)
-        ctx.save_for_backward(logits, labels, lse)
-        return loss.reshape(())
+    def forward(ctx, labels, weights, acc, *logits):
+        k = K(logits[0])
+        out = torch.empty(1, device=logits[0].device, dtype=torch.float32)
+        lses = [k.ce_fwd_weighted(lg, labels, out, _or_empty(acc, lg), float(w), i > 0)
+                for i, (lg, w) in enumerate(zip(logits, weights))]
+        ctx.weights = weights
+        ctx.save_for_backward(labels, *logits, *lses)
+        return out.reshape(())
 
     @staticmethod
     def backward(ctx, go):
-        logits, labels, lse = ctx.saved_tensors
-        g = K(logits).ce_bwd(logits, labels, lse, go.reshape(1).float().contiguous())
-        return g, None
+        saved = ctx.saved_tensors
+        labels, n = saved[0], len(ctx.weights)
+        logits, lses = saved[1:1 + n], saved[1 + n:]
+        go = go.reshape(1).float().contiguous()
+        gs = [K(lg).ce_bwd(lg, labels, lse, go, float(w))
+              for lg, lse, w in zip(logits, lses, ctx.weights)]
+        return (None, None, None) + tuple(gs)
 
 
-def cross_entropy(logits, labels):
-    """Mean softmax cross-entropy (``nn.CrossEntropyLoss()`` at main.py:134,150)."""
-    if torch.is_grad_enabled() and logits.requires_grad:
-        return _CrossEntropy.apply(logits, labels)
-    return K(logits).ce_fwd(logits, labels)[0].reshape(())
+def cross_entropy(logits, labels, weight: float = 1.0, acc: Optional[torch.Tensor] = None,
+                  heads=None):
+    """Mean softmax cross-entropy (``nn.CrossEntropyLoss()`` at main.py:134,150).
+
+    ``heads``: extra (logits, weight) terms summed into the same loss (Inception aux);
+    ``acc``: a float32 device scalar the loss is also added to (no host sync)."""
+    lg = [logits] + [h[0] for h in (heads or [])]
+    ws = (float(weight),) + tuple(float(h[1]) for h in (heads or []))
+    if torch.is_grad_enabled() and any(t.requires_grad for t in lg):
+        return _CrossEntropy.apply(labels, ws, acc, *lg)
+    k = K(logits)
+    out = torch.empty(1, device=logits.device, dtype=torch.float32)
+    for i, (t, w) in enumerate(zip(lg, ws)):
+        k.ce_fwd_weighted(t, labels, out, _or_empty(acc, t), w, i > 0)
+    return out.reshape(())
 
 
 def count_correct(logits, labels, count: torch.Tensor) -> None:

@@ -330,11 +330,31 @@ def ce_fwd(logits, labels):
     return loss, lse
 
 
-def ce_bwd(logits, labels, lse, grad_out):
+def ce_bwd(logits, labels, lse, grad_out, weight=1.0):
     B = logits.shape[0]
     p = torch.exp(_f(logits) - lse[:, None])
     p[torch.arange(B, device=logits.device), labels.long()] -= 1.0
-    return (p * (_f(grad_out).reshape(()) / B)).to(logits.dtype)
+    return (p * (_f(grad_out).reshape(()) * weight / B)).to(logits.dtype)
+
+
+def ce_fwd_weighted(logits, labels, out, acc, weight, accumulate):
+    loss, lse = ce_fwd(logits, labels)
+    v = loss.reshape(1) * weight
+    if accumulate:
+        out[:1] += v
+    else:
+        out[:1] = v
+    if acc is not None and acc.numel() > 0:
+        acc[:1] += v
+    return lse
+
+
+def zero_f32(t):
+    t.zero_()
+
+
+def step_inc(step):
+    step.add_(1.0)
 
 
 def argmax_correct(logits, labels, count):

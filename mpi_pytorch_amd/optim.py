@@ -123,8 +123,7 @@ class FusedAdam(_FlatOptimizer):
                                  self.exp_avg, self.exp_avg_sq, self._shadow(), self.step_t,
                                  float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                                  float(g["weight_decay"]), float(self.grad_scale))
-        self.step_t.add_(1.0)
-        self.arena.refresh_transposed()
+        self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):
         return {"step": torch.tensor(step),
@@ -163,8 +162,7 @@ class FusedSGD(_FlatOptimizer):
                                 float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
                                 float(g["weight_decay"]), bool(g["nesterov"]),
                                 float(self.grad_scale))
-        self.step_t.add_(1.0)
-        self.arena.refresh_transposed()
+        self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):
         return {"momentum_buffer":

@@ -115,11 +115,19 @@ class ParamArena:
         self._tseg = torch.tensor([r for _, r in rows], dtype=torch.int64, device=self.device)
         self._ttiles = tiles
 
-    def refresh_transposed(self) -> None:
-        """Re-derive the transposed shadow from the bf16 shadow (after each update)."""
+    def refresh_transposed(self, step_inc: Optional[torch.Tensor] = None) -> None:
+        """Re-derive the transposed shadow from the bf16 shadow (after each update);
+        ``step_inc``: the optimizer's step counter, incremented by the same launch."""
         if self._tseg is not None:
             from ..ops import _ext
-            _ext.ext().transpose_krsc(self.shadow, self.shadow_t, self._tseg, self._ttiles)
+            _ext.ext().transpose_krsc(self.shadow, self.shadow_t, self._tseg, self._ttiles,
+                                      step_inc if step_inc is not None else torch.Tensor())
+        elif step_inc is not None:
+            if step_inc.is_cuda:
+                from ..ops import _ext
+                _ext.ext().step_inc(step_inc)
+            else:
+                step_inc.add_(1.0)
 
     # ------------------------------------------------------------------------------
     def slice_of(self, p: nn.Parameter):
@@ -134,7 +142,11 @@ class ParamArena:
             self.refresh_transposed()
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        if self.grad.is_cuda:
+            from ..ops import _ext
+            _ext.ext().zero_f32(self.grad)
+        else:
+            self.grad.zero_()
         self._fresh = {id(p) for p in self.trainable}
 
     def take_fresh(self, p: nn.Parameter) -> bool:
