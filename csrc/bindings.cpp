@@ -722,7 +722,8 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor shadow, Tensor step, double
                 momentum, dampening, wd, nesterov ? 1 : 0, gs, cur_stream());
 }
 
-void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles, Tensor step_inc) {
+void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles,
+                    c10::optional<Tensor> step_inc) {
   CHECK_CUDA(w);
   CHECK_CUDA(wt);
   CHECK_CUDA(seg);
@@ -730,7 +731,8 @@ void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles, Tensor
               "transpose_krsc: seg [n][6] int64");
   const c10::OptionalDeviceGuard g(device_of(w));
   mpa::transpose_krsc(bp(w), bpm(wt), seg.contiguous().data_ptr<int64_t>(), (int)seg.size(0),
-                      (int)total_tiles, cur_stream(), fopt_mut(step_inc));
+                      (int)total_tiles, cur_stream(),
+                      step_inc ? fopt_mut(*step_inc) : nullptr);
 }
 
 void zero_f32(Tensor t) {
@@ -1030,7 +1032,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("transpose_krsc", &transpose_krsc, py::arg("w"), py::arg("wt"), py::arg("seg"),
-        py::arg("total_tiles"), py::arg("step_inc") = torch::Tensor());
+        py::arg("total_tiles"), py::arg("step_inc") = py::none());
   m.def("zero_f32", &zero_f32, "t.zero_() on the native path");
   m.def("step_inc", &step_inc);
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");

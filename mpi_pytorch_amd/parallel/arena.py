@@ -121,7 +121,7 @@ class ParamArena:
         if self._tseg is not None:
             from ..ops import _ext
             _ext.ext().transpose_krsc(self.shadow, self.shadow_t, self._tseg, self._ttiles,
-                                      step_inc if step_inc is not None else torch.Tensor())
+                                      step_inc)
         elif step_inc is not None:
             if step_inc.is_cuda:
                 from ..ops import _ext
