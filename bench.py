@@ -256,8 +256,12 @@ def run(args) -> None:
                 small["graph_img_per_s"] = round(_timed(step, data, args, world, sync), 1)
         step.mean_loss()
     if world.rank == 0:
+        metric = "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X"
+        if args.model != "resnet18" or args.image_size != 224:  # a zoo run, not the headline
+            metric = "images/sec (whole node) {} {}x{} training on {} MI355X".format(
+                args.model, args.image_size, args.image_size, world.world_size)
         rec = {
-            "metric": "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world.world_size,

@@ -22,7 +22,7 @@ Design for MI355X / RCCL over xGMI:
   optimizer kernel's ``grad_scale`` (no extra pass over the gradients).
 * Optional bf16 wire format halves xGMI bytes (cast kernels around the collective).
 * ``world_size == 1`` is a no-op, like ``mpi_tools.py:32-33``.
-* Comm-aware persistent grids (``comm_ctas``, ``MPA_COMM_CTAS``, default 8; 0 = off): the
+* Comm-aware persistent grids (``comm_ctas``, ``MPA_COMM_CTAS``, opt-in, e.g. 8; 0 = off): the
   buckets that overlap backward run on a second RCCL communicator capped at ``comm_ctas``
   CTAs (``ncclConfig_t.maxCTAs``), and while one is in flight the persistent conv kernels size
   their grids to the CUs the collective leaves free (``_ext.set_comm_reserve``).  Without
@@ -55,7 +55,10 @@ def _set_reserve(cus: int) -> None:
 # 8 or 32 CTAs held for 2 / 6 ms of backward cost +0.70 / +1.84 ms per step with static
 # persistent grids, +0.38 / +0.61 ms with the reservation - the straggle depends on how
 # long ANY CU is held, not on how many, so few CTAs plus a reservation is the cheap shape.
-DEFAULT_COMM_CTAS = 8
+# Opt-in (MPA_COMM_CTAS=8) until a real multi-GPU run has measured it: the second
+# communicator and the reservation have only met an emulated collective, and the default
+# single-communicator path is RCCL's standard one (round-3 advisor finding).
+DEFAULT_COMM_CTAS = 0
 
 
 def capped_group(max_ctas: int, device: torch.device):
