@@ -213,14 +213,14 @@ class TrainStep:
         return loss.detach()
 
     def __call__(self, x, y) -> torch.Tensor:
-        if self._graph is not None:
+        if self._graph is not None and x.shape == self._static_x.shape:
             self._static_x.copy_(x)
             self._static_y.copy_(y)
             self._graph.replay()
             if self._sync_replay:
                 torch.cuda.current_stream().synchronize()
             loss = self._static_loss
-        else:
+        else:  # eager (also a short last batch of a graph-captured loop)
             loss = self._eager(x, y)
         self._accumulate(loss)
         return loss

@@ -204,6 +204,8 @@ def run_training(cfg: Config) -> dict:
         step.enable_timers()
         step.bucketer.enable_comm_stats()
     history = []
+    use_graph = (cfg.graph == "on" and size == 1 and dev.type == "cuda"
+                 and not cfg.step_timers)
     # fail fast on a stalled rank (e.g. a peer died inside a collective): SURVEY.md §5.3
     dog = Watchdog(cfg.watchdog_s, rank=rank).start()
     gstep = 0
@@ -214,6 +216,9 @@ def run_training(cfg: Config) -> dict:
         t0 = time.perf_counter()
         nimg = 0
         for x, y in train_loader.epoch(epoch, steps_per_epoch):
+            if use_graph and step._graph is None and x.shape[0] == cfg.BATCH_SIZE:
+                # graph = "on", one GPU: capture the whole step once, replay it after
+                step.capture(x, y)
             step(x, y)
             nimg += x.shape[0]
             gstep += 1
