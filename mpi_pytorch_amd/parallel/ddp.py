@@ -143,6 +143,9 @@ class GradBucketer:
         self._wire: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._stats: Optional[list] = None  # (bucket, wire bytes, work, host t0, host t1)
         self.active = world_size > 1
+        # RCCL reports each collective's own device time; other backends are host-timed
+        self._host_timed = self.active and dist.is_initialized() and \
+            dist.get_backend(self.group) != "nccl"
         if self.active:
             arena.add_listener(self._on_grad)
             # (the capped communicator spans the whole world: only for the default group)
@@ -221,8 +224,8 @@ class GradBucketer:
             w = self._works[bi]
             if w is not None:
                 w.wait()
-                if self._stats is not None and not self.arena.grad.is_cuda:
-                    # host backends: wait() returned when the collective did
+                if self._stats is not None and self._host_timed:
+                    # host backends (gloo): wait() returned when the collective did
                     for rec in self._stats[::-1]:
                         if rec[2] is w:
                             rec[4] = time.perf_counter()
