@@ -146,3 +146,43 @@ def test_log_rank_lines_tags_each_rank(tmp_path):
     for h in list(log.handlers):
         log.removeHandler(h)
         h.close()
+
+
+def test_eval_pipeline_two_ranks_sum_reduces_accuracy(tmp_path):
+    """evaluation_pipeline.py under the launcher at world size 2: each rank evaluates its
+    ``array_split`` shard with two predictor lanes and rank 0 logs the SUM-reduced accuracy,
+    which must equal one process's plain batched evaluation of the whole manifest with the
+    same checkpoint (reference: ``/root/reference/evaluation_pipeline.py:190-199``)."""
+    import re
+    import torch
+    from mpi_pytorch_amd.checkpoint import save_checkpoint
+    from mpi_pytorch_amd.config import Config
+    from mpi_pytorch_amd.data.manifest import SyntheticImages, synthetic_manifest
+    from mpi_pytorch_amd.engine.eval_pipeline import load_predictor, plain_eval
+    from mpi_pytorch_amd.models import initialize_model
+    torch.manual_seed(3)
+    model, _ = initialize_model("resnet18", 10, False, False)
+    ckdir = str(tmp_path / "ck") + "/"
+    ck = save_checkpoint({"epoch": 0, "state_dict": model.state_dict()}, 0, "resnet18", ckdir)
+    log = tmp_path / "evaluation.log"
+    cmd = [sys.executable, "-m", "mpi_pytorch_amd.launch", "-n", "2", "--timeout", "500",
+           os.path.join(ROOT, "evaluation_pipeline.py"), "--device", "cpu",
+           "--synthetic_images", "44", "--image_size", "32", "--NUM_CLASSES", "10",
+           "--MODEL_NAME", "resnet18", "--eval_batch", "8", "--eval_lanes", "2",
+           "--CHECKPOINT_DIR", ckdir, "--log_file", str(log)]
+    env = _env()
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    text = log.read_text()
+    acc = float(re.search(r"Accuracy is ([-+0-9.eE]+)", text).group(1))
+    assert "Finished node 3, acc" in text and "Finished node 4, acc" in text
+    assert "2 lanes x 2 ranks" in text
+    cfg = Config(device="cpu", synthetic_images=44, image_size=32, NUM_CLASSES=10,
+                 MODEL_NAME="resnet18", CHECKPOINT_DIR=ckdir)
+    df = synthetic_manifest(44, 10, cfg.seed)
+    oracle = load_predictor(cfg, torch.device("cpu"), ck)
+    correct = plain_eval(oracle, list(df["file_name"].values), list(df["category_id"].values), 8,
+                         SyntheticImages((64, 64)), torch.device("cpu"), (32, 32))
+    assert acc == pytest.approx(correct / 44, abs=1e-9)
