@@ -339,22 +339,77 @@ static uint8_t* ymask_ptr(const c10::optional<Tensor>& m, const Tensor& like) {
 
 // mask (optional, uint8 [numel / 8]): receives the ReLU bit mask of y (bit j of byte i =
 // element 8 i + j > 0) for bn_bwd(ymask=...), which then never reads y
+// channels > 0: x is a wider buffer [..., ldx] and the BN runs on its first `channels`
+// channels (a DenseNet block's feature prefix); stats may then be a wider [2, lds] buffer
+// whose first `channels` columns hold [mean | var]
+// Row stride of a channel-window view [..., C] of a wider NHWC buffer (x[..., a:b]): unit
+// channel stride and uniformly strided rows; a contiguous tensor has row stride C
+static int row_stride(const Tensor& t) {
+  TORCH_CHECK(t.dim() >= 1 && t.stride(-1) == 1, "bn: channels must be contiguous");
+  if (t.dim() == 1) return (int)t.size(0);
+  const int64_t ld = t.stride(-2);
+  int64_t expect = ld * t.size(-2);
+  for (int64_t d = t.dim() - 3; d >= 0; --d) {
+    TORCH_CHECK(t.size(d) == 1 || t.stride(d) == expect, "bn: rows must be uniformly strided");
+    expect *= t.size(d);
+  }
+  TORCH_CHECK(ld >= t.size(-1) && ld % 8 == 0, "bn: row stride must be a multiple of 8");
+  return (int)ld;
+}
+
+// x: the BN input - contiguous, or a channel-window view (row stride ldx); channels > 0:
+// x is contiguous [..., ldx] and the BN runs on its first `channels` channels
+static void bn_prefix(const Tensor& x, int64_t channels, int* C, int* ldx, int* M) {
+  CHECK_CUDA(x);
+  CHECK_BF16(x);
+  if (channels > 0) {
+    CHECK_CONTIG(x);
+    *ldx = x.size(-1);
+    *C = (int)channels;
+  } else {
+    *ldx = row_stride(x);
+    *C = x.size(-1);
+  }
+  TORCH_CHECK(*C <= *ldx && *C % 8 == 0 && *ldx % 8 == 0,
+              "bn: channels must be a multiple of 8 within the row");
+  *M = x.numel() / x.size(-1);
+}
+
+static std::vector<int64_t> with_last(const Tensor& x, int64_t c) {
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = c;
+  return shape;
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
                                  Tensor rvar, double momentum, double eps, Tensor res, bool relu,
-                                 c10::optional<Tensor> counter, c10::optional<Tensor> mask) {
-  CHECK_ACT(x);
-  const int C = x.size(-1);
-  const int M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
+                                 c10::optional<Tensor> counter, c10::optional<Tensor> mask,
+                                 int64_t channels) {
+  int C, ldx, M;
+  bn_prefix(x, channels, &C, &ldx, &M);
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor st = stats;
-  if (!has(st)) {
+  int lds = C;
+  if (has(st)) {
+    CHECK_F32(st);
+    // [2C] contiguous, or a [2, >= C] (view) whose rows hold mean | var: rows stride(0) apart
+    if (st.dim() == 2) {
+      TORCH_CHECK(st.size(0) == 2 && st.size(1) >= C && st.stride(1) == 1,
+                  "bn_fwd_train: stats must be [2, >= C] (mean | var)");
+      lds = (int)st.stride(0);
+    } else {
+      CHECK_CONTIG(st);
+      TORCH_CHECK(st.numel() == 2 * C, "bn_fwd_train: stats must be [2, >= C] (mean | var)");
+    }
+  } else {
+    TORCH_CHECK(ldx == C, "bn_fwd_train: a channel prefix needs precomputed stats");
     st = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
     Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
     mpa::bn_stats(bp(x), M, C, fopt(rmean), st.data_ptr<float>(), ws.data_ptr<float>(),
                   cur_stream());
   }
-  Tensor y = torch::empty_like(x);
+  Tensor y = torch::empty(with_last(x, C), x.options());
+  if (has(res)) TORCH_CHECK(res.numel() == y.numel(), "bn_fwd_train: residual shape");
   Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
   Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
   mpa::bn_fwd_train(bp(x), fopt(st), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
@@ -362,41 +417,84 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
                     mean.data_ptr<float>(), rstd.data_ptr<float>(),
                     (counter && counter->defined() && counter->numel() == 1)
                         ? counter->data_ptr<int64_t>() : nullptr,
-                    cur_stream(), ymask_ptr(mask, x));
+                    cur_stream(), ymask_ptr(mask, y), ldx, lds);
   return {y, mean, rstd};
 }
 
-Tensor bn_fwd_eval(Tensor x, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar, double eps,
-                   Tensor res, bool relu) {
+// per-channel batch statistics [2, C] = [mean | biased var] of x [..., C] (shift: optional
+// per-channel value subtracted before the sums, e.g. the running mean, for precision)
+Tensor bn_stats(Tensor x, Tensor shift) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
+  TORCH_CHECK(C % 8 == 0 && M > 0, "bn_stats: channels must be a multiple of 8");
+  if (has(shift)) TORCH_CHECK(shift.numel() == C && shift.is_contiguous(), "bn_stats: shift");
   const c10::OptionalDeviceGuard g(device_of(x));
-  Tensor y = torch::empty_like(x);
+  Tensor st = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
+  Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
+  mpa::bn_stats(bp(x), M, C, fopt(shift), st.data_ptr<float>(), ws.data_ptr<float>(),
+                cur_stream());
+  return st;
+}
+
+Tensor bn_fwd_eval(Tensor x, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar, double eps,
+                   Tensor res, bool relu, int64_t channels) {
+  int C, ldx, M;
+  bn_prefix(x, channels, &C, &ldx, &M);
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor y = torch::empty(with_last(x, C), x.options());
+  if (has(res)) TORCH_CHECK(res.numel() == y.numel(), "bn_fwd_eval: residual shape");
   mpa::bn_fwd_eval(bp(x), fopt(gamma), fopt(beta), fopt(rmean), fopt(rvar), (float)eps,
-                   bopt(res), relu ? 1 : 0, M, C, bpm(y), cur_stream());
+                   bopt(res), relu ? 1 : 0, M, C, bpm(y), cur_stream(), ldx);
   return y;
 }
 
+// x may be wider than dy (a channel prefix: ldx = x.size(-1)); gacc (fp32 [..., ldg]): dx is
+// ADDED into its first C channels instead of being returned (a dense block's accumulator)
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd, Tensor gamma,
                            Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g,
-                           c10::optional<Tensor> zmask_beta, c10::optional<Tensor> ymask) {
+                           c10::optional<Tensor> zmask_beta, c10::optional<Tensor> ymask,
+                           c10::optional<Tensor> gacc, c10::optional<Tensor> dx_out) {
   CHECK_ACT(dy);
-  CHECK_ACT(x);
-  const int C = x.size(-1);
-  const int M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
-  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd: dy/x shape mismatch");
+  CHECK_CUDA(x);
+  CHECK_BF16(x);
+  const int C = dy.size(-1);
+  // x: same channels as dy (contiguous or a channel-window view), or a contiguous wider
+  // buffer whose first C channels are the BN input (a DenseNet block prefix)
+  const int ldx = (x.size(-1) > C) ? (x.is_contiguous() ? (int)x.size(-1) : -1) : row_stride(x);
+  TORCH_CHECK(ldx > 0, "bn_bwd: a wider x must be contiguous");
+  const int M = dy.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && ldx % 8 == 0 && ldx >= C, "bn: channels must be a multiple of 8");
+  TORCH_CHECK(x.numel() / x.size(-1) == M && x.dim() == dy.dim(), "bn_bwd: dy/x shape mismatch");
+  const bool acc = gacc && gacc->defined() && gacc->numel() > 0;
+  if (acc) {
+    CHECK_CUDA(*gacc);
+    CHECK_CONTIG(*gacc);
+    CHECK_F32(*gacc);
+    TORCH_CHECK(gacc->numel() / gacc->size(-1) == M && gacc->size(-1) >= C &&
+                    gacc->size(-1) % 8 == 0 && !want_g,
+                "bn_bwd: gradient accumulator must be fp32 [..., >= C] with dy's rows");
+  }
+  // dx_out: write dx into this (contiguous or channel-window) bf16 view of dy's shape
+  const bool into = dx_out && dx_out->defined() && dx_out->numel() > 0;
+  int lddx = C;
+  if (into) {
+    CHECK_CUDA(*dx_out);
+    CHECK_BF16(*dx_out);
+    TORCH_CHECK(dx_out->sizes() == dy.sizes() && !acc, "bn_bwd: dx_out must have dy's shape");
+    lddx = row_stride(*dx_out);
+  }
   const c10::OptionalDeviceGuard g(device_of(x));
-  Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
-  Tensor gout = want_g ? torch::empty_like(x) : Tensor();
+  Tensor dx = (want_dx && !acc) ? (into ? *dx_out : torch::empty_like(dy)) : Tensor();
+  Tensor gout = want_g ? torch::empty_like(dy) : Tensor();
   Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
   const Tensor zb = (zmask_beta && zmask_beta->defined()) ? *zmask_beta : Tensor();
   if (has(zb)) TORCH_CHECK(zb.numel() == C, "bn_bwd: zmask beta size");
   mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
-              fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr, want_g ? bpm(gout) : nullptr,
-              ws.data_ptr<float>(), cur_stream(), fopt(zb), ymask_ptr(ymask, x));
+              fopt_mut(dbeta), M, C, (want_dx && !acc) ? bpm(dx) : nullptr,
+              want_g ? bpm(gout) : nullptr, ws.data_ptr<float>(), cur_stream(), fopt(zb),
+              ymask_ptr(ymask, dy), ldx, acc ? gacc->data_ptr<float>() : nullptr,
+              acc ? (int)gacc->size(-1) : 0, lddx);
   return {dx, gout};
 }
 
@@ -908,6 +1006,31 @@ void chan_accum(Tensor g, int64_t off, Tensor src, bool assign) {
                     cur_stream());
 }
 
+// dst[..., off:off+C] = src (same dtype: bf16 activations or fp32 rows, e.g. BN statistics
+// [2, C] into a block's [2, Ctot]); same leading element count
+void chan_insert(Tensor dst, int64_t off, Tensor src) {
+  CHECK_CUDA(dst);
+  CHECK_CUDA(src);
+  CHECK_CONTIG(dst);
+  CHECK_CONTIG(src);
+  TORCH_CHECK(dst.scalar_type() == src.scalar_type() &&
+                  (src.scalar_type() == torch::kBFloat16 || src.scalar_type() == torch::kFloat32),
+              "chan_insert: bf16 or fp32, same dtype");
+  const int64_t u = src.element_size() / 2;  // 16-bit units per element
+  const int64_t ld = dst.size(-1), cs = src.size(-1);
+  TORCH_CHECK(dst.numel() / ld == src.numel() / cs && off >= 0 && off + cs <= ld,
+              "chan_insert: shapes");
+  TORCH_CHECK((ld * u) % 8 == 0 && (cs * u) % 8 == 0 && (off * u) % 8 == 0,
+              "chan_insert: 16-byte aligned channel runs required");
+  const int64_t rows = src.numel() / cs;
+  TORCH_CHECK(rows * (cs * u / 8) < (int64_t(1) << 31), "chan_insert: too large");
+  const c10::OptionalDeviceGuard gd(device_of(dst));
+  if (rows > 0)
+    mpa::chan_insert((mpa::bf16_raw*)dst.data_ptr(), (int)(ld * u), (int)(off * u),
+                     (const mpa::bf16_raw*)src.data_ptr(), (int)(cs * u), (int)rows,
+                     cur_stream());
+}
+
 // bf16 copy of G[..., off:off+C]
 Tensor chan_extract(Tensor g, int64_t off, int64_t cs) {
   CHECK_CUDA(g);
@@ -995,12 +1118,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
         py::arg("res"), py::arg("relu"), py::arg("counter") = py::none(),
-        py::arg("mask") = py::none());
-  m.def("bn_fwd_eval", &bn_fwd_eval);
+        py::arg("mask") = py::none(), py::arg("channels") = 0);
+  m.def("bn_stats", &bn_stats, "[mean | biased var] of x [..., C]");
+  m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"),
+        py::arg("rmean"), py::arg("rvar"), py::arg("eps"), py::arg("res"), py::arg("relu"),
+        py::arg("channels") = 0);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none(),
-        py::arg("ymask") = py::none());
+        py::arg("ymask") = py::none(), py::arg("gacc") = py::none(),
+        py::arg("dx_out") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("comm_emulator", &comm_emulator, "diagnostics: occupy CUs like a concurrent collective");
   m.def("atomic_latency", &atomic_latency, "diagnostics: dependent atomic round trips");
@@ -1037,6 +1164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("step_inc", &step_inc);
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
   m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");
+  m.def("chan_insert", &chan_insert, "dst[..., off:off+C] = src (bf16 or fp32)");
   m.def("preprocess_pil", &preprocess_pil, "PIL-exact bicubic resize + ToTensor + Normalize");
   m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
         py::arg("std"), py::arg("mode"), py::arg("cpad"),

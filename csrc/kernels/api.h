@@ -193,17 +193,23 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
                   int64_t* counter, hipStream_t s,  // counter (num_batches_tracked) += 1
-                  uint8_t* ymask = nullptr);  // optional ReLU bit mask of y ([M*C/8] bytes)
+                  uint8_t* ymask = nullptr,  // optional ReLU bit mask of y ([M*C/8] bytes)
+                  int ldx = 0,   // x row stride (0: C) - a channel prefix of a wider buffer
+                  int lds = 0);  // stats = [mean | var] rows lds apart (0: C)
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
-                 bf16_raw* y, hipStream_t s);
+                 bf16_raw* y, hipStream_t s, int ldx = 0);
 // zmask_beta (y == null): the ReLU mask of y = relu(bn(x)) is recomputed from x with this
 // beta (no residual in the forward), so y is never read
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s,
             const float* zmask_beta = nullptr,
-            const uint8_t* ymask = nullptr);  // bit mask from bn_fwd_train, used instead of y
+            const uint8_t* ymask = nullptr,  // bit mask from bn_fwd_train, used instead of y
+            int ldx = 0,             // x row stride (0: C)
+            float* gacc = nullptr,   // non-null: dx ADDED in fp32 into gacc [M][ldg] (dx unused)
+            int ldg = 0,
+            int lddx = 0);           // dx row stride (0: C) - a channel window of a wider buffer
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);
@@ -254,6 +260,10 @@ void chan_extract(const float* g, int ldg, int off, bf16_raw* dst, int cs, int p
                   hipStream_t s);
 void concat_channels(const bf16_raw* const* xs, const int* chans, int nseg, int pixels,
                      int ctotal, bf16_raw* y, hipStream_t s);
+// dst [rows][ld] (16-bit units) at unit offset off <- src [rows][cs]; ld, off, cs % 8 == 0
+// (bf16 activations, or fp32 rows as pairs of units)
+void chan_insert(bf16_raw* dst, int ld, int off, const bf16_raw* src, int cs, int rows,
+                 hipStream_t s);
 void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, int ctotal,
                     bf16_raw* const* dxs, hipStream_t s);
 

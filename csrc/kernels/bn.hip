@@ -207,9 +207,10 @@ __device__ __forceinline__ uint32_t posmask8(uint4 p) {
 }
 
 // y = relu?(x * sc + sh (+ res)) over this thread's rows; ym (optional): the ReLU mask of y,
-// one bit per element (byte r * C/8 + c0/8), which the backward reads instead of y
+// one bit per element (byte r * C/8 + c0/8), which the backward reads instead of y.  x rows
+// have stride ldx >= C (a channel prefix of a wider buffer: DenseNet's block features)
 template <int UNR, bool YM = false>
-__device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, int c0,
+__device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, int ldx, int c0,
                                               const float* sc, const float* sh,
                                               const bf16_t* __restrict__ x,
                                               const bf16_t* __restrict__ res, int relu,
@@ -219,7 +220,7 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
       cm, M,
       [&](int r, uint4 (&v)[2]) {
         const size_t off = (size_t)r * C + c0;
-        v[0] = *(const uint4*)(x + off);
+        v[0] = *(const uint4*)(x + (size_t)r * ldx + c0);
         if (res) v[1] = *(const uint4*)(res + off);
       },
       [&](int r, uint4 (&v)[2]) {
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask) {
+    unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask, int ldx, int lds) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
@@ -258,8 +259,8 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
   float sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float mu = stats[c0 + j];       // finalized (mean, biased var)
-    const float var = stats[C + c0 + j];
+    const float mu = stats[c0 + j];       // finalized (mean, biased var); rows lds apart
+    const float var = stats[lds + c0 + j];
     const float rs = rsqrtf(var + eps);
     sc[j] = gamma[c0 + j] * rs;
     sh[j] = __builtin_fmaf(-mu, sc[j], beta[c0 + j]);
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
       rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
     }
   }
-  bn_apply_rows<UNR, YM>(cm, M, C, c0, sc, sh, x, res, relu, y, ymask);
+  bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask);
 }
 
 // -------------------------------------------------------------------- forward (eval)
@@ -279,7 +280,7 @@ template <int UNR>
 __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
-    const bf16_t* __restrict__ res, int relu, int M, int C, bf16_t* __restrict__ y) {
+    const bf16_t* __restrict__ res, int relu, int M, int C, bf16_t* __restrict__ y, int ldx) {
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
     sc[j] = gamma[c0 + j] * rs;
     sh[j] = beta[c0 + j] - rmean[c0 + j] * sc[j];
   }
-  bn_apply_rows<UNR>(cm, M, C, c0, sc, sh, x, res, relu, y);
+  bn_apply_rows<UNR>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y);
 }
 
 // ---------------------------------------------------------------------- backward
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, int M, int C,
-    float* __restrict__ slab, float* __restrict__ sums, const uint8_t* __restrict__ ym) {
+    float* __restrict__ slab, float* __restrict__ sums, const uint8_t* __restrict__ ym, int ldx) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float sg[8], sgx[8];
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         if (u < n) {
           const size_t off = (size_t)(r + u * st) * C + c0;
           dv[u] = *(const uint4*)(dy + off);
-          xr[u] = *(const uint4*)(x + off);
+          xr[u] = *(const uint4*)(x + (size_t)(r + u * st) * ldx + c0);
           if (ym) mb[u] = ym[off / 8];
           else if (y) yr[u] = *(const uint4*)(y + off);
         }
@@ -391,14 +392,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // pass 2: dx = a*g + b + c*x ; optionally write g (residual-branch gradient); block 0
 // folds the sums into dgamma/dbeta.  YM (mask from bn_fwd_train) is a template parameter:
 // a runtime mask pointer slowed every variant of this pass by 10-40 % (its row loads no
-// longer stayed in flight).
-template <int UNR, bool YM>
+// longer stayed in flight).  x rows have stride ldx.  ACC: dx is ADDED in fp32 into
+// gacc [M][ldg] (a dense block's gradient accumulator; its rows are loaded with the others)
+// instead of being written as bf16.
+template <int UNR, bool YM, bool ACC = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ ws,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int M, int C,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ gout, const uint8_t* __restrict__ ym) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ gout, const uint8_t* __restrict__ ym, int ldx,
+    float* __restrict__ gacc, int ldg, int lddx) {
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -417,21 +421,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       if (dbeta) dbeta[c0 + j] += sg;
     }
   }
-  if (!dx && !gout) return;
+  if (!ACC && !dx && !gout) return;
   const bool zmask = !YM && !y && beta;
   float msc[8], msh[8];
   if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
-  const bool need_x = dx || zmask;
-  sweep_rows_pl<UNR, 3>(
+  const bool need_x = ACC || dx || zmask;
+  sweep_rows_pl<UNR, ACC ? 5 : 3>(
       cm, M,
-      [&](int r, uint4 (&v)[3]) {
+      [&](int r, uint4 (&v)[ACC ? 5 : 3]) {
         const size_t off = (size_t)r * C + c0;
         v[0] = *(const uint4*)(dy + off);
         if constexpr (YM) v[2].x = ym[off / 8];
         else if (y) v[2] = *(const uint4*)(y + off);
-        if (need_x) v[1] = *(const uint4*)(x + off);
+        if (need_x) v[1] = *(const uint4*)(x + (size_t)r * ldx + c0);
+        if constexpr (ACC) {
+          const uint4* gp = (const uint4*)(gacc + (size_t)r * ldg + c0);
+          v[3] = gp[0];
+          v[4] = gp[1];
+        }
       },
-      [&](int r, uint4 (&v)[3]) {
+      [&](int r, uint4 (&v)[ACC ? 5 : 3]) {
         const size_t off = (size_t)r * C + c0;
         float g[8];
         unpack8(v[0], g);
@@ -454,12 +463,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         } else if (gout) {
           *(uint4*)(gout + off) = v[0];
         }
-        if (dx) {
+        if (ACC || dx) {
           float xv[8];
           unpack8(v[1], xv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
-          *(uint4*)(dx + off) = pack8(xv);
+          if constexpr (ACC) {
+            const uint32_t gw[8] = {v[3].x, v[3].y, v[3].z, v[3].w, v[4].x, v[4].y, v[4].z, v[4].w};
+            uint4 o[2];
+            uint32_t* ow = (uint32_t*)o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ow[j] = __float_as_uint(__uint_as_float(gw[j]) + xv[j]);
+            uint4* gp = (uint4*)(gacc + (size_t)r * ldg + c0);
+            gp[0] = o[0];
+            gp[1] = o[1];
+          } else {
+            *(uint4*)(dx + (size_t)r * lddx + c0) = pack8(xv);
+          }
         }
       });
 }
@@ -1134,39 +1154,61 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
-                  int64_t* counter, hipStream_t s, uint8_t* ymask) {
+                  int64_t* counter, hipStream_t s, uint8_t* ymask, int ldx, int lds) {
+  if (ldx <= 0) ldx = C;
+  if (lds <= 0) lds = C;
   if (ymask)
     BN_LAUNCH_T(bn_fwd_train_kernel, true, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
-                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask);
+                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
+                ldx, lds);
   else
     BN_LAUNCH_T(bn_fwd_train_kernel, false, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
-                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask);
+                momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
+                ldx, lds);
 }
 
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
-                 bf16_raw* y, hipStream_t s) {
+                 bf16_raw* y, hipStream_t s, int ldx) {
   BN_LAUNCH(bn_fwd_eval_kernel, grid_for(M, C), s, x, gamma, beta, rmean,
-                     rvar, eps, res, relu, M, C, y);
+                     rvar, eps, res, relu, M, C, y, ldx > 0 ? ldx : C);
 }
 
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta,
-            const uint8_t* ymask) {
+            const uint8_t* ymask, int ldx, float* gacc, int ldg, int lddx) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials
+  if (ldx <= 0) ldx = C;
+  if (lddx <= 0) lddx = C;
   const dim3 gr = grid_for(M, C);
   float* slab = ws + 2 * C;
   const float* zb = (y || ymask) ? nullptr : zmask_beta;
   if (ymask) y = nullptr;
-  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws, ymask);
+  BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws, ymask,
+            ldx);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
-  if (ymask)
+  if (gacc) {  // dense-block accumulator: dx added into gacc in fp32 (no ymask, no g)
+    const int u = bn_unr();
+    const dim3 ga = grid_for(M, C);
+    if (u == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, false, true>), ga, dim3(256), 0, s, dy, x, y,
+                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
+                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
+    else if (u == 2)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, false, true>), ga, dim3(256), 0, s, dy, x, y,
+                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
+                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, true>), ga, dim3(256), 0, s, dy, x, y,
+                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
+                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
+  } else if (ymask)
     BN_LAUNCH_T(bn_bwd_apply_kernel, true, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb, ws,
-                dgamma, dbeta, M, C, dx, g, ymask);
+                dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx);
   else
     BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb,
-                ws, dgamma, dbeta, M, C, dx, g, ymask);
+                ws, dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx);
 }
 
 // apply pass only, with the reduction sums [sum g | sum g*xhat] already in `sums` (e.g.
@@ -1175,7 +1217,8 @@ void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, cons
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s) {
   BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
-              (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr);
+              (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr, C,
+              (float*)nullptr, 0, C);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,

@@ -28,13 +28,15 @@ class _DenseLayer(nn.Module):
 
     def forward(self, feats):
         x = feats[0] if len(feats) == 1 else Fn.cat_channels(feats)
-        x = self.norm1(x, relu=True)
-        x = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True)
-        return self.conv2(x)
+        return self.tail(self.norm1(x, relu=True))
+
+    def tail(self, x):
+        """conv1 -> norm2 -> relu -> conv2 of the normalised input."""
+        return self.conv2(Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True))
 
 
-# MPA_DENSE_BLOCK_GRAD=0: plain autograd through the per-layer concats (one split and one
-# elementwise add per earlier feature and layer) instead of the block-level accumulator
+# MPA_DENSE_BLOCK_GRAD=0: per-layer concats under plain autograd (one split and one
+# elementwise add per earlier feature and layer) instead of the block feature buffer
 _BLOCK_GRAD = os.environ.get("MPA_DENSE_BLOCK_GRAD", "1") == "1"
 
 
@@ -46,66 +48,129 @@ class _DenseBlock(nn.ModuleDict):
                             _DenseLayer(num_input_features + i * growth_rate, growth_rate,
                                         bn_size))
 
-    def forward(self, x):
-        if _BLOCK_GRAD and self.training and torch.is_grad_enabled() and x.requires_grad:
-            params = [p for p in self.parameters() if p.requires_grad]
-            return _DenseBlockGrad.apply(x, self, *params)
+    def forward(self, x, fused: bool = True):
+        """Returns (block output, its per-channel [mean | var] or None)."""
+        if fused and _BLOCK_GRAD:
+            if self.training and torch.is_grad_enabled() and x.requires_grad:
+                params = [p for p in self.parameters() if p.requires_grad]
+                out = _DenseBlockGrad.apply(x, self, *params)
+                return out, self.__dict__.pop("_stats", None)
+            if not self.training:
+                return _block_eval(self, x), None
         feats = [x]
         for layer in self.values():
             feats.append(layer(feats))
-        return Fn.cat_channels(feats)
+        return Fn.cat_channels(feats), None
+
+
+def _growth(block) -> int:
+    return next(iter(block.values())).conv2.weight.shape[0]
+
+
+def _block_eval(block, x):
+    """Eval forward on the block feature buffer: each layer's norm1 reads its input as the
+    buffer's channel prefix (bn_fwd_eval(channels=C_i)), its output is inserted at its
+    channel offset - no per-layer concat."""
+    k = Fn.K(x)
+    layers = list(block.values())
+    c0 = x.shape[-1]
+    buf = x.new_empty(x.shape[:-1] + (c0 + _growth(block) * len(layers),))
+    k.chan_insert(buf, 0, x)
+    ci = c0
+    for layer in layers:
+        n1 = layer.norm1
+        y1 = k.bn_fwd_eval(buf, n1.weight, n1.bias, n1.running_mean, n1.running_var, n1.eps,
+                           Fn._empty(x), True, channels=ci)
+        out = layer.tail(y1)
+        k.chan_insert(buf, ci, out)
+        ci += out.shape[-1]
+    return buf
 
 
 class _DenseBlockGrad(torch.autograd.Function):
-    """A dense block whose backward sums every feature's gradient in ONE fp32 buffer.
+    """A dense block on ONE feature buffer, with ONE fp32 gradient accumulator.
 
-    Each feature feeds every later layer (through that layer's input concat) and the
-    block output, so plain autograd splits each layer's input gradient into per-feature
-    pieces and adds them feature by feature: O(L^2) small split / add launches per block
-    (535 ATen adds per DenseNet-121 step).  Here the forward runs each layer on a leaf
-    copy of its concatenated input (its own small autograd graph, kept for backward), and
-    the backward walks the layers in reverse with G = the block gradient [..., C_total] in
-    fp32: layer i's output gradient is read from G's channels of feature i
-    (``chan_extract``), its graph is back-propagated, and its input gradient is added to
-    G's first C_i channels (``chan_accum``, one launch).  Parameter gradients land in the
-    flat arena from the layers' own kernels, as in every other model."""
+    Forward: the block input and every layer's 32-channel output live in a buffer
+    [N, H, W, C_total] at their channel offsets (``chan_insert``), so layer i reads its
+    input as the buffer's first C_i channels - no per-layer concat (the O(L^2) copies of
+    torchvision's ``torch.cat(prev_features, 1)``).  Every feature's batch
+    statistics are taken ONCE when it is produced (``bn_stats`` of the new 32 channels)
+    into a block statistics table S [2, C_total]; each layer's norm1 (a different affine and
+    running-stat update per layer, as in the reference) then normalises its prefix from S
+    (``bn_fwd_train(channels=C_i)``) with no statistics pass.  The table also serves the
+    transition / final norm that reads the whole block output.  The rest of each layer
+    (conv1 -> norm2 -> relu -> conv2) runs as its own small autograd graph from a leaf on
+    the normalised input.
+
+    Backward: G = the block gradient in fp32 [..., C_total].  In reverse layer order, layer
+    i's output gradient is read from G (``chan_extract``), its graph back-propagated to the
+    leaf, and norm1's backward (reduce + apply on the buffer prefix, ReLU mask recomputed
+    from the buffer) ADDS its input gradient straight into G's first C_i channels in fp32
+    (``bn_bwd(gacc=G)``): no bf16 dx, no separate accumulate pass.  Parameter gradients land
+    in the flat arena from the layers' own kernels.
+
+    Reference: ``_DenseBlock`` / ``_DenseLayer`` of torchvision densenet121 reached from
+    ``/root/reference/models.py:74-81``."""
 
     @staticmethod
     def forward(ctx, x, block, *params):
-        feats = [x.detach()]
+        k = Fn.K(x)
+        layers = list(block.values())
+        c0 = x.shape[-1]
+        ctot = c0 + _growth(block) * len(layers)
+        x = x.detach().contiguous()
+        buf = x.new_empty(x.shape[:-1] + (ctot,))
+        S = torch.empty(2, ctot, dtype=torch.float32, device=x.device)
+        k.chan_insert(buf, 0, x)
+        # shift for the sums: the consuming norm's running mean (any nearby value will do)
+        k.chan_insert(S, 0, k.bn_stats(x, layers[0].norm1.running_mean[:c0]))
         recs = []
-        with torch.enable_grad():
-            for layer in block.values():
-                inp = Fn.cat_channels(feats) if len(feats) > 1 else feats[0]
-                inp = inp.detach().requires_grad_(True)
-                out = layer([inp])
-                recs.append((inp, out))
-                feats.append(out.detach())
+        ci = c0
+        for li, layer in enumerate(layers):
+            n1 = layer.norm1
+            y1, mean, rstd = k.bn_fwd_train(buf, S, n1.weight, n1.bias, n1.running_mean,
+                                            n1.running_var, n1.momentum_value(), n1.eps,
+                                            Fn._empty(x), True, n1.num_batches_tracked,
+                                            channels=ci)
+            leaf = y1.requires_grad_(True)
+            with torch.enable_grad():
+                out = layer.tail(leaf)
+            g = out.shape[-1]
+            k.chan_insert(buf, ci, out.detach())
+            nxt = layers[li + 1].norm1.running_mean[ci:ci + g] if li + 1 < len(layers) else None
+            k.chan_insert(S, ci, k.bn_stats(out.detach(), Fn._or_empty(nxt, x)))
+            recs.append((leaf, out, mean, rstd, ci))
+            ci += g
+        ctx.block = block
         ctx.recs = recs
-        ctx.sizes = [f.shape[-1] for f in feats]
+        ctx.buf = buf
+        ctx.c0 = c0
         ctx.nparams = len(params)
-        return Fn.cat_channels(feats)
+        block._stats = S
+        return buf
 
     @staticmethod
     def backward(ctx, gy):
         k = Fn.K(gy)
         gy = gy.contiguous()
-        ctot = gy.shape[-1]
-        g = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
-        k.chan_accum(g, 0, gy, True)
-        offs = []
-        o = 0
-        for c in ctx.sizes:
-            offs.append(o)
-            o += c
+        buf = ctx.buf
+        layers = list(ctx.block.values())
+        G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
+        k.chan_accum(G, 0, gy, True)
         for i in range(len(ctx.recs) - 1, -1, -1):
-            inp, out = ctx.recs[i]
-            g_out = k.chan_extract(g, offs[i + 1], ctx.sizes[i + 1]).to(out.dtype)
+            leaf, out, mean, rstd, ci = ctx.recs[i]
+            g_out = k.chan_extract(G, ci, out.shape[-1]).to(out.dtype)
             torch.autograd.backward(out, g_out)
-            if inp.grad is not None:
-                k.chan_accum(g, 0, inp.grad, False)
+            n1 = layers[i].norm1
+            gamma, beta = n1.weight, n1.bias
+            dy = leaf.grad
+            if dy is not None:
+                k.bn_bwd(dy.contiguous(), buf, Fn._empty(dy), mean, rstd, gamma,
+                         Fn._sink(gamma, dy), Fn._sink(beta, dy), True, False, beta, gacc=G)
+            Fn._done(gamma, beta)
             ctx.recs[i] = None
-        dx = k.chan_extract(g, 0, ctx.sizes[0]).to(gy.dtype)
+        dx = k.chan_extract(G, 0, ctx.c0).to(gy.dtype)
+        ctx.buf = None
         return (dx, None) + (None,) * ctx.nparams
 
 
@@ -117,8 +182,8 @@ class _Transition(nn.Sequential):
         self.conv = Conv2d(num_input_features, num_output_features, 1, bias=False)
         self.pool = AvgPool2d(2, 2)
 
-    def forward(self, x):
-        x = self.norm(x, relu=True)
+    def forward(self, x, stats=None):
+        x = self.norm(x, relu=True, stats=stats)
         return self.pool(self.conv(x))
 
 
@@ -142,6 +207,9 @@ class DenseNet(nn.Module):
         self.features.add_module("norm5", BatchNorm2d(nf))
         self.classifier = Linear(nf, num_classes)
         self.avgpool = AdaptiveAvgPool2d((1, 1))
+        # dense blocks on one feature buffer (_DenseBlockGrad / _block_eval); utils/parity.py
+        # turns it off to hook every _DenseLayer as a unit
+        self.fused_blocks = True
         for m in self.modules():
             if isinstance(m, Conv2d):
                 m.init_(nn.init.kaiming_normal_)
@@ -151,10 +219,14 @@ class DenseNet(nn.Module):
     def forward(self, x):
         f = self.features
         x = Fn.conv_bn_relu_maxpool(x, f.conv0, f.norm0, f.pool0)
+        stats = None  # [mean | var] of x when the block that produced it already has them
         for name, m in f.named_children():
-            if name.startswith("denseblock") or name.startswith("transition"):
-                x = m(x)
-        x = f.norm5(x, relu=True)  # features.norm5 then F.relu (torchvision densenet forward)
+            if name.startswith("denseblock"):
+                x, stats = m(x, self.fused_blocks)
+            elif name.startswith("transition"):
+                x, stats = m(x, stats), None
+        # features.norm5 then F.relu (torchvision densenet forward)
+        x = f.norm5(x, relu=True, stats=stats)
         x = self.avgpool(x).reshape(x.shape[0], -1)
         return self.classifier(x)
 

@@ -39,12 +39,46 @@ def _avg3(x, join=None):
     return Fn.avg_pool2d(x, (3, 3), (1, 1), (1, 1), False, True, join=join)
 
 
+# MPA_POOL_FIRST=1: branch_pool as torchvision writes it (3x3 average pool over the block
+# input, then the 1x1 conv) instead of the commuted order below
+_POOL_FIRST = os.environ.get("MPA_POOL_FIRST", "0") == "1"
+
+
+class PoolBranch(BasicConv2d):
+    """``branch_pool = BasicConv2d(avg_pool2d(x, 3, 1, 1))`` of InceptionA/C/E
+    (torchvision inception.py, reached from ``/root/reference/models.py:83-95``).
+
+    The 3x3/s1 average pool with count_include_pad (divisor 9 everywhere) and the 1x1 conv
+    are both linear maps - one spatial per channel, one per-pixel channel mix - so they
+    commute exactly: conv1x1(avg(x)) = avg(conv1x1(x)).  Run in that order the pool (forward
+    and backward) works on the conv's 32-192 output channels instead of the block's 192-2048
+    input channels, and x needs no pooled copy: Mixed_5b-7c read and write 3-10x fewer
+    pool bytes.  BN statistics are taken over the pooled values, as in the reference."""
+
+    def forward(self, x, join=None):
+        if _POOL_FIRST:
+            return super().forward(_avg3(x, join))
+        return Fn.bn_act(_avg3(Fn.conv_act(x, self.conv, relu=False, join=join)), self.bn,
+                         relu=True)
+
+
 def _max3s2(x, join=None):
     return Fn.max_pool2d(x, (3, 3), (2, 2), (0, 0), False, join=join)
 
 
 def _cat(xs):
     return Fn.cat_channels(xs)
+
+
+def _heads(mod, x, heads):
+    """Whether the block's 1x1 branch heads run as ONE grouped GEMM (Fn.conv1x1_group):
+    training with their weights adjacent in the arena (Inception3._mpa_param_groups);
+    ``merge_1x1 = False`` (utils/parity.py) keeps them separate modules."""
+    return getattr(mod, "merge_1x1", True) and _MERGE and Fn.conv1x1_group_ok(x, heads)
+
+
+# MPA_MERGE_1X1=0: every 1x1 branch head is its own GEMM reading the block input
+_MERGE = os.environ.get("MPA_MERGE_1X1", "1") == "1"
 
 
 def _join(mod, x, n, join=None):
@@ -66,14 +100,21 @@ class InceptionA(nn.Module):
         self.branch3x3dbl_1 = BasicConv2d(in_channels, 64, 1)
         self.branch3x3dbl_2 = BasicConv2d(64, 96, 3, padding=1)
         self.branch3x3dbl_3 = BasicConv2d(96, 96, 3, padding=1)
-        self.branch_pool = BasicConv2d(in_channels, pool_features, 1)
+        self.branch_pool = PoolBranch(in_channels, pool_features, 1)
+
+    def heads(self):
+        return [self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1]
 
     def forward(self, x, join=None):
-        j = _join(self, x, 4, join)
-        b1 = self.branch1x1(x, j)
-        b5 = self.branch5x5_2(self.branch5x5_1(x, j))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)))
-        bp = self.branch_pool(_avg3(x, j))
+        if _heads(self, x, self.heads()):
+            j = _join(self, x, 2, join)
+            b1, b5, b3 = Fn.conv1x1_group(x, self.heads(), j)
+        else:
+            j = _join(self, x, 4, join)
+            b1, b5, b3 = self.branch1x1(x, j), self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
+        b5 = self.branch5x5_2(b5)
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(b3))
+        bp = self.branch_pool(x, j)
         return _cat([b1, b5, b3, bp])
 
 
@@ -105,17 +146,24 @@ class InceptionC(nn.Module):
         self.branch7x7dbl_3 = BasicConv2d(c7, c7, (1, 7), padding=(0, 3))
         self.branch7x7dbl_4 = BasicConv2d(c7, c7, (7, 1), padding=(3, 0))
         self.branch7x7dbl_5 = BasicConv2d(c7, 192, (1, 7), padding=(0, 3))
-        self.branch_pool = BasicConv2d(in_channels, 192, 1)
+        self.branch_pool = PoolBranch(in_channels, 192, 1)
+
+    def heads(self):
+        return [self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1]
 
     def forward(self, x, join=None):
-        j = _join(self, x, 4, join)
-        b1 = self.branch1x1(x, j)
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, j)))
-        bd = self.branch7x7dbl_1(x, j)
+        if _heads(self, x, self.heads()):
+            j = _join(self, x, 2, join)
+            b1, b7, bd = Fn.conv1x1_group(x, self.heads(), j)
+        else:
+            j = _join(self, x, 4, join)
+            b1, b7, bd = (self.branch1x1(x, j), self.branch7x7_1(x, j),
+                          self.branch7x7dbl_1(x, j))
+        b7 = self.branch7x7_3(self.branch7x7_2(b7))
         for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
                   self.branch7x7dbl_5):
             bd = m(bd)
-        bp = self.branch_pool(_avg3(x, j))
+        bp = self.branch_pool(x, j)
         return _cat([b1, b7, bd, bp])
 
 
@@ -129,10 +177,18 @@ class InceptionD(nn.Module):
         self.branch7x7x3_3 = BasicConv2d(192, 192, (7, 1), padding=(3, 0))
         self.branch7x7x3_4 = BasicConv2d(192, 192, 3, stride=2)
 
+    def heads(self):
+        return [self.branch3x3_1, self.branch7x7x3_1]
+
     def forward(self, x, join=None):
-        j = _join(self, x, 3, join)
-        b3 = self.branch3x3_2(self.branch3x3_1(x, j))
-        b7 = self.branch7x7x3_1(x, j)
+        # (a join handed in by the parent counts this block's consumers: see Inception3)
+        if _heads(self, x, self.heads()):
+            j = _join(self, x, 2, join)
+            b3, b7 = Fn.conv1x1_group(x, self.heads(), j)
+        else:
+            j = _join(self, x, 3, join)
+            b3, b7 = self.branch3x3_1(x, j), self.branch7x7x3_1(x, j)
+        b3 = self.branch3x3_2(b3)
         for m in (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4):
             b7 = m(b7)
         return _cat([b3, b7, _max3s2(x, j)])
@@ -149,18 +205,24 @@ class InceptionE(nn.Module):
         self.branch3x3dbl_2 = BasicConv2d(448, 384, 3, padding=1)
         self.branch3x3dbl_3a = BasicConv2d(384, 384, (1, 3), padding=(0, 1))
         self.branch3x3dbl_3b = BasicConv2d(384, 384, (3, 1), padding=(1, 0))
-        self.branch_pool = BasicConv2d(in_channels, 192, 1)
+        self.branch_pool = PoolBranch(in_channels, 192, 1)
+
+    def heads(self):
+        return [self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1]
 
     def forward(self, x, join=None):
-        j = _join(self, x, 4, join)
-        b1 = self.branch1x1(x, j)
-        b3 = self.branch3x3_1(x, j)
+        if _heads(self, x, self.heads()):
+            j = _join(self, x, 2, join)
+            b1, b3, bd = Fn.conv1x1_group(x, self.heads(), j)
+        else:
+            j = _join(self, x, 4, join)
+            b1, b3, bd = self.branch1x1(x, j), self.branch3x3_1(x, j), self.branch3x3dbl_1(x, j)
         j3 = _join(self, b3, 2)  # b3 and bd each feed a (1x3) and a (3x1) conv
         b3a, b3b = self.branch3x3_2a(b3, j3), self.branch3x3_2b(b3, j3)
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, j))
+        bd = self.branch3x3dbl_2(bd)
         jd = _join(self, bd, 2)
         bda, bdb = self.branch3x3dbl_3a(bd, jd), self.branch3x3dbl_3b(bd, jd)
-        bp = self.branch_pool(_avg3(x, j))
+        bp = self.branch_pool(x, j)
         # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
         # as one flat concat, which copies every branch once instead of twice
         return _cat([b1, b3a, b3b, bda, bdb, bp])
@@ -227,7 +289,8 @@ class Inception3(nn.Module):
             # Mixed_6e's output feeds the aux head's pool and Mixed_7a's three branches
             # (cross_join = False keeps the two modules' input gradients apart, for the
             # per-unit parity check of utils/parity.py)
-            j = _join(self.Mixed_7a, x, 4) if self.cross_join else None
+            n7a = 3 if _heads(self.Mixed_7a, x, self.Mixed_7a.heads()) else 4
+            j = _join(self.Mixed_7a, x, n7a) if self.cross_join else None
             aux = self.AuxLogits(x, j)
             x = self.Mixed_7a(x, j)
         else:
@@ -240,6 +303,15 @@ class Inception3(nn.Module):
         if self.training and self.aux_logits:
             return InceptionOutputs(x, aux)
         return x
+
+
+def _param_groups(self):
+    """Weights of each block's 1x1 branch heads, back to back in the arena (Fn.conv1x1_group)."""
+    return [[h.conv.weight for h in m.heads()] for m in self.modules()
+            if isinstance(m, (InceptionA, InceptionC, InceptionD, InceptionE))]
+
+
+Inception3._mpa_param_groups = _param_groups
 
 
 def inception_v3(num_classes: int = 1000) -> Inception3:

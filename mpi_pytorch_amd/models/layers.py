@@ -248,8 +248,8 @@ class BatchNorm2d(nn.Module):
         if key in state_dict:
             self._batches_host = int(state_dict[key])
 
-    def forward(self, x, relu: bool = False):
-        return Fn.bn_act(x, self, relu=relu)
+    def forward(self, x, relu: bool = False, stats=None):
+        return Fn.bn_act(x, self, relu=relu, stats=stats)
 
     def extra_repr(self):
         return "{}, eps={}, momentum={}".format(self.num_features, self.eps, self.momentum)

@@ -301,6 +301,90 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
                          _or_empty(residual, x), relu)
 
 
+class _ConvGroupBNAct(torch.autograd.Function):
+    """relu(bn_b(conv_b(x))) for several 1x1 convs that read the same x (Inception's branch
+    heads), as ONE GEMM over their joint output rows.
+
+    The weights sit back to back in the arena (``_mpa_param_groups``), so the joint weight,
+    its bf16 shadow and its gradient are flat views - no copies.  Forward: one conv over
+    N = sum N_b columns with BN statistics from its epilogue, then each branch's BN+ReLU
+    reads its channel window of z (strided rows).  Backward: each branch's BN backward
+    writes its window of ONE dz, then one wgrad (x read once, not once per branch) and ONE
+    dgrad (one write of dx instead of a write plus an accumulate pass per extra branch).
+    Reference: InceptionA/C/D/E branch heads of torchvision inception_v3, reached from
+    ``/root/reference/models.py:83-95``."""
+
+    @staticmethod
+    def forward(ctx, x, W, mods, join, *params):
+        k = K(x)
+        ntot = W.shape[0]
+        stats = torch.empty(2, ntot, device=x.device, dtype=torch.float32)
+        z = k.conv_fwd(x, W, _empty(x), 1, 1, 0, 0, False, stats, _empty(x))
+        outs, saved, o = [], [], 0
+        for m in mods:
+            bn, n = m.bn, m.conv.weight.shape[0]
+            y, mean, rstd = k.bn_fwd_train(z[..., o:o + n], stats[:, o:o + n], bn.weight,
+                                           bn.bias, bn.running_mean, bn.running_var,
+                                           bn.momentum_value(), bn.eps, _empty(x), True,
+                                           bn.num_batches_tracked)
+            outs.append(y)
+            saved.append((mean, rstd, o, n))
+            o += n
+        ctx.mods, ctx.join, ctx.saved, ctx.W = mods, join, saved, W
+        ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.nparams = len(params)
+        ctx.save_for_backward(x, z)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x, z = ctx.saved_tensors
+        k = K(z)
+        dz = torch.empty_like(z)
+        for m, (mean, rstd, o, n), dy in zip(ctx.mods, ctx.saved, dys):
+            gamma, beta = m.bn.weight, m.bn.bias
+            k.bn_bwd(dy.contiguous(), z[..., o:o + n], _empty(dy), mean, rstd, gamma,
+                     _sink(gamma, dy), _sink(beta, dy), True, False, beta,
+                     dx_out=dz[..., o:o + n])
+            _done(gamma, beta)
+        ws = [m.conv.weight for m in ctx.mods]
+        if ws[0].requires_grad:
+            fresh = [_fresh(w) for w in ws]  # (every flag consumed)
+            G = ws[0]._mpa_arena.flat_view(ws, "grad").view(ctx.W.shape)
+            k.conv_wgrad(dz, x, G, 1, 1, 0, 0, overwrite=all(fresh))
+            _done(*ws)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad_joined(k, ctx.join, dz, ctx.W, ctx.in_hw, ctx.mods[0].conv, None)
+        ctx.W = None
+        return (dx, None, None, None) + (None,) * ctx.nparams
+
+
+def conv1x1_group_ok(x, mods) -> bool:
+    """Whether ``conv1x1_group`` can run ``mods`` (train-mode 1x1/s1 BasicConv2d's whose
+    weights are one flat arena range)."""
+    ws = [m.conv.weight for m in mods]
+    a = getattr(ws[0], "_mpa_arena", None)
+    if a is None or not torch.is_grad_enabled() or not all(m.bn.training for m in mods):
+        return False
+    if any(m.conv.kgeom != (1, 1, 0, 0) or m.conv.weight.shape[1:3] != (1, 1) or
+           m.conv.bias is not None or not w.requires_grad for m, w in zip(mods, ws)):
+        return False
+    return a.flat_view(ws, "master") is not None
+
+
+def conv1x1_group(x, mods, join: Optional[GradJoin] = None):
+    """[relu(bn(conv(x))) for each BasicConv2d in mods] as one GEMM (see _ConvGroupBNAct);
+    ``join``: x's gradient is summed with its other consumers' (one contribution here)."""
+    ws = [m.conv.weight for m in mods]
+    a = ws[0]._mpa_arena
+    W = a.flat_view(ws, "shadow" if a.shadow is not None else "master")
+    ntot = sum(w.shape[0] for w in ws)
+    W = W.view(ntot, 1, 1, ws[0].shape[-1])
+    params = [p for m in mods for p in (m.conv.weight, m.bn.weight, m.bn.bias) if p is not None]
+    return _ConvGroupBNAct.apply(x, W, list(mods), join, *params)
+
+
 def _pool_out(n: int, k: int, s: int, p: int, ceil: bool) -> int:
     """Pooled extent, ATen's rule (a ceil-mode window must start inside the padded input)."""
     o = (n + 2 * p - k + (s - 1 if ceil else 0)) // s + 1
@@ -379,7 +463,7 @@ def conv_bn_relu_maxpool(x, conv, bn, pool):
 # ============================================================================ conv + bias
 class _ConvAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, conv, relu):
+    def forward(ctx, x, w, b, conv, relu, join=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
         y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu, _empty(x),
@@ -388,6 +472,7 @@ class _ConvAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.params = (w, b)
         ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.join = join
         ctx.save_for_backward(x, y if relu else None)
         return y
 
@@ -407,15 +492,16 @@ class _ConvAct(torch.autograd.Function):
             _done(w)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k.conv_dgrad(g, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
-                               weight_t_of(w))
-        return dx, None, None, None, None
+            dx = _dgrad_joined(k, ctx.join, g, weight_of(w), ctx.in_hw, conv, weight_t_of(w))
+        return dx, None, None, None, None, None
 
 
-def conv_act(x, conv, relu: bool = False):
+def conv_act(x, conv, relu: bool = False, join: Optional[GradJoin] = None):
+    """act(conv(x) + b); ``join``: x's gradient is summed with its other consumers' (see
+    GradJoin)."""
     x = conv.fit_input(x)
     if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
-        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu)
+        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu, join)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,
@@ -425,9 +511,9 @@ def conv_act(x, conv, relu: bool = False):
 # =========================================================================== standalone BN
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, bn, relu):
+    def forward(ctx, x, gamma, beta, bn, relu, stats=None):
         k = K(x)
-        y, mean, rstd = k.bn_fwd_train(x, _empty(x), gamma, beta, bn.running_mean,
+        y, mean, rstd = k.bn_fwd_train(x, _or_empty(stats, x), gamma, beta, bn.running_mean,
                                        bn.running_var, bn.momentum_value(), bn.eps, _empty(x),
                                        relu, bn.num_batches_tracked)
         ctx.params = (gamma, beta)
@@ -443,12 +529,14 @@ class _BNAct(torch.autograd.Function):
         dx, _g = k.bn_bwd(dy, x, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
                           _sink(beta, dy), bool(ctx.needs_input_grad[0]), False)
         _done(gamma, beta)
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
-def bn_act(x, bn, relu: bool = True):
+def bn_act(x, bn, relu: bool = True, stats: Optional[torch.Tensor] = None):
+    """relu?(bn(x)); ``stats`` (train mode): x's [mean | var] [2, C] when already known
+    (a DenseNet block's per-feature statistics), saving the statistics pass."""
     if bn.training:
-        return _BNAct.apply(x, bn.weight, bn.bias, bn, relu)
+        return _BNAct.apply(x, bn.weight, bn.bias, bn, relu, stats)
     return K(x).bn_fwd_eval(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
                             _empty(x), relu)
 

@@ -113,9 +113,12 @@ def bitmask_unpack(m, shape):
 
 
 def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu,
-                 counter=None, mask=None):
+                 counter=None, mask=None, channels=0):
     # the oracle always uses exact two-pass statistics (``stats`` from a fused producer
-    # epilogue is accepted for API parity but not needed)
+    # epilogue is accepted for API parity but not needed); channels > 0: BN of the first
+    # ``channels`` channels of a wider buffer
+    if channels:
+        x = x[..., :channels]
     C = x.shape[-1]
     xf = _f(x).reshape(-1, C)
     M = xf.shape[0]
@@ -139,7 +142,14 @@ def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, re
     return y, mean.contiguous(), rstd.contiguous()
 
 
-def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
+def bn_stats(x, shift=None):
+    xf = _f(x).reshape(-1, x.shape[-1])
+    return torch.stack([xf.mean(0), xf.var(0, unbiased=False)])
+
+
+def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu, channels=0):
+    if channels:
+        x = x[..., :channels]
     C = x.shape[-1]
     xf = _f(x).reshape(-1, C)
     rstd = torch.rsqrt(rvar + eps)
@@ -152,11 +162,13 @@ def bn_fwd_eval(x, gamma, beta, rmean, rvar, eps, residual, relu):
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zmask_beta=None,
-           ymask=None):
+           ymask=None, gacc=None, dx_out=None):
     """Returns (dx, g) where g = dy masked by ReLU (the residual-branch gradient).  The mask
     comes from ``ymask`` (bn_fwd_train's bit mask) if given, else from ``y``, else - with
-    ``zmask_beta`` - is recomputed from x for y = relu(bn(x))."""
-    C = x.shape[-1]
+    ``zmask_beta`` - is recomputed from x for y = relu(bn(x)).  x may be wider than dy (a
+    channel prefix); ``gacc`` (fp32): dx is added into its first C channels instead."""
+    C = dy.shape[-1]
+    x = x[..., :C]
     g = _f(dy).reshape(-1, C)
     if _opt(ymask) is not None:
         g = g * bitmask_unpack(ymask, g.shape)
@@ -175,10 +187,16 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zma
     if _opt(dbeta) is not None:
         dbeta.add_(sg)
     dx = None
-    if want_dx:
+    if gacc is not None:
+        d = (gamma * rstd) * (g - sg / M - xhat * (sgx / M))
+        gacc[..., :C] += d.reshape(dy.shape)
+    elif want_dx:
         dx = (gamma * rstd) * (g - sg / M - xhat * (sgx / M))
-        dx = dx.reshape(x.shape).to(dy.dtype)
-    return dx, g.reshape(x.shape).to(dy.dtype)
+        dx = dx.reshape(dy.shape).to(dy.dtype)
+        if dx_out is not None:
+            dx_out.copy_(dx)
+            dx = dx_out
+    return dx, g.reshape(dy.shape).to(dy.dtype)
 
 
 def bn_bwd_apply(dy, x, y, mean, rstd, gamma, dgamma, dbeta, sums, want_dx, want_g=True):
@@ -460,6 +478,10 @@ def chan_accum(g, off, src, assign):
         g[..., off:off + cs] = src.float()
     else:
         g[..., off:off + cs] += src.float()
+
+
+def chan_insert(dst, off, src):
+    dst[..., off:off + src.shape[-1]] = src
 
 
 def chan_extract(g, off, cs):

@@ -37,6 +37,27 @@ def _align(n: int) -> int:
     return (n + ALIGN - 1) // ALIGN * ALIGN
 
 
+def _group_params(trainable: List[nn.Parameter], groups) -> List[nn.Parameter]:
+    """Reorder so each group's parameters sit back to back, in the group's order, at the
+    position of its first member (model hint ``_mpa_param_groups``: e.g. the weights of
+    1x1 convs that read the same input and run as ONE GEMM over their joint rows)."""
+    pos = {id(p): i for i, p in enumerate(trainable)}
+    taken, firsts = set(), {}
+    for g in groups:
+        ids = [id(p) for p in g]
+        if len(g) < 2 or any(i not in pos or i in taken for i in ids) or len(set(ids)) < len(ids):
+            continue
+        firsts[min(pos[i] for i in ids)] = list(g)
+        taken.update(ids)
+    out: List[nn.Parameter] = []
+    for i, p in enumerate(trainable):
+        if i in firsts:
+            out.extend(firsts[i])
+        elif id(p) not in taken:
+            out.append(p)
+    return out
+
+
 class ParamArena:
     def __init__(self, model: nn.Module, device: torch.device, shadow: Optional[bool] = None):
         self.device = torch.device(device)
@@ -52,6 +73,9 @@ class ParamArena:
             params.append(p)
             names[id(p)] = n
         trainable = [p for p in params if p.requires_grad][::-1]
+        groups = getattr(model, "_mpa_param_groups", None)
+        if callable(groups):
+            trainable = _group_params(trainable, groups())
         frozen = [p for p in params if not p.requires_grad]
         self.params: List[nn.Parameter] = trainable + frozen
         self.trainable: List[nn.Parameter] = trainable
@@ -133,6 +157,21 @@ class ParamArena:
     def slice_of(self, p: nn.Parameter):
         o = self.offsets[id(p)]
         return o, o + p.numel()
+
+    def flat_view(self, params: List[nn.Parameter], which: str) -> Optional[torch.Tensor]:
+        """ONE flat view of ``params`` in the master / grad / shadow buffer when they sit
+        back to back without alignment padding (see ``_mpa_param_groups``), else None."""
+        o0 = o = self.offsets.get(id(params[0]), -1)
+        if o0 < 0:
+            return None
+        for p in params:
+            if self.offsets.get(id(p)) != o:
+                return None
+            o += p.numel()
+        t = getattr(self, which)
+        if t is None or o > t.numel():
+            return None
+        return t[o0:o]
 
     def sync_shadow(self) -> None:
         """Refresh the bf16 weight shadow from the fp32 masters (after init/load)."""

@@ -159,6 +159,15 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
     cross = getattr(model_gpu, "cross_join", None)
     if cross is not None:
         model_gpu.cross_join = False
+    # DenseNet's fused blocks run each layer's norm1 inside the block, not through the
+    # _DenseLayer module: the plain per-layer path makes every layer a hooked unit
+    fused = getattr(model_gpu, "fused_blocks", None)
+    if fused is not None:
+        model_gpu.fused_blocks = False
+    # Inception's grouped 1x1 branch heads: one GEMM, not the BasicConv2d units
+    grouped = [m for m in model_gpu.modules() if hasattr(m, "heads")]
+    for m in grouped:
+        m.merge_1x1 = False
     try:
         arena = model_gpu._mpa_arena
         arena.zero_grad()
@@ -173,6 +182,10 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             del m.run_group
         if cross is not None:
             model_gpu.cross_join = cross
+        if fused is not None:
+            model_gpu.fused_blocks = fused
+        for m in grouped:
+            m.__dict__.pop("merge_1x1", None)
     g_gpu = arena.grad.detach().cpu()
     out = []
     plain = {name: m for name, m in units}

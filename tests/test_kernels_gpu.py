@@ -611,6 +611,53 @@ def test_bn_relu_bitmask(gpu, M, Cc):
     assert torch.equal(dg, dg2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,Cc,Ctot", [(4096, 64, 96), (3001, 136, 256), (50000, 32, 32)])
+def test_bn_channel_prefix_and_accumulate(gpu, M, Cc, Ctot):
+    """DenseNet block buffer: BN (train / eval forward, z-mask backward) of the first Cc
+    channels of a [M, Ctot] buffer with precomputed [2, Ctot] statistics == the same BN of
+    a contiguous copy, bit for bit; bn_bwd(gacc=G) adds dx into G's first Cc channels in
+    fp32 and leaves the rest untouched; bn_stats / chan_insert against the oracle."""
+    torch.manual_seed(21)
+    buf = (bf(M, Ctot, dev=gpu, scale=2.0) + 0.3).to(torch.bfloat16)
+    xc = buf[:, :Cc].contiguous()
+    S = C().bn_stats(buf, torch.empty(0, device=gpu))
+    Sr = ref.bn_stats(buf)
+    assert rel(S[0], Sr[0]) < 1e-3 and rel(S[1], Sr[1]) < 1e-3
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu)
+    e = torch.empty(0, device=gpu)
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    rm2, rv2 = rm.clone(), rv.clone()
+    y, mean, rstd = C().bn_fwd_train(buf, S, g, b, rm, rv, 0.1, 1e-5, e, True, e, channels=Cc)
+    y2, mean2, rstd2 = C().bn_fwd_train(xc, S[:, :Cc].contiguous(), g, b, rm2, rv2, 0.1, 1e-5, e,
+                                        True, e)
+    torch.cuda.synchronize()
+    assert y.shape == (M, Cc) and torch.equal(y, y2) and torch.equal(rm, rm2)
+    assert torch.equal(C().bn_fwd_eval(buf, g, b, rm, rv, 1e-5, e, True, channels=Cc),
+                       C().bn_fwd_eval(xc, g, b, rm, rv, 1e-5, e, True))
+    dy = bf(M, Cc, dev=gpu)
+    G = torch.randn(M, Ctot, device=gpu)
+    G0 = G.clone()
+    dg, db = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dg2, db2 = dg.clone(), db.clone()
+    dx0, _ = C().bn_bwd(dy, buf, e, mean, rstd, g, dg, db, True, False, b, gacc=G)
+    dx, _ = C().bn_bwd(dy, xc, e, mean2, rstd2, g, dg2, db2, True, False, b)
+    torch.cuda.synchronize()
+    assert dx0 is None or dx0.numel() == 0
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    assert torch.equal(G[:, Cc:], G0[:, Cc:])
+    want = G0[:, :Cc] + dx.float()
+    assert float((G[:, :Cc] - want).abs().max()) <= 1e-2 * float(dx.float().abs().max()) + 1e-6
+    # chan_insert: bf16 activations and fp32 rows
+    dst = torch.zeros(M, Ctot + 32, dtype=torch.bfloat16, device=gpu)
+    C().chan_insert(dst, 32, buf)
+    st = torch.zeros(2, Ctot + 64, device=gpu)
+    C().chan_insert(st, 64, S)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:, 32:], buf) and not dst[:, :32].any()
+    assert torch.equal(st[:, 64:], S) and not st[:, :64].any()
+
+
 def test_bn_stats_from_conv(gpu):
     """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
     torch.manual_seed(5)

@@ -6,7 +6,7 @@ import torch
 import torch.nn.functional as F
 
 from mpi_pytorch_amd.models import initialize_model, ARCH
-from mpi_pytorch_amd.engine import build_model, loss_fn
+from mpi_pytorch_amd.engine import build_model, build_training, loss_fn
 from mpi_pytorch_amd.parallel import World
 
 # torchvision totals at 1000 classes
@@ -281,3 +281,88 @@ def test_whole_model_gradients_are_shattered_in_fp32():
     c_bf16 = cos(g0, grad(x.to(torch.bfloat16).float()))
     c_tiny = cos(g0, grad(x * (1 + 1e-6 * torch.randn_like(x))))
     assert c_tiny > 0.999 and c_bf16 < 0.99, (c_tiny, c_bf16)
+
+
+def test_inception_pool_branch_commutes_with_conv(monkeypatch):
+    """PoolBranch runs avg_pool(conv1x1(x)) instead of conv1x1(avg_pool(x)) (both linear,
+    count_include_pad): output, input gradient and parameter gradients equal the
+    torchvision order (MPA_POOL_FIRST) to fp32 rounding, with BN in train mode."""
+    import mpi_pytorch_amd.models.inception as I
+    from mpi_pytorch_amd.parallel import ParamArena
+    torch.manual_seed(0)
+    m = I.PoolBranch(64, 32, 1)
+    m._mpa_arena = ParamArena(m, torch.device("cpu"))
+    m.train()
+    x = torch.randn(4, 9, 9, 64, requires_grad=True)
+    outs = []
+    for first in (False, True):
+        monkeypatch.setattr(I, "_POOL_FIRST", first)
+        x.grad = None
+        m._mpa_arena.zero_grad()
+        y = m(x)
+        y.backward(torch.linspace(-1, 1, y.numel()).view_as(y))
+        outs.append((y.detach(), x.grad.clone(), m._mpa_arena.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))
+
+
+def test_inception_grouped_heads_equal_separate_convs():
+    """Inception's 1x1 branch heads as ONE grouped GEMM (weights back to back in the arena,
+    per-branch BN on channel windows, one wgrad / dgrad) == the separate BasicConv2d's, in
+    fp32 on the CPU: same logits, same running statistics, gradients to fp32 rounding."""
+    import mpi_pytorch_amd.ops.functional as Fn
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("inception", 10, torch.device("cpu"), World(), 1e-3)
+    model.dropout.p = 0.0
+    a = model._mpa_arena
+    heads = [m for m in model.modules() if hasattr(m, "heads")]
+    assert len(heads) == 10
+    for m in heads:  # every group is one flat arena range
+        assert a.flat_view([h.conv.weight for h in m.heads()], "grad") is not None
+    x = torch.randn(2, 299, 299, 8) * (torch.arange(8) < 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    for merged in (True, False):
+        for m in heads:
+            m.merge_1x1 = merged
+        model.load_state_dict(sd)
+        a.zero_grad()
+        out = model(x)
+        loss_fn(out, y).backward()
+        res.append((out[0].detach(), a.grad.clone(),
+                    [v.clone() for k, v in model.state_dict().items() if "running" in k]))
+    (o1, g1, r1), (o2, g2, r2) = res
+    assert torch.allclose(o1, o2, atol=1e-5)
+    assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
+def test_densenet_feature_buffer_blocks_equal_plain_autograd():
+    """DenseNet blocks on one feature buffer (norm1 on the channel prefix with per-feature
+    statistics taken once, input gradients added into one fp32 accumulator) == per-layer
+    concat + plain autograd, in fp32 on the CPU (train and eval forward, gradients, running
+    statistics)."""
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("densenet", 10, torch.device("cpu"), World(), 1e-3)
+    a = model._mpa_arena
+    x = torch.randn(2, 64, 64, 8) * (torch.arange(8) < 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    for fused in (True, False):
+        model.fused_blocks = fused
+        model.load_state_dict(sd)
+        model.train()
+        a.zero_grad()
+        out = model(x)
+        loss_fn(out, y).backward()
+        model.eval()
+        with torch.no_grad():
+            ev = model(x)
+        res.append((out.detach(), ev, a.grad.clone(),
+                    [v.clone() for k, v in model.state_dict().items() if "running" in k]))
+    (o1, e1, g1, r1), (o2, e2, g2, r2) = res
+    assert torch.allclose(o1, o2, atol=1e-5) and torch.allclose(e1, e2, atol=1e-5)
+    assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
