@@ -603,27 +603,47 @@ Tensor maxpool_bn_bwd(Tensor dp, Tensor idx, Tensor z, Tensor mean, Tensor rstd,
   return dz;
 }
 
+// x: contiguous NHWC or a channel-window view of a wider buffer (pixel stride ldx)
 Tensor avgpool_fwd(Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
                    int64_t pw, bool ceil, bool cip) {
-  CHECK_ACT(x);
+  CHECK_CUDA(x);
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 4, "avgpool: NHWC input");
+  const int ldx = row_stride(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(ldx == C || (C % 8 == 0 && ldx % 8 == 0), "avgpool: window must be 16-B aligned");
   const int P = pool_out(H, kh, sh, ph, ceil), Q = pool_out(W, kw, sw, pw, ceil);
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor y = empty_like_shape(x, {N, P, Q, C}, torch::kBFloat16);
   mpa::avgpool_fwd(bp(x), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, cip ? 1 : 0, bpm(y),
-                   cur_stream());
+                   cur_stream(), ldx);
   return y;
 }
 
+// dx_out (optional): write dx into this [N, H, W, C] view (a channel window of a wider
+// buffer) instead of a new tensor
 Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh,
-                   int64_t sw, int64_t ph, int64_t pw, bool ceil, bool cip) {
+                   int64_t sw, int64_t ph, int64_t pw, bool ceil, bool cip,
+                   c10::optional<Tensor> dx_out) {
   CHECK_ACT(dy);
   (void)ceil;
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
   const c10::OptionalDeviceGuard g(device_of(dy));
-  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  Tensor dx;
+  int ldo = C;
+  if (dx_out && dx_out->defined() && dx_out->numel() > 0) {
+    dx = *dx_out;
+    CHECK_CUDA(dx);
+    CHECK_BF16(dx);
+    TORCH_CHECK(dx.dim() == 4 && dx.size(0) == N && dx.size(1) == H && dx.size(2) == W &&
+                    dx.size(3) == C, "avgpool_bwd: dx_out shape");
+    ldo = row_stride(dx);
+    TORCH_CHECK(ldo == C || (C % 8 == 0 && ldo % 8 == 0), "avgpool: window must be 16-B aligned");
+  } else {
+    dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  }
   mpa::avgpool_bwd(bp(dy), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, cip ? 1 : 0, bpm(dx),
-                   cur_stream());
+                   cur_stream(), ldo);
   return dx;
 }
 
@@ -1143,7 +1163,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dbeta"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("zsel") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
-  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("H"), py::arg("W"), py::arg("kh"),
+        py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("ceil"), py::arg("cip"), py::arg("dx_out") = py::none());
   m.def("adaptive_avgpool_fwd", &adaptive_avgpool_fwd);
   m.def("adaptive_avgpool_bwd", &adaptive_avgpool_bwd);
   m.def("linear_fwd", &linear_fwd);

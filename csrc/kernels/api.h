@@ -239,12 +239,13 @@ void maxpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, in
 void maxpool_bwd(const bf16_raw* dy, const uint8_t* idx, int N, int H, int W, int C, int P,
                  int Q, int kh, int kw, int sh, int sw, int ph, int pw, bf16_raw* dx,
                  hipStream_t s);
+// ldx / ldo: pixel stride of x / dx (0: C) - a channel window of a wider NHWC buffer
 void avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, int kh, int kw,
                  int sh, int sw, int ph, int pw, int count_include_pad, bf16_raw* y,
-                 hipStream_t s);
+                 hipStream_t s, int ldx = 0);
 void avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q, int kh, int kw,
                  int sh, int sw, int ph, int pw, int count_include_pad, bf16_raw* dx,
-                 hipStream_t s);
+                 hipStream_t s, int ldo = 0);
 void adaptive_avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q,
                           bf16_raw* y, hipStream_t s);
 void adaptive_avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q,

@@ -126,7 +126,7 @@ __device__ __forceinline__ float avg_div(int p, int q, int H, int W, int kh, int
 template <int V>
 __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int H, int W, int C,
                                    int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
-                                   int cip, bf16_t* __restrict__ y) {
+                                   int cip, bf16_t* __restrict__ y, int ldx) {
   const int cv = C / V;
   const int64_t total = (int64_t)N * P * Q * cv;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
@@ -147,7 +147,7 @@ __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int H, i
         const int w = w0 + k;
         if ((unsigned)w >= (unsigned)W) continue;
         float f[V];
-        Vec<V>::load(x + (((size_t)n * H + h) * W + w) * C + cc * V, f);
+        Vec<V>::load(x + (((size_t)n * H + h) * W + w) * ldx + cc * V, f);
 #pragma unroll
         for (int j = 0; j < V; ++j) acc[j] += f[j];
       }
@@ -162,7 +162,7 @@ __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int H, i
 template <int V>
 __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, int N, int H, int W, int C,
                                    int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
-                                   int cip, bf16_t* __restrict__ dx) {
+                                   int cip, bf16_t* __restrict__ dx, int ldo) {
   const int cv = C / V;
   const int64_t total = (int64_t)N * H * W * cv;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
@@ -190,7 +190,7 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, int N, int H, 
         for (int j = 0; j < V; ++j) acc[j] += g[j] * d;
       }
     }
-    Vec<V>::store(dx + (((size_t)n * H + h) * W + w) * C + cc * V, acc);
+    Vec<V>::store(dx + (((size_t)n * H + h) * W + w) * ldo + cc * V, acc);
   }
 }
 
@@ -286,14 +286,16 @@ void maxpool_bwd(const bf16_raw* dy, const uint8_t* idx, int N, int H, int W, in
               sw, ph, pw, dx);
 }
 void avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q, int kh, int kw,
-                 int sh, int sw, int ph, int pw, int cip, bf16_raw* y, hipStream_t s) {
+                 int sh, int sw, int ph, int pw, int cip, bf16_raw* y, hipStream_t s, int ldx) {
+  if (ldx <= 0) ldx = C;
   POOL_LAUNCH(avgpool_fwd_kernel, (int64_t)N * P * Q * C, x, N, H, W, C, P, Q, kh, kw, sh, sw,
-              ph, pw, cip, y);
+              ph, pw, cip, y, ldx);
 }
 void avgpool_bwd(const bf16_raw* dy, int N, int H, int W, int C, int P, int Q, int kh, int kw,
-                 int sh, int sw, int ph, int pw, int cip, bf16_raw* dx, hipStream_t s) {
+                 int sh, int sw, int ph, int pw, int cip, bf16_raw* dx, hipStream_t s, int ldo) {
+  if (ldo <= 0) ldo = C;
   POOL_LAUNCH(avgpool_bwd_kernel, (int64_t)N * H * W * C, dy, N, H, W, C, P, Q, kh, kw, sh, sw,
-              ph, pw, cip, dx);
+              ph, pw, cip, dx, ldo);
 }
 void adaptive_avgpool_fwd(const bf16_raw* x, int N, int H, int W, int C, int P, int Q,
                           bf16_raw* y, hipStream_t s) {

@@ -55,6 +55,10 @@ class PoolBranch(BasicConv2d):
     input channels, and x needs no pooled copy: Mixed_5b-7c read and write 3-10x fewer
     pool bytes.  BN statistics are taken over the pooled values, as in the reference."""
 
+    # avg_pool2d(3, 1, 1, ceil_mode=False, count_include_pad=True) as the grouped GEMM's
+    # (kh, kw, sh, sw, ph, pw, ceil, cip) for this member (Fn.conv1x1_group)
+    pool_after = (3, 3, 1, 1, 1, 1, False, True)
+
     def forward(self, x, join=None):
         if _POOL_FIRST:
             return super().forward(_avg3(x, join))
@@ -103,18 +107,17 @@ class InceptionA(nn.Module):
         self.branch_pool = PoolBranch(in_channels, pool_features, 1)
 
     def heads(self):
-        return [self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1]
+        return [self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
-        if _heads(self, x, self.heads()):
-            j = _join(self, x, 2, join)
-            b1, b5, b3 = Fn.conv1x1_group(x, self.heads(), j)
+        if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
+            b1, b5, b3, bp = Fn.conv1x1_group(x, self.heads(), join)
         else:
             j = _join(self, x, 4, join)
             b1, b5, b3 = self.branch1x1(x, j), self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
+            bp = self.branch_pool(x, j)
         b5 = self.branch5x5_2(b5)
         b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(b3))
-        bp = self.branch_pool(x, j)
         return _cat([b1, b5, b3, bp])
 
 
@@ -149,21 +152,20 @@ class InceptionC(nn.Module):
         self.branch_pool = PoolBranch(in_channels, 192, 1)
 
     def heads(self):
-        return [self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1]
+        return [self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
-        if _heads(self, x, self.heads()):
-            j = _join(self, x, 2, join)
-            b1, b7, bd = Fn.conv1x1_group(x, self.heads(), j)
+        if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
+            b1, b7, bd, bp = Fn.conv1x1_group(x, self.heads(), join)
         else:
             j = _join(self, x, 4, join)
             b1, b7, bd = (self.branch1x1(x, j), self.branch7x7_1(x, j),
                           self.branch7x7dbl_1(x, j))
+            bp = self.branch_pool(x, j)
         b7 = self.branch7x7_3(self.branch7x7_2(b7))
         for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
                   self.branch7x7dbl_5):
             bd = m(bd)
-        bp = self.branch_pool(x, j)
         return _cat([b1, b7, bd, bp])
 
 
@@ -208,21 +210,20 @@ class InceptionE(nn.Module):
         self.branch_pool = PoolBranch(in_channels, 192, 1)
 
     def heads(self):
-        return [self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1]
+        return [self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
-        if _heads(self, x, self.heads()):
-            j = _join(self, x, 2, join)
-            b1, b3, bd = Fn.conv1x1_group(x, self.heads(), j)
+        if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
+            b1, b3, bd, bp = Fn.conv1x1_group(x, self.heads(), join)
         else:
             j = _join(self, x, 4, join)
             b1, b3, bd = self.branch1x1(x, j), self.branch3x3_1(x, j), self.branch3x3dbl_1(x, j)
+            bp = self.branch_pool(x, j)
         j3 = _join(self, b3, 2)  # b3 and bd each feed a (1x3) and a (3x1) conv
         b3a, b3b = self.branch3x3_2a(b3, j3), self.branch3x3_2b(b3, j3)
         bd = self.branch3x3dbl_2(bd)
         jd = _join(self, bd, 2)
         bda, bdb = self.branch3x3dbl_3a(bd, jd), self.branch3x3dbl_3b(bd, jd)
-        bp = self.branch_pool(x, j)
         # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
         # as one flat concat, which copies every branch once instead of twice
         return _cat([b1, b3a, b3b, bda, bdb, bp])

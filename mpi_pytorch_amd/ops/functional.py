@@ -308,9 +308,12 @@ class _ConvGroupBNAct(torch.autograd.Function):
     The weights sit back to back in the arena (``_mpa_param_groups``), so the joint weight,
     its bf16 shadow and its gradient are flat views - no copies.  Forward: one conv over
     N = sum N_b columns with BN statistics from its epilogue, then each branch's BN+ReLU
-    reads its channel window of z (strided rows).  Backward: each branch's BN backward
-    writes its window of ONE dz, then one wgrad (x read once, not once per branch) and ONE
-    dgrad (one write of dx instead of a write plus an accumulate pass per extra branch).
+    reads its channel window of z (strided rows).  A member with ``pool_after`` (Inception's
+    pool branch: 1x1 conv and 3x3 average pool commute) average-pools its window first and
+    takes its BN statistics from the pooled values.  Backward: each branch's BN (and pool)
+    backward writes its window of ONE dz, then one wgrad (x read once, not once per branch)
+    and ONE dgrad (one write of dx instead of a write plus an accumulate pass per extra
+    branch).
     Reference: InceptionA/C/D/E branch heads of torchvision inception_v3, reached from
     ``/root/reference/models.py:83-95``."""
 
@@ -323,12 +326,17 @@ class _ConvGroupBNAct(torch.autograd.Function):
         outs, saved, o = [], [], 0
         for m in mods:
             bn, n = m.bn, m.conv.weight.shape[0]
-            y, mean, rstd = k.bn_fwd_train(z[..., o:o + n], stats[:, o:o + n], bn.weight,
-                                           bn.bias, bn.running_mean, bn.running_var,
-                                           bn.momentum_value(), bn.eps, _empty(x), True,
-                                           bn.num_batches_tracked)
+            pool = getattr(m, "pool_after", None)
+            if pool is not None:  # avg-pool the window, BN statistics of the pooled values
+                zin = k.avgpool_fwd(z[..., o:o + n], *pool)
+                st = _empty(x)
+            else:
+                zin, st = z[..., o:o + n], stats[:, o:o + n]
+            y, mean, rstd = k.bn_fwd_train(zin, st, bn.weight, bn.bias, bn.running_mean,
+                                           bn.running_var, bn.momentum_value(), bn.eps,
+                                           _empty(x), True, bn.num_batches_tracked)
             outs.append(y)
-            saved.append((mean, rstd, o, n))
+            saved.append((mean, rstd, o, n, zin if pool is not None else None, pool))
             o += n
         ctx.mods, ctx.join, ctx.saved, ctx.W = mods, join, saved, W
         ctx.in_hw = (x.shape[1], x.shape[2])
@@ -341,11 +349,16 @@ class _ConvGroupBNAct(torch.autograd.Function):
         x, z = ctx.saved_tensors
         k = K(z)
         dz = torch.empty_like(z)
-        for m, (mean, rstd, o, n), dy in zip(ctx.mods, ctx.saved, dys):
+        for m, (mean, rstd, o, n, zp, pool), dy in zip(ctx.mods, ctx.saved, dys):
             gamma, beta = m.bn.weight, m.bn.bias
-            k.bn_bwd(dy.contiguous(), z[..., o:o + n], _empty(dy), mean, rstd, gamma,
-                     _sink(gamma, dy), _sink(beta, dy), True, False, beta,
-                     dx_out=dz[..., o:o + n])
+            if pool is not None:
+                dzp, _g = k.bn_bwd(dy.contiguous(), zp, _empty(dy), mean, rstd, gamma,
+                                   _sink(gamma, dy), _sink(beta, dy), True, False, beta)
+                k.avgpool_bwd(dzp, z.shape[1], z.shape[2], *pool, dx_out=dz[..., o:o + n])
+            else:
+                k.bn_bwd(dy.contiguous(), z[..., o:o + n], _empty(dy), mean, rstd, gamma,
+                         _sink(gamma, dy), _sink(beta, dy), True, False, beta,
+                         dx_out=dz[..., o:o + n])
             _done(gamma, beta)
         ws = [m.conv.weight for m in ctx.mods]
         if ws[0].requires_grad:
@@ -370,6 +383,10 @@ def conv1x1_group_ok(x, mods) -> bool:
     if any(m.conv.kgeom != (1, 1, 0, 0) or m.conv.weight.shape[1:3] != (1, 1) or
            m.conv.bias is not None or not w.requires_grad for m, w in zip(mods, ws)):
         return False
+    if any(getattr(m, "pool_after", None) is not None and
+           tuple(m.pool_after[2:6]) != (1, 1, (m.pool_after[0] - 1) // 2,
+                                        (m.pool_after[1] - 1) // 2) for m in mods):
+        return False  # (a pooled window must keep z's spatial size)
     return a.flat_view(ws, "master") is not None
 
 

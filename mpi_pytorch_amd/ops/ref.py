@@ -295,14 +295,18 @@ def avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
     return _nhwc(y).to(x.dtype)
 
 
-def avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
+def avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, count_include_pad, dx_out=None):
     N, P, Q, C = dy.shape
     xin = torch.zeros(N, C, H, W, device=dy.device, requires_grad=True)
     with torch.enable_grad():
         y = F.avg_pool2d(xin, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
                          count_include_pad=count_include_pad)
         (gx,) = torch.autograd.grad(y, xin, _nchw(_f(dy)))
-    return _nhwc(gx).to(dy.dtype)
+    gx = _nhwc(gx).to(dy.dtype)
+    if dx_out is not None:
+        dx_out.copy_(gx)
+        return dx_out
+    return gx
 
 
 def adaptive_avgpool_fwd(x, oh, ow):

@@ -658,6 +658,24 @@ def test_bn_channel_prefix_and_accumulate(gpu, M, Cc, Ctot):
     assert torch.equal(st[:, 64:], S) and not st[:, :64].any()
 
 
+def test_avgpool_channel_window(gpu):
+    """3x3/s1 average pool of a channel window of a wider buffer (Inception's grouped pool
+    branch) == the pool of a contiguous copy; the backward writes only its window."""
+    torch.manual_seed(22)
+    z = bf(4, 17, 17, 96, dev=gpu)
+    win = z[..., 32:64]
+    y = C().avgpool_fwd(win, 3, 3, 1, 1, 1, 1, False, True)
+    y2 = C().avgpool_fwd(win.contiguous(), 3, 3, 1, 1, 1, 1, False, True)
+    dy = bf(4, 17, 17, 32, dev=gpu)
+    dz = torch.zeros(4, 17, 17, 96, dtype=torch.bfloat16, device=gpu)
+    C().avgpool_bwd(dy, 17, 17, 3, 3, 1, 1, 1, 1, False, True, dx_out=dz[..., 32:64])
+    dx2 = C().avgpool_bwd(dy, 17, 17, 3, 3, 1, 1, 1, 1, False, True)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    assert torch.equal(dz[..., 32:64], dx2)
+    assert not dz[..., :32].any() and not dz[..., 64:].any()
+
+
 def test_bn_stats_from_conv(gpu):
     """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
     torch.manual_seed(5)
