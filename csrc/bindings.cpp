@@ -391,6 +391,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   Tensor st = stats;
   int lds = C;
   if (has(st)) {
+    CHECK_CUDA(st);
     CHECK_F32(st);
     // [2C] contiguous, or a [2, >= C] (view) whose rows hold mean | var: rows stride(0) apart
     if (st.dim() == 2) {
@@ -412,7 +413,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   if (has(res)) TORCH_CHECK(res.numel() == y.numel(), "bn_fwd_train: residual shape");
   Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
   Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
-  mpa::bn_fwd_train(bp(x), fopt(st), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
+  mpa::bn_fwd_train(bp(x), st.data_ptr<float>(), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
                     (float)momentum, (float)eps, bopt(res), relu ? 1 : 0, M, C, bpm(y),
                     mean.data_ptr<float>(), rstd.data_ptr<float>(),
                     (counter && counter->defined() && counter->numel() == 1)
@@ -470,7 +471,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   if (acc) {
     CHECK_CUDA(*gacc);
     CHECK_CONTIG(*gacc);
-    CHECK_F32(*gacc);
+    TORCH_CHECK(gacc->scalar_type() == torch::kFloat32 || gacc->scalar_type() == torch::kBFloat16,
+                "bn_bwd: gradient accumulator must be fp32 or bf16");
     TORCH_CHECK(gacc->numel() / gacc->size(-1) == M && gacc->size(-1) >= C &&
                     gacc->size(-1) % 8 == 0 && !want_g,
                 "bn_bwd: gradient accumulator must be fp32 [..., >= C] with dy's rows");
@@ -493,8 +495,9 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   mpa::bn_bwd(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma), fopt_mut(dgamma),
               fopt_mut(dbeta), M, C, (want_dx && !acc) ? bpm(dx) : nullptr,
               want_g ? bpm(gout) : nullptr, ws.data_ptr<float>(), cur_stream(), fopt(zb),
-              ymask_ptr(ymask, dy), ldx, acc ? gacc->data_ptr<float>() : nullptr,
-              acc ? (int)gacc->size(-1) : 0, lddx);
+              ymask_ptr(ymask, dy), ldx, acc ? (float*)gacc->data_ptr() : nullptr,
+              acc ? (int)gacc->size(-1) : 0, lddx,
+              acc && gacc->scalar_type() == torch::kBFloat16);
   return {dx, gout};
 }
 
@@ -1051,6 +1054,28 @@ void chan_insert(Tensor dst, int64_t off, Tensor src) {
                      cur_stream());
 }
 
+// dense copy of src[..., off:off+cs] (bf16 or fp32)
+Tensor chan_slice(Tensor src, int64_t off, int64_t cs) {
+  CHECK_CUDA(src);
+  CHECK_CONTIG(src);
+  TORCH_CHECK(src.scalar_type() == torch::kBFloat16 || src.scalar_type() == torch::kFloat32,
+              "chan_slice: bf16 or fp32");
+  const int64_t u = src.element_size() / 2;
+  const int64_t ld = src.size(-1);
+  TORCH_CHECK(off >= 0 && cs > 0 && off + cs <= ld && (ld * u) % 8 == 0 && (cs * u) % 8 == 0 &&
+                  (off * u) % 8 == 0, "chan_slice: 16-byte aligned channel runs required");
+  const int64_t rows = src.numel() / ld;
+  TORCH_CHECK(rows * (cs * u / 8) < (int64_t(1) << 31), "chan_slice: too large");
+  const c10::OptionalDeviceGuard gd(device_of(src));
+  std::vector<int64_t> shape(src.sizes().begin(), src.sizes().end());
+  shape.back() = cs;
+  Tensor out = torch::empty(shape, src.options());
+  if (rows > 0)
+    mpa::chan_slice((const mpa::bf16_raw*)src.data_ptr(), (int)(ld * u), (int)(off * u),
+                    (mpa::bf16_raw*)out.data_ptr(), (int)(cs * u), (int)rows, cur_stream());
+  return out;
+}
+
 // bf16 copy of G[..., off:off+C]
 Tensor chan_extract(Tensor g, int64_t off, int64_t cs) {
   CHECK_CUDA(g);
@@ -1187,6 +1212,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
   m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");
   m.def("chan_insert", &chan_insert, "dst[..., off:off+C] = src (bf16 or fp32)");
+  m.def("chan_slice", &chan_slice, "dense copy of src[..., off:off+C] (bf16 or fp32)");
   m.def("preprocess_pil", &preprocess_pil, "PIL-exact bicubic resize + ToTensor + Normalize");
   m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
         py::arg("std"), py::arg("mode"), py::arg("cpad"),

@@ -209,7 +209,8 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
             int ldx = 0,             // x row stride (0: C)
             float* gacc = nullptr,   // non-null: dx ADDED in fp32 into gacc [M][ldg] (dx unused)
             int ldg = 0,
-            int lddx = 0);           // dx row stride (0: C) - a channel window of a wider buffer
+            int lddx = 0,            // dx row stride (0: C) - a channel window of a wider buffer
+            bool gacc_bf16 = false); // gacc holds bf16 (cast the pointer) instead of fp32
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);
@@ -265,6 +266,9 @@ void concat_channels(const bf16_raw* const* xs, const int* chans, int nseg, int 
 // (bf16 activations, or fp32 rows as pairs of units)
 void chan_insert(bf16_raw* dst, int ld, int off, const bf16_raw* src, int cs, int rows,
                  hipStream_t s);
+// dst [rows][cs] <- src [rows][ld] at unit offset off (the inverse of chan_insert)
+void chan_slice(const bf16_raw* src, int ld, int off, bf16_raw* dst, int cs, int rows,
+                hipStream_t s);
 void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, int ctotal,
                     bf16_raw* const* dxs, hipStream_t s);
 

@@ -392,10 +392,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // pass 2: dx = a*g + b + c*x ; optionally write g (residual-branch gradient); block 0
 // folds the sums into dgamma/dbeta.  YM (mask from bn_fwd_train) is a template parameter:
 // a runtime mask pointer slowed every variant of this pass by 10-40 % (its row loads no
-// longer stayed in flight).  x rows have stride ldx.  ACC: dx is ADDED in fp32 into
-// gacc [M][ldg] (a dense block's gradient accumulator; its rows are loaded with the others)
-// instead of being written as bf16.
-template <int UNR, bool YM, bool ACC = false>
+// longer stayed in flight).  x rows have stride ldx.  ACC: dx is ADDED into gacc [M][ldg]
+// (a dense block's gradient accumulator; its rows are loaded with the others) instead of
+// being written as bf16 - ACC 1: fp32 accumulator, ACC 2: bf16 accumulator (one rounding
+// per contribution, as autograd's own bf16 sums; half the accumulator traffic).
+template <int UNR, bool YM, int ACC = 0>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -426,21 +427,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   float msc[8], msh[8];
   if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
   const bool need_x = ACC || dx || zmask;
-  sweep_rows_pl<UNR, ACC ? 5 : 3>(
+  sweep_rows_pl<UNR, ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)>(
       cm, M,
-      [&](int r, uint4 (&v)[ACC ? 5 : 3]) {
+      [&](int r, uint4 (&v)[ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)]) {
         const size_t off = (size_t)r * C + c0;
         v[0] = *(const uint4*)(dy + off);
         if constexpr (YM) v[2].x = ym[off / 8];
         else if (y) v[2] = *(const uint4*)(y + off);
         if (need_x) v[1] = *(const uint4*)(x + (size_t)r * ldx + c0);
-        if constexpr (ACC) {
+        if constexpr (ACC == 1) {
           const uint4* gp = (const uint4*)(gacc + (size_t)r * ldg + c0);
           v[3] = gp[0];
           v[4] = gp[1];
+        } else if constexpr (ACC == 2) {
+          v[3] = *(const uint4*)((const bf16_t*)gacc + (size_t)r * ldg + c0);
         }
       },
-      [&](int r, uint4 (&v)[ACC ? 5 : 3]) {
+      [&](int r, uint4 (&v)[ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)]) {
         const size_t off = (size_t)r * C + c0;
         float g[8];
         unpack8(v[0], g);
@@ -468,7 +471,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
           unpack8(v[1], xv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) xv[j] = a[j] * g[j] + b[j] + cco[j] * xv[j];
-          if constexpr (ACC) {
+          if constexpr (ACC == 2) {
+            float gv[8];
+            unpack8(v[3], gv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] += xv[j];
+            *(uint4*)((bf16_t*)gacc + (size_t)r * ldg + c0) = pack8(gv);
+          } else if constexpr (ACC == 1) {
             const uint32_t gw[8] = {v[3].x, v[3].y, v[3].z, v[3].w, v[4].x, v[4].y, v[4].z, v[4].w};
             uint4 o[2];
             uint32_t* ow = (uint32_t*)o;
@@ -1177,7 +1186,7 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta,
-            const uint8_t* ymask, int ldx, float* gacc, int ldg, int lddx) {
+            const uint8_t* ymask, int ldx, float* gacc, int ldg, int lddx, bool gacc_bf16) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials
   if (ldx <= 0) ldx = C;
   if (lddx <= 0) lddx = C;
@@ -1188,21 +1197,23 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
   BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws, ymask,
             ldx);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
-  if (gacc) {  // dense-block accumulator: dx added into gacc in fp32 (no ymask, no g)
+  if (gacc) {  // dense-block accumulator: dx added into gacc (no ymask, no g)
     const int u = bn_unr();
     const dim3 ga = grid_for(M, C);
-    if (u == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, false, true>), ga, dim3(256), 0, s, dy, x, y,
-                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
-                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
-    else if (u == 2)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, false, true>), ga, dim3(256), 0, s, dy, x, y,
-                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
-                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, true>), ga, dim3(256), 0, s, dy, x, y,
-                         mean, rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,
-                         (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C);
+#define BN_ACC_LAUNCH(U, A)                                                                 \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<U, false, A>), ga, dim3(256), 0, s, dy, x, y, mean, \
+                     rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,             \
+                     (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C)
+    if (gacc_bf16) {
+      if (u == 4) BN_ACC_LAUNCH(4, 2);
+      else if (u == 2) BN_ACC_LAUNCH(2, 2);
+      else BN_ACC_LAUNCH(1, 2);
+    } else {
+      if (u == 4) BN_ACC_LAUNCH(4, 1);
+      else if (u == 2) BN_ACC_LAUNCH(2, 1);
+      else BN_ACC_LAUNCH(1, 1);
+    }
+#undef BN_ACC_LAUNCH
   } else if (ymask)
     BN_LAUNCH_T(bn_bwd_apply_kernel, true, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb, ws,
                 dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx);

@@ -85,6 +85,19 @@ void chan_insert(bf16_raw* dst, int ld, int off, const bf16_raw* src, int cs, in
   hipLaunchKernelGGL(concat_kernel<false>, dim3(gx, 1), dim3(256), 0, s, a, dst, rows);
 }
 
+void chan_slice(const bf16_raw* src, int ld, int off, bf16_raw* dst, int cs, int rows,
+                hipStream_t s) {
+  CatArgs a{};
+  a.cv = ld / 8;
+  a.seg[0] = dst;
+  a.off[0] = off / 8;
+  a.cs[0] = cs / 8;
+  const int64_t work = (int64_t)rows * a.cs[0];
+  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 4096));
+  hipLaunchKernelGGL(concat_kernel<true>, dim3(gx, 1), dim3(256), 0, s, a,
+                     const_cast<bf16_raw*>(src), rows);
+}
+
 void split_channels(const bf16_raw* dy, const int* chans, int nseg, int pixels, int ctotal,
                     bf16_raw* const* dxs, hipStream_t s) {
   launch(true, dxs, chans, nseg, pixels, ctotal, const_cast<bf16_raw*>(dy), s);

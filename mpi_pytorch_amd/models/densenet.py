@@ -38,6 +38,9 @@ class _DenseLayer(nn.Module):
 # MPA_DENSE_BLOCK_GRAD=0: per-layer concats under plain autograd (one split and one
 # elementwise add per earlier feature and layer) instead of the block feature buffer
 _BLOCK_GRAD = os.environ.get("MPA_DENSE_BLOCK_GRAD", "1") == "1"
+# MPA_DENSE_GRAD_BF16=1: the block gradient accumulator in bf16 (one rounding per
+# contribution, as autograd's own bf16 sums of the concat's split) instead of fp32
+_GRAD_BF16 = os.environ.get("MPA_DENSE_GRAD_BF16", "0") == "1"
 
 
 class _DenseBlock(nn.ModuleDict):
@@ -155,11 +158,16 @@ class _DenseBlockGrad(torch.autograd.Function):
         gy = gy.contiguous()
         buf = ctx.buf
         layers = list(ctx.block.values())
-        G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
-        k.chan_accum(G, 0, gy, True)
+        if _GRAD_BF16:
+            G = gy.clone()
+        else:
+            G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
+            k.chan_accum(G, 0, gy, True)
         for i in range(len(ctx.recs) - 1, -1, -1):
             leaf, out, mean, rstd, ci = ctx.recs[i]
-            g_out = k.chan_extract(G, ci, out.shape[-1]).to(out.dtype)
+            g = out.shape[-1]
+            g_out = (k.chan_slice(G, ci, g) if _GRAD_BF16 else
+                     k.chan_extract(G, ci, g).to(out.dtype))
             torch.autograd.backward(out, g_out)
             n1 = layers[i].norm1
             gamma, beta = n1.weight, n1.bias
@@ -169,7 +177,8 @@ class _DenseBlockGrad(torch.autograd.Function):
                          Fn._sink(gamma, dy), Fn._sink(beta, dy), True, False, beta, gacc=G)
             Fn._done(gamma, beta)
             ctx.recs[i] = None
-        dx = k.chan_extract(G, 0, ctx.c0).to(gy.dtype)
+        dx = (k.chan_slice(G, 0, ctx.c0) if _GRAD_BF16 else
+              k.chan_extract(G, 0, ctx.c0).to(gy.dtype))
         ctx.buf = None
         return (dx, None) + (None,) * ctx.nparams
 

@@ -484,6 +484,10 @@ def chan_accum(g, off, src, assign):
         g[..., off:off + cs] += src.float()
 
 
+def chan_slice(src, off, cs):
+    return src[..., off:off + cs].clone()
+
+
 def chan_insert(dst, off, src):
     dst[..., off:off + src.shape[-1]] = src
 

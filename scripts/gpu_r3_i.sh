@@ -15,5 +15,5 @@ b inc_new MPA_X=1 && b inc_nomerge MPA_MERGE_1X1=0 && b inc_old MPA_MERGE_1X1=0 
 ARGS="$ARGS --graph on" b inc_new_graph MPA_X=1
 ARGS="--model densenet --image-size 224 --batch 256"
 b dn_fused MPA_X=1 && b dn_plain MPA_DENSE_BLOCK_GRAD=0 || exit 1
-ARGS="$ARGS --graph on" b dn_fused_graph MPA_X=1
+b dn_fused_g16 MPA_DENSE_GRAD_BF16=1 && ARGS="$ARGS --graph on" b dn_fused_graph MPA_X=1
 exit 0

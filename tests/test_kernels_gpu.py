@@ -648,6 +648,16 @@ def test_bn_channel_prefix_and_accumulate(gpu, M, Cc, Ctot):
     assert torch.equal(G[:, Cc:], G0[:, Cc:])
     want = G0[:, :Cc] + dx.float()
     assert float((G[:, :Cc] - want).abs().max()) <= 1e-2 * float(dx.float().abs().max()) + 1e-6
+    # bf16 accumulator (MPA_DENSE_GRAD_BF16): one bf16 rounding of (G + dx) per element
+    G16 = torch.randn(M, Ctot, device=gpu).to(torch.bfloat16)
+    G16_0 = G16.clone()
+    C().bn_bwd(dy, buf, e, mean, rstd, g, torch.zeros_like(dg), torch.zeros_like(db), True,
+               False, b, gacc=G16)
+    torch.cuda.synchronize()
+    assert torch.equal(G16[:, Cc:], G16_0[:, Cc:])
+    want16 = G16_0[:, :Cc].float() + dx.float()
+    assert float((G16[:, :Cc].float() - want16).abs().max()) <= 2e-2 * float(want16.abs().max())
+    assert torch.equal(C().chan_slice(buf, 8, Cc - 8), buf[:, 8:Cc])
     # chan_insert: bf16 activations and fp32 rows
     dst = torch.zeros(M, Ctot + 32, dtype=torch.bfloat16, device=gpu)
     C().chan_insert(dst, 32, buf)
