@@ -30,9 +30,13 @@ class _DenseLayer(nn.Module):
         x = feats[0] if len(feats) == 1 else Fn.cat_channels(feats)
         return self.tail(self.norm1(x, relu=True))
 
-    def tail(self, x):
-        """conv1 -> norm2 -> relu -> conv2 of the normalised input."""
-        return self.conv2(Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True))
+    def tail(self, x, stats=None, shift=None):
+        """conv1 -> norm2 -> relu -> conv2 of the normalised input; ``stats`` receives the
+        output's [mean | var] from conv2's epilogue."""
+        z = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True)
+        if stats is None:
+            return self.conv2(z)
+        return Fn.conv_act(z, self.conv2, stats=stats, shift=shift)
 
 
 # MPA_DENSE_BLOCK_GRAD=0: per-layer concats under plain autograd (one split and one
@@ -136,12 +140,13 @@ class _DenseBlockGrad(torch.autograd.Function):
                                             Fn._empty(x), True, n1.num_batches_tracked,
                                             channels=ci)
             leaf = y1.requires_grad_(True)
-            with torch.enable_grad():
-                out = layer.tail(leaf)
-            g = out.shape[-1]
-            k.chan_insert(buf, ci, out.detach())
+            g = layer.conv2.weight.shape[0]
+            st = torch.empty(2, g, dtype=torch.float32, device=x.device)
             nxt = layers[li + 1].norm1.running_mean[ci:ci + g] if li + 1 < len(layers) else None
-            k.chan_insert(S, ci, k.bn_stats(out.detach(), Fn._or_empty(nxt, x)))
+            with torch.enable_grad():  # the new feature's statistics from conv2's epilogue
+                out = layer.tail(leaf, st, nxt)
+            k.chan_insert(buf, ci, out.detach())
+            k.chan_insert(S, ci, st)
             recs.append((leaf, out, mean, rstd, ci))
             ci += g
         ctx.block = block
