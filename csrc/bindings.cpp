@@ -353,7 +353,7 @@ static int row_stride(const Tensor& t) {
     TORCH_CHECK(t.size(d) == 1 || t.stride(d) == expect, "bn: rows must be uniformly strided");
     expect *= t.size(d);
   }
-  TORCH_CHECK(ld >= t.size(-1) && ld % 8 == 0, "bn: row stride must be a multiple of 8");
+  TORCH_CHECK(ld >= t.size(-1), "channel window: row stride below the row width");
   return (int)ld;
 }
 
@@ -485,6 +485,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
     CHECK_BF16(*dx_out);
     TORCH_CHECK(dx_out->sizes() == dy.sizes() && !acc, "bn_bwd: dx_out must have dy's shape");
     lddx = row_stride(*dx_out);
+    TORCH_CHECK(lddx % 8 == 0, "bn_bwd: dx_out row stride must be a multiple of 8");
   }
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor dx = (want_dx && !acc) ? (into ? *dx_out : torch::empty_like(dy)) : Tensor();
