@@ -134,20 +134,24 @@ def _timed(step, data, args, world, sync) -> float:
     """Whole-job img/s of ``args.steps`` steps after ``args.warmup`` warm-up steps, bracketed
     like the headline measurement (barrier + device sync, max time over ranks)."""
     from mpi_pytorch_amd.parallel import barrier
+    from mpi_pytorch_amd.engine import steps_without_gc
     for _ in range(max(args.warmup, 2)):
         x, y = data.next()
         step(x, y)
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        x, y = data.next()
-        step(x, y)
-    sync()
-    barrier()
-    sync()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=world.device)
+    # the training driver's loop policy: cyclic GC at the boundaries, not mid-step
+    with steps_without_gc():
+        sync()
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            x, y = data.next()
+            step(x, y)
+        sync()
+        barrier()
+        sync()
+        t1 = time.perf_counter()
+    t = torch.tensor([t1 - t0], dtype=torch.float64, device=world.device)
     if world.world_size > 1:
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

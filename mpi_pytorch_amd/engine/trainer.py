@@ -42,7 +42,7 @@ from ..parallel import (init_world, get_world, barrier, scatter_object, broadcas
                         shard_dataframe, array_split_sizes, replica_checksum)
 from ..parallel.sharding import equal_step_count
 from ..utils.logging import init_logger, MetricsWriter, log_rank_lines
-from .step import build_training
+from .step import build_training, steps_without_gc
 from ..models import input_spec
 
 
@@ -215,20 +215,21 @@ def run_training(cfg: Config) -> dict:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         nimg = 0
-        for x, y in train_loader.epoch(epoch, steps_per_epoch):
-            if use_graph and step._graph is None and x.shape[0] == cfg.BATCH_SIZE:
-                # graph = "on", one GPU: capture the whole step once, replay it after
-                step.capture(x, y)
-            step(x, y)
-            nimg += x.shape[0]
-            gstep += 1
-            if dev.type == "cuda":
-                # progress = the step's kernels COMPLETED on the device, not enqueued
-                ev = torch.cuda.Event()
-                ev.record()
-                dog.beat_on(gstep, ev)
-            else:
-                dog.beat(gstep)
+        with steps_without_gc():  # cyclic GC at the epoch boundary, not mid-step
+            for x, y in train_loader.epoch(epoch, steps_per_epoch):
+                if use_graph and step._graph is None and x.shape[0] == cfg.BATCH_SIZE:
+                    # graph = "on", one GPU: capture the whole step once, replay it after
+                    step.capture(x, y)
+                step(x, y)
+                nimg += x.shape[0]
+                gstep += 1
+                if dev.type == "cuda":
+                    # progress = the step's kernels COMPLETED on the device, not enqueued
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    dog.beat_on(gstep, ev)
+                else:
+                    dog.beat(gstep)
         tr_loss = step.mean_loss()
         if dev.type == "cuda":
             torch.cuda.synchronize()
