@@ -857,6 +857,25 @@ void transpose_krsc(Tensor w, Tensor wt, Tensor seg, int64_t total_tiles,
                       step_inc ? fopt_mut(*step_inc) : nullptr);
 }
 
+void zero_cols_f32(Tensor t, int64_t period, int64_t first, int64_t count) {
+  CHECK_CUDA(t);
+  CHECK_CONTIG(t);
+  CHECK_F32(t);
+  TORCH_CHECK(period > 0 && first >= 0 && count >= 0 && first + count <= period &&
+                  t.numel() % period == 0, "zero_cols_f32: columns outside the row");
+  const c10::OptionalDeviceGuard g(device_of(t));
+  mpa::zero_cols_f32(t.data_ptr<float>(), t.numel() / period, (int)period, (int)first,
+                     (int)count, cur_stream());
+}
+
+void add_bf16_(Tensor a, Tensor b) {
+  CHECK_ACT(a);
+  CHECK_ACT(b);
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() % 8 == 0, "add_bf16_: same size, % 8");
+  const c10::OptionalDeviceGuard g(device_of(a));
+  mpa::add_bf16(bpm(a), bp(b), a.numel(), cur_stream());
+}
+
 void zero_f32(Tensor t) {
   CHECK_CUDA(t);
   CHECK_CONTIG(t);
@@ -1209,6 +1228,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_krsc", &transpose_krsc, py::arg("w"), py::arg("wt"), py::arg("seg"),
         py::arg("total_tiles"), py::arg("step_inc") = py::none());
   m.def("zero_f32", &zero_f32, "t.zero_() on the native path");
+  m.def("zero_cols_f32", &zero_cols_f32, "zero columns [first, first+count) of t as [-1, period]");
+  m.def("add_bf16_", &add_bf16_, "a += b (bf16, fp32 add)");
   m.def("step_inc", &step_inc);
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
   m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");

@@ -288,6 +288,10 @@ void ce_fwd_weighted(const bf16_raw* logits, const int64_t* labels, int B, int N
                      float* lse, hipStream_t s);
 // fp32 t[0:n) = 0 (n % 4 == 0, 16-B aligned); step[0] += 1
 void zero_f32(float* t, int64_t n, hipStream_t s);
+// t as [rows][period] fp32: zero columns [first, first + count)
+void zero_cols_f32(float* t, int64_t rows, int period, int first, int count, hipStream_t s);
+// a += b, bf16 [n] (n % 8 == 0, 16-B aligned)
+void add_bf16(bf16_raw* a, const bf16_raw* b, int64_t n, hipStream_t s);
 void step_inc(float* step, hipStream_t s);
 void argmax_correct(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld,
                     int64_t* count, hipStream_t s);

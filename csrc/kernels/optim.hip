@@ -196,6 +196,47 @@ __global__ __launch_bounds__(256) void zero_f32_kernel(float4* __restrict__ t, i
 
 __global__ void step_inc_kernel(float* step) { *step += 1.f; }
 
+// t viewed as [rows][period] fp32: zero columns [first, first + count) of every row (the
+// pixel-pair stem's weight-gradient column past the kernel, layers.Conv2d.fix_grad)
+__global__ __launch_bounds__(256) void zero_cols_f32_kernel(float* __restrict__ t, int64_t rows,
+                                                            int period, int first, int count) {
+  const int64_t n = rows * count;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / count;
+    t[r * period + first + (int)(i - r * count)] = 0.f;
+  }
+}
+
+// a += b over bf16 vectors (fp32 add, one rounding): two computed gradient contributions
+// of one activation (GradJoin) summed without an ATen elementwise kernel
+__global__ __launch_bounds__(256) void add_bf16_kernel(uint4* __restrict__ a,
+                                                       const uint4* __restrict__ b, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float x[8], y[8];
+    unpack8(a[i], x);
+    unpack8(b[i], y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += y[j];
+    a[i] = pack8(x);
+  }
+}
+
+void zero_cols_f32(float* t, int64_t rows, int period, int first, int count, hipStream_t s) {
+  const int64_t n = rows * count;
+  if (n > 0)
+    hipLaunchKernelGGL(zero_cols_f32_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, s, t,
+                       rows, period, first, count);
+}
+
+void add_bf16(bf16_raw* a, const bf16_raw* b, int64_t n, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  if (n8 > 0)
+    hipLaunchKernelGGL(add_bf16_kernel, dim3(blocks_for((n8 + 1) / 2)), dim3(256), 0, s,
+                       (uint4*)a, (const uint4*)b, n8);
+}
+
 void zero_f32(float* t, int64_t n, hipStream_t s) {
   const int64_t n4 = n / 4;
   if (n4 > 0)

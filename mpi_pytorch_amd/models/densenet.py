@@ -167,7 +167,9 @@ class _DenseBlockGrad(torch.autograd.Function):
         buf = ctx.buf
         layers = list(ctx.block.values())
         if _GRAD_BF16:
-            G = gy.clone()
+            # the block output's gradient comes from its one consumer's BN backward (the
+            # transition / norm5) as a fresh tensor: accumulate into it in place
+            G = gy if (gy._base is None and gy.dtype == torch.bfloat16) else gy.clone()
         else:
             G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
             k.chan_accum(G, 0, gy, True)

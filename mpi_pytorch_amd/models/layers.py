@@ -209,7 +209,8 @@ class Conv2d(nn.Module):
         (second pixel of the last pair) must keep exactly zero weight."""
         kw = self.kernel_size[1]
         if self.pair and kw % 2 and g is not None:
-            g.view(g.shape[0], self.kernel_size[0], self.sp, 8)[:, :, self.sp - 1, 4:].zero_()
+            # g as [K * kh][sp * 8]: the last pair's second pixel = columns (sp-1)*8+4 .. sp*8
+            Fn.K(g).zero_cols_f32(g, self.sp * 8, (self.sp - 1) * 8 + 4, 4)
 
     def extra_repr(self):
         return "{}, {}, kernel_size={}, stride={}, padding={}, bias={}".format(

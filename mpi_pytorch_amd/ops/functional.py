@@ -147,8 +147,9 @@ def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
         acc = t
     elif isinstance(prev, _Deferred):
         acc = prev.run(t)  # the parked dgrad accumulates into t
-    else:
-        acc = prev.add_(t)  # two computed tensors (no zoo model produces this pair)
+    else:  # two computed tensors (Inception's Mixed_7a maxpool + aux-head avg-pool)
+        acc = prev.contiguous()
+        K(acc).add_bf16_(acc, t.contiguous())
     if last:
         return acc
     join.partial = acc
@@ -594,16 +595,16 @@ class _LinearAct(torch.autograd.Function):
 def _padded_grad(dy, width: int):
     """Gradient of a padded layer's output view as a contiguous [B, width] tensor.  The
     cross-entropy backward already returns a view of a [B, width] buffer with zero padding
-    columns - use that buffer (after re-zeroing the padding defensively); anything else
-    is zero-padded by a copy."""
+    columns - use that buffer (ce_bwd wrote its zeros:
+    tests/test_kernels_gpu.py::test_cross_entropy_padded_rows); anything else is
+    zero-padded by a copy."""
     if dy.shape[1] == width:
         return dy.contiguous()
     base = dy._base
     if (base is not None and base.dim() == 2 and tuple(base.shape) == (dy.shape[0], width)
             and base.is_contiguous() and dy.data_ptr() == base.data_ptr()
             and dy.stride() == base.stride()):
-        base[:, dy.shape[1]:].zero_()
-        return base
+        return base  # (ce_bwd wrote zeros into the padding columns)
     return torch.nn.functional.pad(dy, (0, width - dy.shape[1])).contiguous()
 
 

@@ -484,6 +484,14 @@ def chan_accum(g, off, src, assign):
         g[..., off:off + cs] += src.float()
 
 
+def zero_cols_f32(t, period, first, count):
+    t.view(-1, period)[:, first:first + count] = 0
+
+
+def add_bf16_(a, b):
+    a.add_(b)
+
+
 def chan_slice(src, off, cs):
     return src[..., off:off + cs].clone()
 
