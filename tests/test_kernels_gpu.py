@@ -686,6 +686,21 @@ def test_avgpool_channel_window(gpu):
     assert not dz[..., :32].any() and not dz[..., 64:].any()
 
 
+def test_zero_cols_and_bf16_add(gpu):
+    """The two elementwise helpers that keep ATen out of the step: zero a column range of an
+    fp32 [rows][period] view (stem gradient fix-up) and a += b in bf16 (GradJoin)."""
+    t = torch.randn(64 * 7, 32, device=gpu)
+    want = t.clone()
+    want[:, 28:32] = 0
+    C().zero_cols_f32(t, 32, 28, 4)
+    a, b = bf(4096, 24, dev=gpu), bf(4096, 24, dev=gpu)
+    want_ab = (a.float() + b.float()).to(torch.bfloat16)
+    C().add_bf16_(a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(t, want)
+    assert torch.equal(a, want_ab)
+
+
 def test_bn_stats_from_conv(gpu):
     """bn_fwd_train fed by conv epilogue statistics == standalone statistics."""
     torch.manual_seed(5)
