@@ -55,6 +55,8 @@ def loss_fn(out, labels, acc=None):
     return Fn.cross_entropy(out, labels, acc=acc)
 
 
+# MPA_EARLY_HEAD_OPT=0: the classifier's optimizer update waits for the end of backward
+_EARLY_HEAD = os.environ.get("MPA_EARLY_HEAD_OPT", "1") == "1"
 # MPA_STEP_GC=1 leaves Python's cyclic collector running inside the training loop
 _STEP_GC = os.environ.get("MPA_STEP_GC", "0") == "1"
 
@@ -202,6 +204,49 @@ class TrainStep:
         # roctx ranges fwd / bwd / comm_wait / opt around the host enqueue of each phase
         # (rocprofv3 --marker-trace shows them beside the kernels); MPA_ROCTX=1
         self.markers = markers() if os.environ.get("MPA_ROCTX", "0") == "1" else None
+        # early classifier update: the arena's first bucket is the classifier (64,500-class
+        # heads: 75 % of ResNet-18's parameters); once its gradients are final (and, over
+        # RCCL, all-reduced) its optimizer update runs on a side stream under the rest of
+        # the backward instead of after it
+        self._head = self._early_head()
+        self._head_left = 0
+        self._head_launched = False
+        self._side = None
+        if self._head is not None:
+            self._side = torch.cuda.Stream(dev)
+            self.arena.add_listener(self._on_grad)
+
+    def _early_head(self):
+        if not _EARLY_HEAD or self.arena.device.type != "cuda":
+            return None
+        b = self.bucketer
+        if not b.buckets or b.comm_dtype == "bf16" or not hasattr(self.opt, "step_range"):
+            return None
+        from ..models.layers import Linear
+        lin = {id(p) for m in self.model.modules() if isinstance(m, Linear)
+               for p in m.parameters()}
+        lo, hi = b.ranges[0]
+        ps = b.buckets[0]
+        if lo != 0 or not all(id(p) in lin for p in ps) or hi < 0.2 * self.arena.n_train:
+            return None
+        return hi, {id(p) for p in ps}
+
+    def _on_grad(self, p) -> None:
+        """Arena listener: the classifier's last gradient landed (its dgrad was enqueued
+        before - _LinearAct.backward) -> its update goes out on the side stream, after
+        the compute stream's work so far and, with several ranks, after its all-reduce."""
+        if self._head_left <= 0 or id(p) not in self._head[1]:
+            return
+        self._head_left -= 1
+        if self._head_left:
+            return
+        self._side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._side):
+            w = self.bucketer._works[0] if self.bucketer.active else None
+            if w is not None:
+                w.wait()  # (the side stream waits for the bucket's all-reduce)
+            self.opt.step_range(self._head[0])
+        self._head_launched = True
 
     def enable_timers(self) -> StepTimer:
         """Turn on per-phase HIP-event timing of eager steps (GPU only)."""
@@ -217,6 +262,8 @@ class TrainStep:
         if m is not None:
             m.range_push("fwd")
         self.arena.zero_grad()
+        if self._head is not None:
+            self._head_left = len(self._head[1])
         out = self.model(x)
         loss = loss_fn(out, y, acc=self.loss_sum)
         if t is not None:
@@ -236,6 +283,10 @@ class TrainStep:
         if m is not None:
             m.range_pop()
             m.range_push("opt")
+        if self._head_launched:  # the step counter advances after both updates read it
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._head_launched = False
+        self._head_left = 0
         self.opt.step()
         if t is not None:
             t.mark(4)

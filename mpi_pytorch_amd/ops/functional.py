@@ -583,12 +583,15 @@ class _LinearAct(torch.autograd.Function):
         k = K(dy)
         dy = _padded_grad(dy, w.shape[0])
         g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
+        # dgrad before the weight gradient's notify: once every gradient of a classifier is
+        # final, its optimizer update may start on a side stream (TrainStep's early head
+        # update) - nothing may read the old bf16 weight after that point
+        dx = (k.linear_dgrad(g, weight_of(w), weight_t_of(w)) if ctx.needs_input_grad[0]
+              else None)
         _done(b)
         if w.requires_grad:
             k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
             _done(w)
-        dx = (k.linear_dgrad(g, weight_of(w), weight_t_of(w)) if ctx.needs_input_grad[0]
-              else None)
         return dx, None, None, None, None
 
 

@@ -44,6 +44,7 @@ class _FlatOptimizer:
         dev = arena.device
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
         self.grad_scale = 1.0
+        self._done_lo = 0  # [0, _done_lo) already updated this step (step_range)
         self.param_groups = [self._group_defaults()]
         self.param_groups[0]["params"] = self.params
 
@@ -61,6 +62,17 @@ class _FlatOptimizer:
 
     def _group_defaults(self) -> Dict:
         raise NotImplementedError
+
+    def _update(self, lo: int, hi: int) -> None:
+        raise NotImplementedError
+
+    def step_range(self, hi: int) -> None:
+        """Update the arena prefix [0, hi) now (its gradients are final); the next
+        ``step()`` updates only the rest and then advances the step counter, so both
+        launches use the same step.  (TrainStep's early classifier update.)"""
+        if hi > 0:
+            self._update(0, hi)
+            self._done_lo = hi
 
     def _kernel(self):
         return Fn.K(self.arena.master)
@@ -114,15 +126,22 @@ class FusedAdam(_FlatOptimizer):
                  differentiable=False, fused=None)
         return d
 
-    def step(self) -> None:
+    def _update(self, lo: int, hi: int) -> None:
         g = self.param_groups[0]
-        if self.arena.n_train == 0:
-            return
         b1, b2 = g["betas"]
-        self._kernel().adam_step(self.arena.train_master(), self.arena.grad[:self.arena.n_train],
-                                 self.exp_avg, self.exp_avg_sq, self._shadow(), self.step_t,
+        sh = self._shadow()
+        self._kernel().adam_step(self.arena.master[lo:hi], self.arena.grad[lo:hi],
+                                 self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi],
+                                 sh[lo:hi] if sh.numel() else sh, self.step_t,
                                  float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                                  float(g["weight_decay"]), float(self.grad_scale))
+
+    def step(self) -> None:
+        if self.arena.n_train == 0:
+            return
+        lo, self._done_lo = self._done_lo, 0
+        if lo < self.arena.n_train:
+            self._update(lo, self.arena.n_train)
         self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):
@@ -153,15 +172,21 @@ class FusedSGD(_FlatOptimizer):
         d.update(maximize=False, foreach=None, differentiable=False, fused=None)
         return d
 
-    def step(self) -> None:
+    def _update(self, lo: int, hi: int) -> None:
         g = self.param_groups[0]
+        sh = self._shadow()
+        self._kernel().sgd_step(self.arena.master[lo:hi], self.arena.grad[lo:hi],
+                                self.momentum_buffer[lo:hi], sh[lo:hi] if sh.numel() else sh,
+                                self.step_t, float(g["lr"]), float(g["momentum"]),
+                                float(g["dampening"]), float(g["weight_decay"]),
+                                bool(g["nesterov"]), float(self.grad_scale))
+
+    def step(self) -> None:
         if self.arena.n_train == 0:
             return
-        self._kernel().sgd_step(self.arena.train_master(), self.arena.grad[:self.arena.n_train],
-                                self.momentum_buffer, self._shadow(), self.step_t,
-                                float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
-                                float(g["weight_decay"]), bool(g["nesterov"]),
-                                float(self.grad_scale))
+        lo, self._done_lo = self._done_lo, 0
+        if lo < self.arena.n_train:
+            self._update(lo, self.arena.n_train)
         self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):

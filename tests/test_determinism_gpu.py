@@ -77,3 +77,34 @@ def test_graph_replays_bitwise_equal_eager(det):
     assert bad.numel() == 0, "first diverging replay %d: %s vs %s" % (
         int(bad[0]), float(got[bad[0]]), float(ref[bad[0]]))
     assert torch.equal(model._mpa_arena.master, ref_master)
+
+
+def test_early_head_update_bitwise(det):
+    """The classifier's optimizer update issued on a side stream as soon as its gradients
+    are final (TrainStep._early_head) == the whole update after backward, bitwise; also
+    under HIP-graph replay (the side stream forks from and joins the captured stream)."""
+    gpu = det
+    nc = 64500  # the headline head: 75 % of ResNet-18's parameters
+    x, y = _batch(gpu, B=16, hw=32, nc=nc)
+    outs = []
+    for early in (True, False):
+        model, opt, step = _train(gpu, nc=nc)
+        assert step._head is not None
+        if not early:
+            step._head = None
+        losses = [step(x, y).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        outs.append((torch.stack(losses).cpu(), model._mpa_arena.master.cpu().clone(),
+                     opt.exp_avg_sq.cpu().clone(), float(opt.step_t)))
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(torch.as_tensor(u), torch.as_tensor(v))
+    model, opt, step = _train(gpu, nc=nc)
+    ref = torch.stack([step(x, y).clone() for _ in range(12)])[2:]
+    torch.cuda.synchronize()
+    ref_master = model._mpa_arena.master.clone()
+    del model, opt, step
+    model, opt, step = _train(gpu, nc=nc)
+    assert step.capture(x, y, warmup=2)
+    got = torch.stack([step(x, y).clone() for _ in range(10)])
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref) and torch.equal(model._mpa_arena.master, ref_master)
