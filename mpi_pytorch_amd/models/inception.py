@@ -252,6 +252,10 @@ class Inception3(nn.Module):
         self.aux_logits = aux_logits
         self.transform_input = False
         self.cross_join = True
+        # Conv2d_2b -> maxpool1 and Conv2d_4a -> maxpool2 as the fused conv + BN + ReLU +
+        # max-pool op (one pass over the conv output, as the ResNet / DenseNet stems);
+        # utils/parity.py turns it off to hook the two BasicConv2d units
+        self.fuse_stem_pools = True
         self.Conv2d_1a_3x3 = BasicConv2d(3, 32, 3, stride=2)
         self.Conv2d_2a_3x3 = BasicConv2d(32, 32, 3)
         self.Conv2d_2b_3x3 = BasicConv2d(32, 64, 3, padding=1)
@@ -280,10 +284,17 @@ class Inception3(nn.Module):
                 m.init_(lambda w, s=std: nn.init.trunc_normal_(w, 0.0, s, -2, 2))
 
     def forward(self, x):
-        for m in (self.Conv2d_1a_3x3, self.Conv2d_2a_3x3, self.Conv2d_2b_3x3, self.maxpool1,
-                  self.Conv2d_3b_1x1, self.Conv2d_4a_3x3, self.maxpool2, self.Mixed_5b,
-                  self.Mixed_5c, self.Mixed_5d, self.Mixed_6a, self.Mixed_6b, self.Mixed_6c,
-                  self.Mixed_6d, self.Mixed_6e):
+        x = self.Conv2d_2a_3x3(self.Conv2d_1a_3x3(x))
+        if self.fuse_stem_pools:
+            x = Fn.conv_bn_relu_maxpool(x, self.Conv2d_2b_3x3.conv, self.Conv2d_2b_3x3.bn,
+                                        self.maxpool1)
+            x = Fn.conv_bn_relu_maxpool(self.Conv2d_3b_1x1(x), self.Conv2d_4a_3x3.conv,
+                                        self.Conv2d_4a_3x3.bn, self.maxpool2)
+        else:
+            x = self.maxpool1(self.Conv2d_2b_3x3(x))
+            x = self.maxpool2(self.Conv2d_4a_3x3(self.Conv2d_3b_1x1(x)))
+        for m in (self.Mixed_5b, self.Mixed_5c, self.Mixed_5d, self.Mixed_6a, self.Mixed_6b,
+                  self.Mixed_6c, self.Mixed_6d, self.Mixed_6e):
             x = m(x)
         aux = None
         if self.AuxLogits is not None and self.training:

@@ -164,6 +164,9 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
     fused = getattr(model_gpu, "fused_blocks", None)
     if fused is not None:
         model_gpu.fused_blocks = False
+    pools = getattr(model_gpu, "fuse_stem_pools", None)
+    if pools is not None:
+        model_gpu.fuse_stem_pools = False
     # Inception's grouped 1x1 branch heads: one GEMM, not the BasicConv2d units
     grouped = [m for m in model_gpu.modules() if hasattr(m, "heads")]
     for m in grouped:
@@ -184,6 +187,8 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             model_gpu.cross_join = cross
         if fused is not None:
             model_gpu.fused_blocks = fused
+        if pools is not None:
+            model_gpu.fuse_stem_pools = pools
         for m in grouped:
             m.__dict__.pop("merge_1x1", None)
     g_gpu = arena.grad.detach().cpu()

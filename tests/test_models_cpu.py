@@ -366,3 +366,28 @@ def test_densenet_feature_buffer_blocks_equal_plain_autograd():
     assert torch.allclose(o1, o2, atol=1e-5) and torch.allclose(e1, e2, atol=1e-5)
     assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
+def test_inception_fused_stem_pools_equal_modules():
+    """Conv2d_2b -> maxpool1 and Conv2d_4a -> maxpool2 as fused conv+BN+ReLU+max-pool ops ==
+    the BasicConv2d + MaxPool2d modules (fp32, CPU): logits, running stats, gradients."""
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("inception", 10, torch.device("cpu"), World(), 1e-3)
+    model.dropout.p = 0.0
+    a = model._mpa_arena
+    x = torch.randn(2, 299, 299, 8) * (torch.arange(8) < 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    for fused in (True, False):
+        model.fuse_stem_pools = fused
+        model.load_state_dict(sd)
+        a.zero_grad()
+        out = model(x)
+        loss_fn(out, y).backward()
+        res.append((out[0].detach(), a.grad.clone(),
+                    [v.clone() for k, v in model.state_dict().items() if "running" in k]))
+    (o1, g1, r1), (o2, g2, r2) = res
+    assert torch.allclose(o1, o2, atol=1e-5)
+    assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
