@@ -222,6 +222,8 @@ class TrainStep:
         b = self.bucketer
         if not b.buckets or b.comm_dtype == "bf16" or not hasattr(self.opt, "step_range"):
             return None
+        if b.active and not b.overlap:  # (the head's all-reduce would only start at finish)
+            return None
         from ..models.layers import Linear
         lin = {id(p) for m in self.model.modules() if isinstance(m, Linear)
                for p in m.parameters()}
