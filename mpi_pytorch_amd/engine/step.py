@@ -55,8 +55,11 @@ def loss_fn(out, labels, acc=None):
     return Fn.cross_entropy(out, labels, acc=acc)
 
 
-# MPA_EARLY_HEAD_OPT=0: the classifier's optimizer update waits for the end of backward
-_EARLY_HEAD = os.environ.get("MPA_EARLY_HEAD_OPT", "1") == "1"
+# MPA_EARLY_HEAD_OPT=1: the classifier's optimizer update runs on a side stream under the
+# rest of the backward.  Off by default: on one MI355X the concurrent streaming update slows
+# the backward it overlaps by more than it hides (same-box A/B, profiles/early_head_ab_r3.txt:
+# ResNet-18 b1024 48.0k vs 48.2k, b128 28.1k vs 28.7k, Inception 6.99k vs 7.09k img/s).
+_EARLY_HEAD = os.environ.get("MPA_EARLY_HEAD_OPT", "0") == "1"
 # MPA_STEP_GC=1 leaves Python's cyclic collector running inside the training loop
 _STEP_GC = os.environ.get("MPA_STEP_GC", "0") == "1"
 

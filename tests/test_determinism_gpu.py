@@ -87,6 +87,17 @@ def test_early_head_update_bitwise(det):
     nc = 64500  # the headline head: 75 % of ResNet-18's parameters
     x, y = _batch(gpu, B=16, hw=32, nc=nc)
     outs = []
+    import mpi_pytorch_amd.engine.step as S
+    old = S._EARLY_HEAD
+    S._EARLY_HEAD = True  # (opt-in feature: exercised here)
+    try:
+        _early_head_runs(gpu, x, y, nc)
+    finally:
+        S._EARLY_HEAD = old
+
+
+def _early_head_runs(gpu, x, y, nc):
+    outs = []
     for early in (True, False):
         model, opt, step = _train(gpu, nc=nc)
         assert step._head is not None
