@@ -20,6 +20,7 @@
 //
 // Markers: roctx ranges so rocprofv3 --marker-trace shows step phases.
 #include "runtime.h"
+#include "ring_core.h"
 
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -47,18 +48,22 @@ struct Slot {
   uint8_t* img = nullptr;    // pinned [B,H,W,3]
   int64_t* labels = nullptr; // pinned [B]
   int32_t* ext = nullptr;    // pinned [B,2] (h, w) of each image inside the pitch
-  int64_t batch_index = -1;
-  int count = 0;             // valid images (the last batch of a manifest may be short)
 };
 
+static int checked_depth(int depth) {
+  TORCH_CHECK(depth >= 2, "BatchRing depth must be >= 2");
+  return depth;
+}
+
+// Torch-facing ring: pinned slot payloads + the producers' fill functions around the
+// scheduling core (ring_core.h: slot states, batch-order hand-off, stop).
 class BatchRing {
  public:
   BatchRing(int batch, int H, int W, int64_t num_classes, int depth, int threads, uint64_t seed,
             int64_t start_index, int64_t stride, bool synthetic)
-      : B_(batch), H_(H), W_(W), nc_(num_classes), seed_(seed), next_index_(start_index),
-        next_consume_(start_index), stride_(stride), synthetic_(synthetic),
-        threads_(std::max(1, threads)) {
-    TORCH_CHECK(depth >= 2, "BatchRing depth must be >= 2");
+      : B_(batch), H_(H), W_(W), nc_(num_classes), seed_(seed), synthetic_(synthetic),
+        threads_(std::max(1, threads)),
+        core_(checked_depth(depth), start_index, stride) {
     TORCH_CHECK(batch >= 1 && H >= 1 && W >= 1 && stride >= 1, "BatchRing: bad geometry");
     slots_.resize(depth);
     const size_t img_bytes = (size_t)B_ * H_ * W_ * 3;
@@ -74,28 +79,17 @@ class BatchRing {
                   "hipHostMalloc failed");
       s.ext = (int32_t*)p;
     }
-    for (int i = 0; i < depth; ++i) empty_.push_back(i);
-    if (synthetic_) {
-      for (int t = 0; t < threads_; ++t) workers_.emplace_back([this] { produce(); });
-    }
+    if (synthetic_)
+      core_.run_producers(threads_, [this](int id, int64_t b) { return fill_synthetic(id, b); });
   }
 
   ~BatchRing() { stop(); free_all(); }
 
-  void stop() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stopping_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : workers_)
-      if (t.joinable()) t.join();
-    workers_.clear();
-  }
+  void stop() { core_.stop(); }
 
   // window mode: image i = tex[offs[i,0] : +H, offs[i,1] : +W], label labels[i]
   void set_window_source(torch::Tensor tex, torch::Tensor offs, torch::Tensor labels) {
-    TORCH_CHECK(!synthetic_ && workers_.empty() && !window_, "BatchRing: source already set");
+    TORCH_CHECK(!synthetic_ && !core_.producing() && !window_, "BatchRing: source already set");
     TORCH_CHECK(tex.device().is_cpu() && tex.scalar_type() == torch::kUInt8 && tex.dim() == 3 &&
                     tex.size(2) == 3 && tex.is_contiguous(),
                 "set_window_source: tex must be a contiguous CPU uint8 [TH, TW, 3]");
@@ -115,40 +109,33 @@ class BatchRing {
     wlabels_ = labels;
     n_items_ = offs.size(0);
     window_ = true;
-    for (int t = 0; t < threads_; ++t) workers_.emplace_back([this] { produce(); });
+    core_.run_producers(threads_, [this](int id, int64_t b) { return fill_window(id, b); },
+                        num_batches());
   }
 
   int64_t num_batches() const { return window_ ? (n_items_ + B_ - 1) / B_ : -1; }
 
   // consumer: block until the NEXT batch (in batch-index order) is filled; releases the GIL
   std::tuple<int, torch::Tensor, torch::Tensor, int64_t> acquire() {
-    int id = -1;
+    int id;
     {
       pybind11::gil_scoped_release nogil;
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return find_ready() >= 0 || stopping_; });
-      id = find_ready();
-      TORCH_CHECK(id >= 0, "BatchRing stopped");
-      for (auto it = ready_.begin(); it != ready_.end(); ++it)
-        if (*it == id) { ready_.erase(it); break; }
-      next_consume_ += stride_;
+      id = core_.acquire();
     }
-    return {id, view_img(id), view_labels(id), slots_[id].batch_index};
+    TORCH_CHECK(id >= 0, "BatchRing stopped");
+    return {id, view_img(id), view_labels(id), core_.batch_index(id)};
   }
 
   // (valid image count, pinned int32 [B,2] extents) of an acquired slot
   std::tuple<int, torch::Tensor> info(int id) {
     TORCH_CHECK(id >= 0 && id < (int)slots_.size(), "BatchRing: bad slot");
     auto opt = torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true);
-    return {slots_[id].count, torch::from_blob(slots_[id].ext, {B_, 2}, opt)};
+    return {core_.count(id), torch::from_blob(slots_[id].ext, {B_, 2}, opt)};
   }
 
   void release(int id) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      empty_.push_back(id);
-    }
-    cv_.notify_all();
+    TORCH_CHECK(id >= 0 && id < (int)slots_.size(), "BatchRing: bad slot");
+    core_.release(id);
   }
 
   // external producer API (real-data mode): grab an empty slot, fill it, commit
@@ -156,12 +143,9 @@ class BatchRing {
     int id;
     {
       pybind11::gil_scoped_release nogil;
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return !empty_.empty() || stopping_; });
-      TORCH_CHECK(!empty_.empty(), "BatchRing stopped");
-      id = empty_.front();
-      empty_.pop_front();
+      id = core_.acquire_empty();
     }
+    TORCH_CHECK(id >= 0, "BatchRing stopped");
     auto opt = torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true);
     return {id, view_img(id), view_labels(id), torch::from_blob(slots_[id].ext, {B_, 2}, opt)};
   }
@@ -173,24 +157,12 @@ class BatchRing {
       TORCH_CHECK(slots_[id].ext[2 * b] >= 1 && slots_[id].ext[2 * b] <= H_ &&
                       slots_[id].ext[2 * b + 1] >= 1 && slots_[id].ext[2 * b + 1] <= W_,
                   "BatchRing.commit: image ", b, " extent outside the slot pitch");
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      slots_[id].batch_index = batch_index;
-      slots_[id].count = count;
-      ready_.push_back(id);
-    }
-    cv_.notify_all();
+    core_.commit(id, batch_index, count);
   }
 
-  int depth() const { return (int)slots_.size(); }
+  int depth() const { return core_.depth(); }
 
  private:
-  int find_ready() const {  // the slot holding batch next_consume_, or -1
-    for (int id : ready_)
-      if (slots_[id].batch_index == next_consume_) return id;
-    return -1;
-  }
-
   torch::Tensor view_img(int id) {
     auto opt = torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true);
     return torch::from_blob(slots_[id].img, {B_, H_, W_, 3}, opt);
@@ -207,7 +179,8 @@ class BatchRing {
     }
   }
 
-  void fill_synthetic(Slot& s, int64_t bidx) {
+  int fill_synthetic(int id, int64_t bidx) {
+    Slot& s = slots_[id];
     const size_t per_img = (size_t)H_ * W_ * 3;
     for (int b = 0; b < B_; ++b) {
       uint64_t st = seed_ * 0x100000001B3ull ^ ((uint64_t)bidx * B_ + b);
@@ -222,11 +195,11 @@ class BatchRing {
       for (size_t i = n64 * 8; i < per_img; ++i) s.img[per_img * b + i] = (uint8_t)(x >> (i & 7));
     }
     full_extents(s);
-    s.batch_index = bidx;
-    s.count = B_;
+    return B_;
   }
 
-  void fill_window(Slot& s, int64_t bidx) {
+  int fill_window(int id, int64_t bidx) {
+    Slot& s = slots_[id];
     const int64_t i0 = bidx * B_;
     const int n = (int)std::min<int64_t>(B_, n_items_ - i0);
     const uint8_t* tex = tex_.data_ptr<uint8_t>();
@@ -242,32 +215,7 @@ class BatchRing {
       s.labels[b] = lab[i0 + b];
     }
     full_extents(s);
-    s.batch_index = bidx;
-    s.count = n;
-  }
-
-  void produce() {
-    while (true) {
-      int id;
-      int64_t bidx;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return !empty_.empty() || stopping_; });
-        if (stopping_) return;
-        bidx = next_index_;
-        if (window_ && bidx * B_ >= n_items_) return;  // manifest exhausted
-        id = empty_.front();
-        empty_.pop_front();
-        next_index_ += stride_;
-      }
-      if (window_) fill_window(slots_[id], bidx);
-      else fill_synthetic(slots_[id], bidx);
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        ready_.push_back(id);
-      }
-      cv_.notify_all();
-    }
+    return n;
   }
 
   void free_all() {
@@ -284,18 +232,13 @@ class BatchRing {
   int B_, H_, W_;
   int64_t nc_;
   uint64_t seed_;
-  int64_t next_index_, next_consume_, stride_;
   bool synthetic_;
   int threads_;
   bool window_ = false;
   torch::Tensor tex_, offs_, wlabels_;
   int64_t n_items_ = 0;
   std::vector<Slot> slots_;
-  std::deque<int> empty_, ready_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stopping_ = false;
-  std::vector<std::thread> workers_;
+  RingCore core_;  // last: its producer threads stop (destructor) before the slots go
 };
 
 }  // namespace

@@ -35,6 +35,9 @@ def launch(nprocs: int, cmd, env_extra=None, timeout: float = 0.0) -> int:
                     "LOCAL_WORLD_SIZE": str(nprocs), "MASTER_ADDR": "127.0.0.1",
                     "MASTER_PORT": str(port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if env.get("MPA_DEBUG_SYNC") == "1":  # serialized-kernel debug mode (ops/_ext.py)
+            env.setdefault("AMD_SERIALIZE_KERNEL", "3")
+            env.setdefault("HIP_LAUNCH_BLOCKING", "1")
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         if env_extra:

@@ -16,6 +16,42 @@ import os
 
 _ext = None
 _err = None
+_synced = None
+
+# Serialized-kernel debug mode: MPA_DEBUG_SYNC=1 makes every native op
+# synchronize the device when it returns, so an asynchronous HIP fault is raised at the op
+# that launched it, with its name.  For kernel-level serialization export
+# AMD_SERIALIZE_KERNEL=3 and HIP_LAUNCH_BLOCKING=1 as well (read at HIP init; the launcher
+# does it for every rank when MPA_DEBUG_SYNC=1 is set).
+_DEBUG_SYNC = os.environ.get("MPA_DEBUG_SYNC", "0") == "1"
+
+
+class SyncedExt:
+    """The native module with a device sync + error attribution after every op call."""
+
+    def __init__(self, mod, sync=None):
+        self._mod = mod
+        self._sync = sync
+
+    def __getattr__(self, name):
+        f = getattr(self._mod, name)
+        if not callable(f) or isinstance(f, type):
+            return f  # (classes such as BatchRing pass through)
+
+        def call(*args, **kwargs):
+            out = f(*args, **kwargs)
+            try:
+                if self._sync is not None:
+                    self._sync()
+                else:
+                    import torch
+                    torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError("native op '%s' failed on the device: %s" % (name, e)) from e
+            return out
+
+        call.__name__ = name
+        return call
 
 
 def load():
@@ -43,8 +79,15 @@ def available() -> bool:
 
 
 def ext():
-    """Return the native module; raises loudly when it is missing."""
-    return load()
+    """Return the native module; raises loudly when it is missing.  Under MPA_DEBUG_SYNC=1
+    the module is wrapped so every op synchronizes and names itself on a device error."""
+    global _synced
+    m = load()
+    if not _DEBUG_SYNC:
+        return m
+    if _synced is None:
+        _synced = SyncedExt(m)
+    return _synced
 
 
 def so_path() -> str:
