@@ -80,7 +80,7 @@ struct EpiIn {
   uint2 a[4][4];
 };
 
-template <int EPI>
+template <int EPI, int NJ>
 __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m0, int n0,
                                             int wave, int lane) {
   if constexpr (!(EPI & (EP_BETA | EP_BNRED))) {
@@ -95,7 +95,7 @@ __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m
       const int m = min(m0 + wave * 64 + i * 16 + (lane & 15), p.M - 1);  // rows >= M: unused
       const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) {
+      for (int jn = 0; jn < NJ; ++jn) {
         if constexpr (EPI & EP_BNRED) {
           in.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
         } else {
@@ -212,7 +212,9 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
   }
 }
 
-template <bool WRES, int EPI, bool FULL, bool PROD>
+// NJ: 16-column fragment groups per wave (4: 64-wide column tiles; 2: N == 32 - the weight
+// image's upper 32 columns are zero-filled DMAs and never read, no MFMA touches them)
+template <bool WRES, int EPI, bool FULL, bool PROD, int NJ>
 __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
   constexpr int HB_DPT = WRES ? 2 : 4;  // next-item DMAs per tap (no producer waves)
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   // per-column epilogue operands of the block's 64 columns: bias (or BN mean) and stats
   // shift (or BN rstd), parked in LDS rather than in 32 VGPRs held through every MFMA; the
   // first item's barrier publishes them
-  if (tid < HB_BN) {
+  if (tid < 16 * NJ) {
     const float* bsrc = (EPI & EP_BNRED) ? p.ep_mean : p.bias;
     const float* ssrc = (EPI & EP_BNRED) ? p.ep_rstd : p.stats_shift;
     const float b = bsrc ? bsrc[n0 + tid] : 0.f, sv = ssrc ? ssrc[n0 + tid] : 0.f;
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       for (int i = 0; i < 4; ++i)
         a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
+      for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
     ld(0, 0);
 #pragma unroll
@@ -419,7 +421,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jn = 0; jn < 4; ++jn)
+        for (int jn = 0; jn < NJ; ++jn)
           acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
                               (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
       if constexpr (!PROD) {
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       } else {
         wait_all_barrier();
       }
-      if (cc == max(CC - 2, 0)) epi_preload<EPI>(p, ein, m0, n0, wave, lane);
+      if (cc == max(CC - 2, 0)) epi_preload<EPI, NJ>(p, ein, m0, n0, wave, lane);
       const bool more = k + 1 < nitems;
       const int cc1 = cc + 1 == CC ? 0 : cc + 1;
       if constexpr (!PROD) {
@@ -483,7 +485,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0, std::true_type{});
+          for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0, std::true_type{});
       }
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
       // after its top barrier, which every wave passes only once done reading stage st)
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
+      for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
   }
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
 }
@@ -557,12 +559,15 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 
   // ---- DMA lanes.  dy: instruction j of this wave = rows 8 (4 wave + j) + lane/8 of the
   // tile (k-step image (row >> 5), mn_off<64> swizzle at the source)
+  // (K % 64 == 32: the last k partition's upper 32 k read zeros - kok - and are not stored)
   uint32_t drow[4];
+  bool kok[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = 8 * (4 * wave + j) + (lane >> 3);
     const int chunk = (lane & 7) ^ mn_swz<64>(row & 31);
     drow[j] = ((uint32_t)row * K + k0 + chunk * 8) * 2;  // + pixel0 * K * 2 per tile
+    kok[j] = k0 + chunk * 8 < K;
   }
   // halo: instruction j = pixels 16 (7 wave + j) + lane/4 of the image; chunk 1 of the
   // partition is the same lanes with the descriptor base 64 B further
@@ -578,7 +583,9 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   // buffer descriptors, once: dy and the partition's two 32-channel halo chunks
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, h.dy_bytes);
   const __amdgpu_buffer_rsrc_t rx0 = make_rsrc(p.x, h.x_bytes);
-  const __amdgpu_buffer_rsrc_t rx1 = make_rsrc((const char*)p.x + 64, h.x_bytes);
+  // (C % 64 == 32: the last channel partition's second chunk is an empty buffer: zeros)
+  const __amdgpu_buffer_rsrc_t rx1 =
+      make_rsrc((const char*)p.x + 64, c0 + 32 < C ? h.x_bytes : 0u);
   uint32_t hv[HW_HIW], dv[4];
   // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
   const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
@@ -605,7 +612,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = 8 * (4 * wave + j) + (lane >> 3);
-      dv[j] = m0 + row < M ? drow[j] + (uint32_t)m0 * K * 2 : 0x80000000u;
+      dv[j] = (m0 + row < M && kok[j]) ? drow[j] + (uint32_t)m0 * K * 2 : 0x80000000u;
     }
     const int mlast = M - 1 - img0 * HW;
 #pragma unroll
@@ -703,12 +710,14 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   // c = c0 + 16 wave + 4 (lane/16) .. +3
   const int64_t ncols = 9 * (int64_t)C;
   float* dst = p.slab + (int64_t)z * K * ncols;
+  const int cw = c0 + 16 * wave;  // this wave's 16 channels (wave-uniform validity)
 #pragma unroll
   for (int km = 0; km < 4; ++km) {
     const int kk = k0 + 16 * km + li;
+    if (k0 + 16 * km >= K || cw >= C) continue;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
-      *(f32x4*)(dst + (int64_t)kk * ncols + t * C + c0 + 16 * wave + 4 * g) = acc[km][t];
+      *(f32x4*)(dst + (int64_t)kk * ncols + t * C + cw + 4 * g) = acc[km][t];
   }
 }
 
@@ -778,7 +787,10 @@ static int halo_epi(const IGemmArgs& a) {
 
 bool conv3_halo_ok(const IGemmArgs& a) {
   if (!g_halo || a.nphase > 0 || a.stap || a.T != 9 || a.Uh != 1 || a.Uw != 1) return false;
-  if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.N % HB_BN != 0 || a.M <= 0)
+  if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.M <= 0) return false;
+  // 64-wide column tiles, or one 32-wide tile (DenseNet's growth-rate convs) in the
+  // flavours instantiated for it
+  if (a.N % HB_BN != 0 && !(a.N == 32 && (halo_epi(a) == 0 || halo_epi(a) == EP_STATS)))
     return false;
   // dense [M][ldc] output (stride-1 geometry), 32-bit element offsets in the epilogue
   if (a.dH != a.oH || a.dW != a.oW || a.Uoh != 1 || a.Uow != 1 || a.Poh != 0 || a.Pow != 0)
@@ -818,27 +830,37 @@ static const bool g_halo_prod = [] {
   return !(e && atoi(e) == 0);
 }();
 
-template <int EPI, bool PROD>
+template <int EPI, bool PROD, int NJ>
 static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                           hipStream_t s) {
   const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
   const dim3 blk(PROD ? 512 : 256);
   if (wres && full)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, PROD>), dim3(grid), blk, 0, s, a, h);
-  else if (wres)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false, PROD>), dim3(grid), blk, 0, s, a, h);
-  else if (full)
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true, PROD>), dim3(grid), blk, 0, s, a, h);
-  else
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false, PROD>), dim3(grid), blk, 0, s, a,
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, PROD, NJ>), dim3(grid), blk, 0, s, a,
                        h);
+  else if (wres)
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false, PROD, NJ>), dim3(grid), blk, 0, s, a,
+                       h);
+  else if (full)
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true, PROD, NJ>), dim3(grid), blk, 0, s, a,
+                       h);
+  else
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false, PROD, NJ>), dim3(grid), blk, 0, s,
+                       a, h);
 }
 
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  if (g_halo_prod) launch_halo_k<EPI, true>(wres, grid, a, h, s);
-  else launch_halo_k<EPI, false>(wres, grid, a, h, s);
+  if (g_halo_prod) launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
+  else launch_halo_k<EPI, false, 4>(wres, grid, a, h, s);
+}
+
+// N == 32 (plain and statistics epilogues only; producer-wave blocks)
+template <int EPI>
+static void launch_halo32(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
+                          hipStream_t s) {
+  launch_halo_k<EPI, true, 2>(wres, grid, a, h, s);
 }
 
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
@@ -868,6 +890,11 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
   const bool wres = g_halo_wres && a.tiles_n == 1 && h.cc <= 2;
+  if (a.N == 32) {
+    if (halo_epi(a) == EP_STATS) launch_halo32<EP_STATS>(wres, grid, a, h, s);
+    else launch_halo32<0>(wres, grid, a, h, s);
+    return grid;
+  }
   switch (halo_epi(a)) {
     case 0: launch_halo<0>(wres, grid, a, h, s); break;
     case EP_BETA: launch_halo<EP_BETA>(wres, grid, a, h, s); break;
@@ -885,7 +912,8 @@ static int halo_wgrad_pitch(int W) { return (W + 2 + 15) / 16 * 16; }
 static bool halo_wgrad_geom(const WGradArgs& a) {
   if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1)
     return false;
-  if (a.P != a.H || a.Q != a.W || a.C % 64 != 0 || a.Kout % 64 != 0) return false;
+  // 64 x 64 partitions; a 32-wide remainder in either dimension is zero-filled
+  if (a.P != a.H || a.Q != a.W || a.C % 32 != 0 || a.Kout % 32 != 0) return false;
   const int64_t HW = (int64_t)a.H * a.W;
   if (a.Mpix % HW != 0 || HW + HW_BM >= 65536 || a.W + 2 > 255) return false;
   if ((int64_t)a.Mpix * a.C * 2 >= (1ll << 31) || (int64_t)a.Mpix * a.Kout * 2 >= (1ll << 31))
@@ -896,7 +924,7 @@ static bool halo_wgrad_geom(const WGradArgs& a) {
 }
 
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols) {
-  if (Ncols % 9 != 0 || (Ncols / 9) % 64 != 0 || Kout % 64 != 0) return 0;
+  if (Ncols % 9 != 0 || (Ncols / 9) % 32 != 0 || Kout % 32 != 0) return 0;
   return (int64_t)HALO_MAX_ROWS * 64 * 64 * 9;  // <= 256 blocks x one 64x9x64 partition
 }
 
@@ -916,8 +944,8 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.mag_h1 = magic(a.H + 1);
   h.mag_hw = magic(a.H * a.W);
   h.tiles_m = (a.Mpix + HW_BM - 1) / HW_BM;
-  h.kparts = a.Kout / 64;
-  h.parts = h.kparts * (a.C / 64);
+  h.kparts = (a.Kout + 63) / 64;
+  h.parts = h.kparts * ((a.C + 63) / 64);
   const int G = std::min(active_cus(), HALO_MAX_ROWS);
   h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);

@@ -456,47 +456,72 @@ __global__ __launch_bounds__(256) void wgrad_reduce_scalar_kernel(const float* _
 }
 
 // ----------------------------------------------------------- split-K finalize (fp32->bf16)
-__global__ void splitk_finalize_kernel(const float* __restrict__ ws, int S,
-                                       bf16_t* __restrict__ out, int M, int N,
-                                       const float* __restrict__ bias, int relu,
-                                       float* __restrict__ slab,
-                                       const float* __restrict__ shift,
-                                       float* __restrict__ sums, int beta) {
-  // sums the S split partials [S][M][N] (+ the existing output when beta); one block per
-  // 64 columns x (rows strided by
-  // gridDim.y); statistics go to the per-block-row slab [gridDim.y][2N]
+// Sums the S split partials [S][M][N] (+ the existing output when beta).  A block owns CW
+// columns (CW = 32 for 32-wide GEMMs, so no lane idles) and 256 / CW rows per pass, rows
+// strided by gridDim.y; two rows per thread are in flight per pass (the S loads of both are
+// independent).  Statistics go to the per-block-row slab [gridDim.y][2N].  (The round-2
+// form, 64 columns x 4 rows per block and at most 64 block rows, left a 32-wide 12,544-row
+// finalize at 59 us: 64 blocks, half their lanes idle, one dependent row at a time.)
+template <int CW>
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(
+    const float* __restrict__ ws, int S, bf16_t* __restrict__ out, int M, int N,
+    const float* __restrict__ bias, int relu, float* __restrict__ slab,
+    const float* __restrict__ shift, float* __restrict__ sums, int beta) {
+  constexpr int RP = 256 / CW;
   __shared__ float red[2][256];
-  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r0 = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int n = blockIdx.x * CW + (threadIdx.x % CW);
+  const int r0 = blockIdx.y * RP + threadIdx.x / CW;
+  const int rstep = gridDim.y * RP;
   const size_t MN = (size_t)M * N;
   float s = 0.f, q = 0.f;
   const float b = (bias && n < N) ? bias[n] : 0.f;
   const float k = (shift && n < N) ? shift[n] : 0.f;
+  auto fin = [&](int m, float v) {
+    if (beta) v += bf2f(out[(size_t)m * N + n]);
+    if (relu) v = fmaxf(v, 0.f);
+    const bf16_t o = f2bf(v);
+    out[(size_t)m * N + n] = o;
+    const float rv = bf2f(o) - k;
+    s += rv;
+    q += rv * rv;
+  };
   if (n < N) {
-    for (int m = r0; m < M; m += gridDim.y * 4) {
+    int m = r0;
+    for (; m + rstep < M; m += 2 * rstep) {
+      float v0 = b, v1 = b;
+      const float* w0 = ws + (size_t)m * N + n;
+      const float* w1 = w0 + (size_t)rstep * N;
+      for (int z = 0; z < S; ++z) {
+        v0 += w0[z * MN];
+        v1 += w1[z * MN];
+      }
+      fin(m, v0);
+      fin(m + rstep, v1);
+    }
+    if (m < M) {
       float v = b;
       for (int z = 0; z < S; ++z) v += ws[z * MN + (size_t)m * N + n];
-      if (beta) v += bf2f(out[(size_t)m * N + n]);
-      if (relu) v = fmaxf(v, 0.f);
-      const bf16_t o = f2bf(v);
-      out[(size_t)m * N + n] = o;
-      const float rv = bf2f(o) - k;
-      s += rv;
-      q += rv * rv;
+      fin(m, v);
     }
   }
   if (slab) {
-    if (blockIdx.y == 0 && threadIdx.x < 64 && n < N) {  // start value of the slab reduction
+    if (blockIdx.y == 0 && threadIdx.x < CW && n < N) {  // start value of the slab reduction
       sums[n] = 0.f;
       sums[N + n] = 0.f;
     }
     red[0][threadIdx.x] = s;
     red[1][threadIdx.x] = q;
     __syncthreads();
-    if (threadIdx.x < 64 && n < N) {
+    if (threadIdx.x < CW && n < N) {
       const int t = threadIdx.x;
-      slab[(size_t)blockIdx.y * 2 * N + n] = red[0][t] + red[0][t + 64] + red[0][t + 128] + red[0][t + 192];
-      slab[(size_t)blockIdx.y * 2 * N + N + n] = red[1][t] + red[1][t + 64] + red[1][t + 128] + red[1][t + 192];
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < RP; ++r) {
+        a0 += red[0][t + r * CW];
+        a1 += red[1][t + r * CW];
+      }
+      slab[(size_t)blockIdx.y * 2 * N + n] = a0;
+      slab[(size_t)blockIdx.y * 2 * N + N + n] = a1;
     }
   }
 }
@@ -726,8 +751,8 @@ int64_t igemm_ws_floats(int M, int N, int Ktot) {
   return best;
 }
 
-// statistics slab rows: one per 128-row M-tile (the smallest BM of any plan) or per
-// splitk_finalize block row (<= 64), then the [2][N] sums
+// statistics slab rows: one per 128-row M-tile (the smallest BM of any plan), per halo /
+// stem block or per splitk_finalize block row (<= slab_rows_max), then the [2][N] sums
 static int64_t slab_rows_max(int M) {
   return std::max<int64_t>((M + 127) / 128, std::max(64, HALO_MAX_ROWS));
 }
@@ -851,11 +876,20 @@ static void rows_run_plan(IGemmArgs a, bool bkc, int vw, float* ws, float* slab,
   }
   int slab_rows = tiles_m;
   if (splits > 1) {
-    const int gy = std::min(64, (a.M + 3) / 4);
-    dim3 grid((a.N + 63) / 64, gy);
-    hipLaunchKernelGGL(splitk_finalize_kernel, grid, dim3(256), 0, s, ws, splits,
-                       (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
-                       stats ? slab : (float*)nullptr, a.stats_shift, sums, a.beta);
+    // ~512+ blocks (two rows in flight per thread), at most one slab row per block row
+    const int cw = a.N <= 32 ? 32 : 64, rp = 256 / cw, gx = (a.N + cw - 1) / cw;
+    const int gy = (int)std::min<int64_t>(slab_rows_max(a.M),
+                                          std::max(1, std::min((a.M + 2 * rp - 1) / (2 * rp),
+                                                               (1024 + gx - 1) / gx)));
+    dim3 grid(gx, gy);
+    if (cw == 32)
+      hipLaunchKernelGGL(splitk_finalize_kernel<32>, grid, dim3(256), 0, s, ws, splits,
+                         (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
+                         stats ? slab : (float*)nullptr, a.stats_shift, sums, a.beta);
+    else
+      hipLaunchKernelGGL(splitk_finalize_kernel<64>, grid, dim3(256), 0, s, ws, splits,
+                         (bf16_t*)final_out, a.M, a.N, a.bias, a.relu,
+                         stats ? slab : (float*)nullptr, a.stats_shift, sums, a.beta);
     slab_rows = gy;
   }
   if (stats) slab_stats(slab, slab_rows, a.N, a.stats_shift, a.M, sums, stats, s);
@@ -1119,7 +1153,7 @@ static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   if (igemm_engine() >= 1 && conv3_halo_wgrad_ok(a)) {  // 3x3 / stride 1: halo-staged
     const int z = conv3_halo_wgrad(a, s);
-    const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 64 == 0: float4 rows
+    const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 32 == 0: float4 rows
     const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
                        a.overwrite);

@@ -220,6 +220,10 @@ HALO_CASES = [
     (3, 17, 17, 128, 64),    # halo wgrad at pitch 32, odd W, tiles across images
     (52, 14, 14, 256, 512),  # 320 tiles on 256 persistent blocks (two rounds), ragged last tile
     (25, 56, 56, 64, 64),    # resident weights, 307 tiles
+    (2, 28, 28, 128, 32),    # DenseNet growth conv: 32-wide halo forward, zero-padded wgrad k
+    (3, 7, 7, 128, 32),      # DenseNet block 4: 32-wide, tiles across many 7x7 images
+    (2, 17, 17, 32, 64),     # 32-channel wgrad partition (second halo chunk empty)
+    (2, 9, 9, 96, 96),       # wgrad K and C with a 32-wide remainder partition
 ]
 
 
@@ -356,6 +360,33 @@ def test_gemm_autotune(gpu, case):
         assert rel(b, a) < 1e-3 and torch.equal(b, c)
     table = C().igemm_tuned_table()
     assert "rows" in table and "wgrad" in table
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, C, K: 1x1 convs deep enough in K to split (split-K finalize, 32 / 64 columns)
+    (64, 7, 7, 544, 32),
+    (16, 5, 5, 768, 96),
+    (4, 7, 7, 1024, 512),
+])
+def test_splitk_finalize(gpu, case):
+    """Split-K forward (fp32 partial slab + splitk_finalize: sum, bias, ReLU, bf16, shifted
+    BN statistics) == the fp32 oracle, for 32-column and wider GEMMs."""
+    torch.manual_seed(27)
+    N, H, W, Cc, K = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    w = bf(K, 1, 1, Cc, dev=gpu, scale=1.0 / math.sqrt(Cc))
+    e = torch.empty(0, device=gpu)
+    b = torch.randn(K, device=gpu)
+    shift = torch.randn(K, device=gpu) * 0.1
+    for bias, relu, stats in ((e, False, True), (b, True, False), (b, False, True)):
+        st = torch.zeros(2, K, device=gpu) if stats else e
+        y = C().conv_fwd(x, w, bias, 1, 1, 0, 0, relu, st, shift if stats else e)
+        str_ = torch.zeros(2, K, device=gpu) if stats else e
+        yr = ref.conv_fwd(x, w, bias, 1, 1, 0, 0, relu, str_, shift if stats else e)
+        torch.cuda.synchronize()
+        assert rel(y, yr) < 2e-2
+        if stats:
+            assert rel(st, str_) < 2e-2
 
 
 def test_conv_halo_repeatable(gpu):
