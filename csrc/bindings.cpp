@@ -267,6 +267,91 @@ std::vector<Tensor> conv_dgrad_bnred(Tensor dy, Tensor w, int64_t H, int64_t W, 
   return {dx, r.sums};
 }
 
+// DenseNet norm1 -> conv1 (1x1, stride 1) backward hand-off: conv1's dgrad with the ReLU(BN)
+// mask, the (sum g, sum g * xhat) reduction and G[..., :Ci] += gamma*rstd * g in ONE GEMM
+// epilogue (ep_gacc); no dy tensor is written.  zbuf / G: the block feature buffer and
+// block gradient, [..., Ctot] with the same row stride; returns the sums [2 * Ci] for
+// bn_defer_step.
+Tensor conv_dgrad_bnred_gacc(Tensor dz, Tensor w, Tensor wt, Tensor zbuf, Tensor mean,
+                             Tensor rstd, Tensor gamma, Tensor beta, Tensor G) {
+  CHECK_ACT(dz);
+  CHECK_ACT(w);
+  CHECK_ACT(wt);
+  CHECK_ACT(zbuf);
+  CHECK_CUDA(G);
+  CHECK_CONTIG(G);
+  const int N = dz.size(0), H = dz.size(1), W = dz.size(2), K = dz.size(3);
+  const int Ci = w.size(3);
+  TORCH_CHECK(w.size(0) == K && w.size(1) == 1 && w.size(2) == 1 && wt.numel() == w.numel(),
+              "conv_dgrad_bnred_gacc: 1x1 weight [K][1][1][Ci] and its transpose");
+  TORCH_CHECK(zbuf.is_contiguous() && zbuf.dim() == 4 && zbuf.size(0) == N &&
+                  zbuf.size(1) == H && zbuf.size(2) == W && zbuf.size(3) >= Ci,
+              "conv_dgrad_bnred_gacc: zbuf must be the contiguous [N, H, W, >= Ci] buffer");
+  TORCH_CHECK(G.sizes() == zbuf.sizes(), "conv_dgrad_bnred_gacc: G must have zbuf's shape");
+  TORCH_CHECK(G.scalar_type() == torch::kBFloat16 || G.scalar_type() == torch::kFloat32,
+              "conv_dgrad_bnred_gacc: G must be bf16 or fp32");
+  TORCH_CHECK(conv_bnred_ok(K, Ci) && Ci % 8 == 0 && zbuf.size(3) % 8 == 0,
+              "conv_dgrad_bnred_gacc: unsupported shape/engine");
+  for (const Tensor* t : {&mean, &rstd, &gamma, &beta}) {
+    CHECK_CUDA(*t);
+    CHECK_F32(*t);
+    TORCH_CHECK(t->numel() >= Ci, "conv_dgrad_bnred_gacc: per-channel vector size");
+  }
+  const c10::OptionalDeviceGuard g(device_of(dz));
+  mpa::IGemmArgs a{};
+  a.A = bp(dz); a.aH = H; a.aW = W; a.aC = K;
+  a.oH = H; a.oW = W; a.M = N * H * W;
+  a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+  a.T = 1;
+  a.taps.dh[0] = 0; a.taps.dw[0] = 0; a.taps.bt[0] = 0;
+  a.Ktot = K;
+  a.B = bp(wt); a.N = Ci; a.RS = 1; a.ldb = K; a.b_tapmap = 1;
+  a.C = G.data_ptr(); a.ldc = (int)zbuf.size(3);
+  a.dH = H; a.dW = W; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
+  a.ep_z = bp(zbuf);
+  a.ep_y = nullptr;
+  a.ep_mean = mean.data_ptr<float>();
+  a.ep_rstd = rstd.data_ptr<float>();
+  a.ep_gamma = gamma.data_ptr<float>();
+  a.ep_beta = beta.data_ptr<float>();
+  a.ep_gacc = G.data_ptr();
+  a.ep_gacc_f32 = G.scalar_type() == torch::kFloat32 ? 1 : 0;
+  Tensor sums = torch::empty({2 * Ci}, dz.options().dtype(torch::kFloat32));
+  Tensor slab = torch::empty({mpa::igemm_bnred_slab_floats(a.M, Ci, 1)},
+                             dz.options().dtype(torch::kFloat32));
+  mpa::igemm_rows_dgrad_bnred(a, 8, true, slab.data_ptr<float>(), sums.data_ptr<float>(),
+                              cur_stream());
+  return sums;
+}
+
+// see mpa::bn_defer_step (bn.hip): fold layer sums into the block's deferred-correction
+// table k12 [2, Ctot] and apply the final correction to G's channels [s0, Ci)
+void bn_defer_step(Tensor sums, Tensor gamma, Tensor mean, Tensor rstd, int64_t s0, Tensor k12,
+                   Tensor dgamma, Tensor dbeta, Tensor G, Tensor x) {
+  CHECK_CUDA(G);
+  CHECK_CONTIG(G);
+  CHECK_ACT(x);
+  CHECK_F32(k12);
+  CHECK_CONTIG(k12);
+  const int Ci = sums.numel() / 2;
+  const int ctot = x.size(-1);
+  const int M = x.numel() / ctot;
+  TORCH_CHECK(x.is_contiguous() && G.sizes() == x.sizes() && k12.numel() == 2 * ctot,
+              "bn_defer_step: G / x / k12 shapes");
+  TORCH_CHECK(s0 >= 0 && s0 < Ci && Ci <= ctot && (Ci - s0) % 8 == 0 &&
+                  256 % ((Ci - s0) / 8) == 0,
+              "bn_defer_step: slice [s0, Ci) must be 8-channel groups dividing 256");
+  for (const Tensor* t : {&gamma, &mean, &rstd}) {
+    CHECK_F32(*t);
+    TORCH_CHECK(t->numel() >= Ci, "bn_defer_step: per-channel vector size");
+  }
+  const c10::OptionalDeviceGuard g(device_of(x));
+  mpa::bn_defer_step(sums.data_ptr<float>(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), Ci, (int)s0, M, k12.data_ptr<float>(), ctot,
+                     fopt_mut(dgamma), fopt_mut(dbeta), G.data_ptr(),
+                     G.scalar_type() == torch::kFloat32, ctot, bp(x), ctot, cur_stream());
+}
+
 std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd,
                                  Tensor gamma, Tensor dgamma, Tensor dbeta, Tensor sums,
                                  bool want_dx, bool want_g) {
@@ -1174,6 +1259,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("overwrite") = false,
         "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
+  m.def("conv_dgrad_bnred_gacc", &conv_dgrad_bnred_gacc);
+  m.def("bn_defer_step", &bn_defer_step);
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, py::arg("dy"), py::arg("w"), py::arg("H"),
         py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt"),
         py::arg("z"), py::arg("y"), py::arg("mean"), py::arg("rstd"),

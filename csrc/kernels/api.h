@@ -86,6 +86,12 @@ struct IGemmArgs {
   // gamma*rstd, beta))) > 0) and never reads y; the implicit GEMM always reads ep_y
   const float* ep_gamma;
   const float* ep_beta;
+  // ep_gacc (rows kernel, with ep_bnred and ep_gamma / ep_beta): no output is written;
+  // instead gamma*rstd * g is ADDED into ep_gacc (same row stride ldc as ep_z; bf16 with
+  // one rounding, or fp32 when ep_gacc_f32) - the DenseNet block-gradient form whose
+  // per-channel BN-backward corrections are deferred (bn_defer_fold / bn_defer_apply)
+  void* ep_gacc;
+  int ep_gacc_f32;
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
                           // columns (dw .. dw+3, weight taps bt .. bt+ns-1), Ktot = 32 * T
   int beta;               // 1: accumulate, C = acc + C (bf16 read-add-write, one rounding):
@@ -177,6 +183,11 @@ void igemm_set_stem(int on);  // MPA_STEM_DIRECT=0 disables (A/B, tests)
 // ws: float workspace of bn_ws_floats(M, C) elements (per-block partial-sum slab)
 int64_t bn_ws_floats(int M, int C);
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
+// deferred BN-backward corrections of a dense block (bn.hip, bn_defer_step_kernel); the host
+// guarantees (Ci - s0) % 8 == 0 and 256 % ((Ci - s0) / 8) == 0
+void bn_defer_step(const float* sums, const float* gamma, const float* mean, const float* rstd,
+                   int Ci, int s0, int M, float* k12, int ldk, float* dgamma, float* dbeta,
+                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, hipStream_t s);
 // MPA_DETERMINISTIC: fixed-order cross-block reductions, no timing-based tile autotuning
 void set_deterministic(int on);
 bool deterministic();

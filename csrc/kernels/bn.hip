@@ -1151,6 +1151,73 @@ static bool pool_k3s2p1_even(const PoolGeom& g) {
          g.H == 2 * g.P && g.W == 2 * g.Q;
 }
 
+// --------------------------------------- deferred BN-backward corrections (DenseNet)
+// A dense block's norm1 layers all normalise channel c with the SAME batch statistics (the
+// block table, taken once when the feature is produced), so their backward terms
+//   dx_i = a_i g_i - a_i mean(g_i) - a_i mean(g_i xhat) xhat,   a_i = gamma_i rstd
+// split into a per-layer local part a_i g_i - added into the block gradient G by the
+// consumer conv's dgrad epilogue (ep_gacc) - and per-channel constants that SUM over layers:
+//   K1[c] = -sum_i a_i mean(g_i),  K2[c] = -sum_i a_i mean(g_i xhat),
+// applied once per channel as G += K1 + K2 xhat when the channel's gradient is complete.
+// One launch after layer i's dgrad: block 0 folds layer i's sums into K (channels < s0) and
+// the (gamma, beta) gradients; every block applies the now-final correction (K plus layer
+// i's own term) to the channels [s0, Ci) no later layer reads (layer i-1's 32 outputs, or
+// the block input for i = 0).  Thread = 8 channels x rows strided by the grid.
+template <bool F32>
+__global__ __launch_bounds__(256) void bn_defer_step_kernel(
+    const float* __restrict__ sums, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ rstd, int Ci, int s0, int M,
+    float invM, float* __restrict__ k12, int ldk, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, void* __restrict__ G, int ldg, const bf16_t* __restrict__ x,
+    int ldx) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < Ci; c += 256) {
+      const float sg = sums[c], sgx = sums[Ci + c];
+      if (dgamma) dgamma[c] += sgx;
+      if (dbeta) dbeta[c] += sg;
+      if (c < s0) {
+        const float a = gamma[c] * rstd[c];
+        k12[c] -= a * sg * invM;
+        k12[ldk + c] -= a * sgx * invM;
+      }
+    }
+  }
+  const int cg = (Ci - s0) / 8, rpp = 256 / cg;  // host: 256 % cg == 0
+  const int c0 = s0 + (threadIdx.x % cg) * 8;
+  float k1[8], k2[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float a = gamma[c] * rstd[c];
+    k1[j] = k12[c] - a * sums[c] * invM;
+    k2[j] = k12[ldk + c] - a * sums[Ci + c] * invM;
+    mu[j] = mean[c];
+    rs[j] = rstd[c];
+  }
+  for (int m = blockIdx.x * rpp + (int)threadIdx.x / cg; m < M; m += gridDim.x * rpp) {
+    float xv[8];
+    unpack8(*(const uint4*)(x + (size_t)m * ldx + c0), xv);
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = k1[j] + k2[j] * ((xv[j] - mu[j]) * rs[j]);
+    if constexpr (F32) {
+      f32x4* gp = (f32x4*)((float*)G + (size_t)m * ldg + c0);
+      f32x4 g0 = gp[0], g1 = gp[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { g0[j] += d[j]; g1[j] += d[4 + j]; }
+      gp[0] = g0;
+      gp[1] = g1;
+    } else {
+      uint4* gp = (uint4*)((bf16_t*)G + (size_t)m * ldg + c0);
+      float gv[8];
+      unpack8(*gp, gv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] += d[j];
+      *gp = pack8(gv);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------ launchers
 void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,
               hipStream_t s) {
@@ -1317,4 +1384,21 @@ void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, c
                      mean, rstd, gamma, beta, ws, dgamma, dbeta, C, g, dz);
 }
 
+}  // namespace mpa
+
+namespace mpa {
+void bn_defer_step(const float* sums, const float* gamma, const float* mean, const float* rstd,
+                   int Ci, int s0, int M, float* k12, int ldk, float* dgamma, float* dbeta,
+                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, hipStream_t s) {
+  const int cg = (Ci - s0) / 8, rpp = 256 / cg;
+  const int blocks = std::max(1, std::min(2048, (M + rpp - 1) / rpp));
+  if (g_f32)
+    hipLaunchKernelGGL(bn_defer_step_kernel<true>, dim3(blocks), dim3(256), 0, s, sums, gamma,
+                       mean, rstd, Ci, s0, M, 1.f / (float)M, k12, ldk, dgamma, dbeta, G, ldg,
+                       (const bf16_t*)x, ldx);
+  else
+    hipLaunchKernelGGL(bn_defer_step_kernel<false>, dim3(blocks), dim3(256), 0, s, sums, gamma,
+                       mean, rstd, Ci, s0, M, 1.f / (float)M, k12, ldk, dgamma, dbeta, G, ldg,
+                       (const bf16_t*)x, ldx);
+}
 }  // namespace mpa

@@ -214,6 +214,10 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
     // bias / stats shift; in BN-reduce mode the same registers carry mean / rstd
     f32x4 bias[TN], shift[TN];
     const bool bnred = p.ep_bnred != 0;
+    // z-mask affine (bnred with gamma / beta and no y): bn_fwd_train's scale / shift
+    const bool zmask = bnred && !p.ep_y && p.ep_gamma && p.ep_beta;
+    const bool gacc = bnred && p.ep_gacc != nullptr;
+    f32x4 msc[TN], msh[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -228,6 +232,16 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
       if (ssrc) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? ssrc[n + r] : 0.f;
+      }
+      msc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      msh[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (zmask) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sc = (n + r < p.N) ? p.ep_gamma[n + r] * shift[j][r] : 0.f;
+          msc[j][r] = sc;
+          msh[j][r] = (n + r < p.N) ? __builtin_fmaf(-bias[j][r], sc, p.ep_beta[n + r]) : 0.f;
+        }
       }
     }
     size_t orows[TM];
@@ -250,14 +264,27 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
     // accumulate mode: issue every read of the existing output up front (one exposed
     // latency for the tile instead of one per fragment)
     uint2 oldv[TM][TN];
-    if (p.beta) {
+    if (p.beta || (gacc && !p.ep_gacc_f32)) {
+      const bf16_t* src = gacc ? (const bf16_t*)p.ep_gacc : out;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wcol0 + j * 16 + nl;
-          oldv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(out + orows[i] + n)
+          oldv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(src + orows[i] + n)
                                                  : make_uint2(0u, 0u);
+        }
+    }
+    // BN-backward reduction: z of every fragment up front as well
+    uint2 zv[TM][TN];
+    if (bnred) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wcol0 + j * 16 + nl;
+          zv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(p.ep_z + orows[i] + n)
+                                              : make_uint2(0u, 0u);
         }
     }
 #pragma unroll
@@ -273,10 +300,14 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
           // dy (bf16-rounded like the unfused path) masked by ReLU(y); x_hat from z
           bool live[4] = {true, true, true, true};
           if (mok && n + 3 < p.N) {
-            const uint2 zz = *(const uint2*)(p.ep_z + orow + n);
+            const uint2 zz = zv[i][j];
             zr[0] = bf2f(zz.x & 0xffff); zr[1] = bf2f(zz.x >> 16);
             zr[2] = bf2f(zz.y & 0xffff); zr[3] = bf2f(zz.y >> 16);
-            if (p.ep_y) {
+            if (zmask) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                live[r] = bf2f(f2bf(__builtin_fmaf(zr[r], msc[j][r], msh[j][r]))) > 0.f;
+            } else if (p.ep_y) {
               const uint2 yy = *(const uint2*)(p.ep_y + orow + n);
               live[0] = (yy.x & 0x7fff) != 0 && !(yy.x & 0x8000);
               live[1] = ((yy.x >> 16) & 0x7fff) != 0 && !(yy.x & 0x80000000u);
@@ -288,7 +319,10 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
             for (int r = 0; r < 4; ++r) {
               if (n + r < p.N) {
                 zr[r] = bf2f(p.ep_z[orow + n + r]);
-                if (p.ep_y) live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
+                if (zmask)
+                  live[r] = bf2f(f2bf(__builtin_fmaf(zr[r], msc[j][r], msh[j][r]))) > 0.f;
+                else if (p.ep_y)
+                  live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
               }
             }
           }
@@ -318,7 +352,32 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
           }
         }
         const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-        if (mok) {
+        if (mok && gacc) {
+          // block-gradient accumulate: G += gamma*rstd * g (the deferred BN-backward form)
+          if (p.ep_gacc_f32) {
+            float* gp = (float*)p.ep_gacc + orow + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) gp[r] += msc[j][r] * v[r];
+          } else if (n + 3 < p.N) {
+            const uint2 oo = oldv[i][j];
+            const float a0 = bf2f(oo.x & 0xffff) + msc[j][0] * v[0];
+            const float a1 = bf2f(oo.x >> 16) + msc[j][1] * v[1];
+            const float a2 = bf2f(oo.y & 0xffff) + msc[j][2] * v[2];
+            const float a3 = bf2f(oo.y >> 16) + msc[j][3] * v[3];
+            *(uint2*)((bf16_t*)p.ep_gacc + orow + n) = make_uint2(pack2(a0, a1), pack2(a2, a3));
+          } else {
+            bf16_t* gp = (bf16_t*)p.ep_gacc + orow + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) gp[r] = f2bf(bf2f(gp[r]) + msc[j][r] * v[r]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // BN backward's reduction, as below
+            s[j][r] += v[r];
+            q[j][r] += v[r] * (zr[r] - bias[j][r]) * shift[j][r];
+          }
+        } else if (mok) {
           if (n + 3 < p.N) {
             *(uint2*)(out + orow + n) = make_uint2(lo, hi);
           } else {

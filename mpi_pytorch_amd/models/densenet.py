@@ -30,10 +30,11 @@ class _DenseLayer(nn.Module):
         x = feats[0] if len(feats) == 1 else Fn.cat_channels(feats)
         return self.tail(self.norm1(x, relu=True))
 
-    def tail(self, x, stats=None, shift=None):
+    def tail(self, x, stats=None, shift=None, link=None):
         """conv1 -> norm2 -> relu -> conv2 of the normalised input; ``stats`` receives the
-        output's [mean | var] from conv2's epilogue."""
-        z = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True)
+        output's [mean | var] from conv2's epilogue; ``link`` (Fn.BNLink) describes norm1 for
+        the fused conv1-dgrad / norm1-backward hand-off."""
+        z = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True, link_in=link)
         if stats is None:
             return self.conv2(z)
         return Fn.conv_act(z, self.conv2, stats=stats, shift=shift)
@@ -48,6 +49,17 @@ _BLOCK_GRAD = os.environ.get("MPA_DENSE_BLOCK_GRAD", "1") == "1"
 # 6652 img/s vs 6413 with an fp32 accumulator (twice the accumulator traffic).
 # MPA_DENSE_GRAD_BF16=0 keeps the accumulator in fp32.
 _GRAD_BF16 = os.environ.get("MPA_DENSE_GRAD_BF16", "1") == "1"
+# Deferred norm1 backward (see _DenseBlockGrad.backward): conv1's dgrad epilogue adds
+# gamma*rstd * g into the block gradient and reduces (sum g, sum g*xhat); the per-channel
+# rest of every layer's BN backward is summed and applied once per channel.  No dy
+# tensor, no norm1 reduce / apply passes over the O(L^2) channel prefixes.
+# MPA_DENSE_DEFER=0 restores the per-layer bn_bwd(gacc=G).
+_DEFER = os.environ.get("MPA_DENSE_DEFER", "0") == "1"
+
+
+def _defer_ok(c0: int, growth: int) -> bool:
+    """bn_defer_step's slice shapes: 8-channel groups whose count divides 256."""
+    return all(n % 8 == 0 and 256 % (n // 8) == 0 for n in (c0, growth))
 
 
 class _DenseBlock(nn.ModuleDict):
@@ -136,6 +148,7 @@ class _DenseBlockGrad(torch.autograd.Function):
         k.chan_insert(S, 0, k.bn_stats(x, layers[0].norm1.running_mean[:c0]))
         recs = []
         ci = c0
+        defer = _DEFER and _defer_ok(c0, _growth(block))
         for li, layer in enumerate(layers):
             n1 = layer.norm1
             y1, mean, rstd = k.bn_fwd_train(buf, S, n1.weight, n1.bias, n1.running_mean,
@@ -146,11 +159,16 @@ class _DenseBlockGrad(torch.autograd.Function):
             g = layer.conv2.weight.shape[0]
             st = torch.empty(2, g, dtype=torch.float32, device=x.device)
             nxt = layers[li + 1].norm1.running_mean[ci:ci + g] if li + 1 < len(layers) else None
+            link = None
+            if defer and n1.weight is not None and n1.bias is not None:
+                link = Fn.BNLink()  # norm1 = ReLU(BN) of buf[..., :ci] (z-mask form)
+                link.z, link.mean, link.rstd = buf, mean, rstd
+                link.gamma, link.beta = n1.weight, n1.bias
             with torch.enable_grad():  # the new feature's statistics from conv2's epilogue
-                out = layer.tail(leaf, st, nxt)
+                out = layer.tail(leaf, st, nxt, link)
             k.chan_insert(buf, ci, out.detach())
             k.chan_insert(S, ci, st)
-            recs.append((leaf, out, mean, rstd, ci))
+            recs.append((leaf, out, mean, rstd, ci, link))
             ci += g
         ctx.block = block
         ctx.recs = recs
@@ -173,16 +191,34 @@ class _DenseBlockGrad(torch.autograd.Function):
         else:
             G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)
             k.chan_accum(G, 0, gy, True)
+        # deferred corrections K1 | K2 per channel (see bn_defer_step)
+        k12 = None
+        if any(r[5] is not None for r in ctx.recs):
+            k12 = torch.empty(2, G.shape[-1], dtype=torch.float32, device=G.device)
+            k.zero_f32(k12)
         for i in range(len(ctx.recs) - 1, -1, -1):
-            leaf, out, mean, rstd, ci = ctx.recs[i]
+            leaf, out, mean, rstd, ci, link = ctx.recs[i]
             g = out.shape[-1]
             g_out = (k.chan_slice(G, ci, g) if _GRAD_BF16 else
                      k.chan_extract(G, ci, g).to(out.dtype))
+            if link is not None:
+                link.gacc = G
             torch.autograd.backward(out, g_out)
             n1 = layers[i].norm1
             gamma, beta = n1.weight, n1.bias
             dy = leaf.grad
-            if dy is not None:
+            if link is not None and link.sums is not None:
+                # conv1's dgrad added gamma*rstd * g into G[..., :ci]; fold this layer's
+                # corrections and finish the channels no earlier layer reads: layer i-1's
+                # output (ci - growth .. ci), or the block input for layer 0
+                s0 = 0 if i == 0 else ci - ctx.recs[i - 1][1].shape[-1]
+                k.bn_defer_step(link.sums, gamma, mean, rstd, s0, k12, Fn._sink(gamma, G),
+                                Fn._sink(beta, G), G, buf)
+                link.sums = link.gacc = link.z = None
+            elif link is not None:
+                raise RuntimeError("dense block: conv1's fused BN-backward hand-off did not run "
+                                   "(MPA_DENSE_DEFER=0 selects the per-layer form)")
+            elif dy is not None:
                 k.bn_bwd(dy.contiguous(), buf, Fn._empty(dy), mean, rstd, gamma,
                          Fn._sink(gamma, dy), Fn._sink(beta, dy), True, False, beta, gacc=G)
             Fn._done(gamma, beta)

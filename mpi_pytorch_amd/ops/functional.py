@@ -86,10 +86,14 @@ class BNLink:
     mask and sums (g, g * x_hat) while the gradient is still in registers - and the
     producer's backward runs only the BN apply pass (no reduce pass, no re-read of dy/y)."""
 
-    __slots__ = ("z", "y", "mean", "rstd", "gamma", "beta", "sums")
+    __slots__ = ("z", "y", "mean", "rstd", "gamma", "beta", "sums", "gacc")
 
     def __init__(self):
         self.z = self.y = self.mean = self.rstd = self.gamma = self.beta = self.sums = None
+        # gacc: a DenseNet block gradient.  The consumer's (1x1) dgrad then ADDS gamma*rstd *
+        # g into its first Ci channels instead of returning dx, and the producer side
+        # (_DenseBlockGrad) finishes the BN backward with deferred per-channel corrections
+        self.gacc = None
 
 
 class GradJoin:
@@ -269,7 +273,12 @@ class _ConvBNAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             li = ctx.link_in
             wt = weight_t_of(w)
-            if (li is not None and li.z is not None and (wt is not None or not dz.is_cuda)
+            if (li is not None and li.gacc is not None and (wt is not None or not dz.is_cuda)
+                    and k.conv_bnred_ok(w.shape[0], w.shape[3])):
+                li.sums = k.conv_dgrad_bnred_gacc(dz, weight_of(w), wt, li.z, li.mean, li.rstd,
+                                                  li.gamma, li.beta, li.gacc)
+                dx = None
+            elif (li is not None and li.z is not None and (wt is not None or not dz.is_cuda)
                     and k.conv_bnred_ok(w.shape[0], w.shape[3])):
                 dx, li.sums = k.conv_dgrad_bnred(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1],
                                                  sh, sw, ph, pw, wt, li.z,

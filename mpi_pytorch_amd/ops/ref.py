@@ -242,6 +242,48 @@ def conv_dgrad_bnred(dy, w, H, W, sh, sw, ph, pw, wt, z, y, mean, rstd, gamma=No
     return g.reshape(dx.shape).to(dx.dtype), sums
 
 
+def conv_dgrad_bnred_gacc(dz, w, wt, zbuf, mean, rstd, gamma, beta, G):
+    """1x1 / stride-1 dgrad fused with the backward of the ReLU(BN) that produced its input
+    (a DenseNet norm1 over the block buffer's first Ci channels): G[..., :Ci] += gamma*rstd *
+    g with g the masked dgrad (no dy tensor); returns [sum g | sum g * xhat].  The rest of
+    the BN backward is deferred to bn_defer_step."""
+    Ci = w.shape[-1]
+    N, H, W_ = dz.shape[:3]
+    dx = conv_dgrad(dz, w, H, W_, 1, 1, 0, 0)
+    g = _f(dx).to(dz.dtype).float().reshape(-1, Ci)  # the kernel rounds dy to bf16 first
+    z = _f(zbuf[..., :Ci]).reshape(-1, Ci)
+    sc = gamma.float()[:Ci] * rstd[:Ci]
+    sh_ = beta.float()[:Ci] - mean[:Ci] * sc
+    g = g * ((z * sc + sh_).to(torch.bfloat16).float() > 0)
+    xhat = (z - mean[:Ci]) * rstd[:Ci]
+    Gv = G[..., :Ci]
+    Gv.copy_((Gv.float() + (sc * g).reshape(Gv.shape)).to(G.dtype))
+    return torch.cat([g.sum(0), (g * xhat).sum(0)])
+
+
+def bn_defer_step(sums, gamma, mean, rstd, s0, k12, dgamma, dbeta, G, x):
+    """Fold a dense layer's norm1 sums into the block's deferred corrections k12 [2, Ctot]
+    (channels < s0) and the (gamma, beta) gradients, and apply the final correction
+    G += K1 + K2 * xhat to the channels [s0, Ci)."""
+    Ci = sums.numel() // 2
+    M = x.numel() // x.shape[-1]
+    sg, sgx = sums[:Ci], sums[Ci:]
+    if _opt(dgamma) is not None:
+        dgamma.add_(sgx)
+    if _opt(dbeta) is not None:
+        dbeta.add_(sg)
+    a = gamma.float()[:Ci] * rstd[:Ci]
+    t1, t2 = -a * sg / M, -a * sgx / M
+    k1 = k12[0, s0:Ci] + t1[s0:]
+    k2 = k12[1, s0:Ci] + t2[s0:]
+    k12[0, :s0] += t1[:s0]
+    k12[1, :s0] += t2[:s0]
+    xs = _f(x[..., s0:Ci])
+    xhat = (xs - mean[s0:Ci]) * rstd[s0:Ci]
+    Gv = G[..., s0:Ci]
+    Gv.copy_((Gv.float() + k1 + k2 * xhat).to(G.dtype))
+
+
 # ---------------------------------------------------------------------------------- pool
 def _pool_out(H, k, s, p, ceil):
     if ceil:

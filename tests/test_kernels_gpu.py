@@ -389,6 +389,41 @@ def test_splitk_finalize(gpu, case):
             assert rel(st, str_) < 2e-2
 
 
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+def test_dense_deferred_norm1_backward(gpu, gdt):
+    """DenseNet norm1 -> conv1 hand-off: the 1x1 dgrad epilogue adds gamma*rstd * g into the
+    block gradient's channel prefix and reduces (sum g, sum g*xhat); bn_defer_step folds the
+    per-channel corrections and finishes a channel slice - both == the fp32 oracle."""
+    torch.manual_seed(41)
+    N, H, W, ctot, Ci, K = 3, 14, 14, 320, 256, 128
+    buf = bf(N, H, W, ctot, dev=gpu, scale=2.0)
+    dz = bf(N, H, W, K, dev=gpu)
+    w = bf(K, 1, 1, Ci, dev=gpu, scale=1.0 / math.sqrt(K))
+    wt = w.permute(3, 1, 2, 0).reshape(Ci, 1, K).contiguous()
+    mean = torch.randn(ctot, device=gpu) * 0.3
+    rstd = torch.rand(ctot, device=gpu) + 0.5
+    gamma = torch.rand(Ci, device=gpu) + 0.5
+    beta = torch.randn(Ci, device=gpu) * 0.2
+    G0 = torch.randn(N, H, W, ctot, device=gpu).to(gdt)
+    G, Gr = G0.clone(), G0.clone()
+    sums = C().conv_dgrad_bnred_gacc(dz, w, wt, buf, mean, rstd, gamma, beta, G)
+    sr = ref.conv_dgrad_bnred_gacc(dz, w, wt, buf, mean, rstd, gamma, beta, Gr)
+    torch.cuda.synchronize()
+    assert rel(G, Gr) < 1e-2 and rel(sums, sr) < 2e-2
+    assert torch.equal(G[..., Ci:], G0[..., Ci:])  # channels past the prefix untouched
+    for s0 in (224, 0):  # a 32-channel slice (layer i > 0), the whole prefix (layer 0)
+        k12 = torch.randn(2, ctot, device=gpu)
+        dg, db = torch.zeros(Ci, device=gpu), torch.zeros(Ci, device=gpu)
+        k12r, dgr, dbr = k12.clone(), dg.clone(), db.clone()
+        G1, G1r = G.clone(), G.clone()
+        C().bn_defer_step(sums, gamma, mean, rstd, s0, k12, dg, db, G1, buf)
+        ref.bn_defer_step(sums, gamma, mean, rstd, s0, k12r, dgr, dbr, G1r, buf)
+        torch.cuda.synchronize()
+        assert rel(G1, G1r) < 1e-2 and rel(k12, k12r) < 1e-5
+        assert rel(dg, dgr) < 1e-5 and rel(db, dbr) < 1e-5
+        assert torch.equal(G1[..., :s0], G[..., :s0]) and torch.equal(G1[..., Ci:], G[..., Ci:])
+
+
 def test_conv_halo_repeatable(gpu):
     """Persistent 2-stage ring: repeated launches are bitwise identical (race screen)."""
     torch.manual_seed(23)
