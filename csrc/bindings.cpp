@@ -317,10 +317,10 @@ Tensor conv_dgrad_bnred_gacc(Tensor dz, Tensor w, Tensor wt, Tensor zbuf, Tensor
   a.ep_gacc = G.data_ptr();
   a.ep_gacc_f32 = G.scalar_type() == torch::kFloat32 ? 1 : 0;
   Tensor sums = torch::empty({2 * Ci}, dz.options().dtype(torch::kFloat32));
-  Tensor slab = torch::empty({mpa::igemm_bnred_slab_floats(a.M, Ci, 1)},
+  TORCH_CHECK(mpa::dense_gacc_ok(a), "conv_dgrad_bnred_gacc: operand sizes");
+  Tensor slab = torch::empty({(int64_t)((a.M + 127) / 128) * 2 * Ci},
                              dz.options().dtype(torch::kFloat32));
-  mpa::igemm_rows_dgrad_bnred(a, 8, true, slab.data_ptr<float>(), sums.data_ptr<float>(),
-                              cur_stream());
+  mpa::dense_gacc(a, slab.data_ptr<float>(), sums.data_ptr<float>(), cur_stream());
   return sums;
 }
 

@@ -86,10 +86,10 @@ struct IGemmArgs {
   // gamma*rstd, beta))) > 0) and never reads y; the implicit GEMM always reads ep_y
   const float* ep_gamma;
   const float* ep_beta;
-  // ep_gacc (rows kernel, with ep_bnred and ep_gamma / ep_beta): no output is written;
-  // instead gamma*rstd * g is ADDED into ep_gacc (same row stride ldc as ep_z; bf16 with
-  // one rounding, or fp32 when ep_gacc_f32) - the DenseNet block-gradient form whose
-  // per-channel BN-backward corrections are deferred (bn_defer_fold / bn_defer_apply)
+  // ep_gacc (dense_gacc.hip only): no output is written; gamma*rstd * g is ADDED into
+  // ep_gacc (same row stride ldc as ep_z; bf16 with one rounding, or fp32 when
+  // ep_gacc_f32) - the DenseNet block gradient, whose per-channel BN-backward corrections
+  // are deferred (bn_defer_step)
   void* ep_gacc;
   int ep_gacc_f32;
   int stap;               // 8-channel "super-tap" forward: each tap entry = 4 adjacent kernel
@@ -185,6 +185,9 @@ int64_t bn_ws_floats(int M, int C);
 void slab_reduce(const float* slab, int S, int W, float* out, bool zero_out, hipStream_t s);
 // deferred BN-backward corrections of a dense block (bn.hip, bn_defer_step_kernel); the host
 // guarantees (Ci - s0) % 8 == 0 and 256 % ((Ci - s0) / 8) == 0
+// DenseNet norm1 -> conv1 dgrad hand-off kernel (dense_gacc.hip)
+bool dense_gacc_ok(const IGemmArgs& a);
+void dense_gacc(IGemmArgs a, float* slab, float* sums, hipStream_t s);
 void bn_defer_step(const float* sums, const float* gamma, const float* mean, const float* rstd,
                    int Ci, int s0, int M, float* k12, int ldk, float* dgamma, float* dbeta,
                    void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, hipStream_t s);

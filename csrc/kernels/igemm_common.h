@@ -214,10 +214,6 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
     // bias / stats shift; in BN-reduce mode the same registers carry mean / rstd
     f32x4 bias[TN], shift[TN];
     const bool bnred = p.ep_bnred != 0;
-    // z-mask affine (bnred with gamma / beta and no y): bn_fwd_train's scale / shift
-    const bool zmask = bnred && !p.ep_y && p.ep_gamma && p.ep_beta;
-    const bool gacc = bnred && p.ep_gacc != nullptr;
-    f32x4 msc[TN], msh[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -232,16 +228,6 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
       if (ssrc) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) shift[j][r] = (n + r < p.N) ? ssrc[n + r] : 0.f;
-      }
-      msc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      msh[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (zmask) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sc = (n + r < p.N) ? p.ep_gamma[n + r] * shift[j][r] : 0.f;
-          msc[j][r] = sc;
-          msh[j][r] = (n + r < p.N) ? __builtin_fmaf(-bias[j][r], sc, p.ep_beta[n + r]) : 0.f;
-        }
       }
     }
     size_t orows[TM];
@@ -264,27 +250,14 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
     // accumulate mode: issue every read of the existing output up front (one exposed
     // latency for the tile instead of one per fragment)
     uint2 oldv[TM][TN];
-    if (p.beta || (gacc && !p.ep_gacc_f32)) {
-      const bf16_t* src = gacc ? (const bf16_t*)p.ep_gacc : out;
+    if (p.beta) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wcol0 + j * 16 + nl;
-          oldv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(src + orows[i] + n)
+          oldv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(out + orows[i] + n)
                                                  : make_uint2(0u, 0u);
-        }
-    }
-    // BN-backward reduction: z of every fragment up front as well
-    uint2 zv[TM][TN];
-    if (bnred) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wcol0 + j * 16 + nl;
-          zv[i][j] = (moks[i] && n + 3 < p.N) ? *(const uint2*)(p.ep_z + orows[i] + n)
-                                              : make_uint2(0u, 0u);
         }
     }
 #pragma unroll
@@ -300,14 +273,10 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
           // dy (bf16-rounded like the unfused path) masked by ReLU(y); x_hat from z
           bool live[4] = {true, true, true, true};
           if (mok && n + 3 < p.N) {
-            const uint2 zz = zv[i][j];
+            const uint2 zz = *(const uint2*)(p.ep_z + orow + n);
             zr[0] = bf2f(zz.x & 0xffff); zr[1] = bf2f(zz.x >> 16);
             zr[2] = bf2f(zz.y & 0xffff); zr[3] = bf2f(zz.y >> 16);
-            if (zmask) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                live[r] = bf2f(f2bf(__builtin_fmaf(zr[r], msc[j][r], msh[j][r]))) > 0.f;
-            } else if (p.ep_y) {
+            if (p.ep_y) {
               const uint2 yy = *(const uint2*)(p.ep_y + orow + n);
               live[0] = (yy.x & 0x7fff) != 0 && !(yy.x & 0x8000);
               live[1] = ((yy.x >> 16) & 0x7fff) != 0 && !(yy.x & 0x80000000u);
@@ -319,10 +288,42 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
             for (int r = 0; r < 4; ++r) {
               if (n + r < p.N) {
                 zr[r] = bf2f(p.ep_z[orow + n + r]);
-                if (zmask)
-                  live[r] = bf2f(f2bf(__builtin_fmaf(zr[r], msc[j][r], msh[j][r]))) > 0.f;
-                else if (p.ep_y)
-                  live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
+                if (p.ep_y) live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = bf2f(f2bf(acc[i][j][r]));
+            v[r] = live[r] ? d : 0.f;
+          }
+        } else {
+          float old[4] = {0.f, 0.f, 0.f, 0.f};
+          if (p.beta && mok) {
+            if (n + 3 < p.N) {
+              const uint2 oo = oldv[i][j];
+              old[0] = bf2f(oo.x & 0xffff); old[1] = bf2f(oo.x >> 16);
+              old[2] = bf2f(oo.y & 0xffff); old[3] = bf2f(oo.y >> 16);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) old[r] = bf2f(out[orow + n + r]);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = acc[i][j][r] + bias[j][r] + old[r];
+            if (p.relu) t = fmaxf(t, 0.f);
+            v[r] = t;
+          }
+        }
+        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
+        if (mok) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (n + r < p.N) {
+                zr[r] = bf2f(p.ep_z[orow + n + r]);
+                if (p.ep_y) live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
               }
             }
           }
