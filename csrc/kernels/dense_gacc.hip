@@ -40,6 +40,7 @@ __device__ __forceinline__ int gb_lane_chunk(int lane) {
 }
 }  // namespace
 
+template <bool F32>
 __global__ __launch_bounds__(256, 2) void dense_gacc_kernel(IGemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[GB_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -51,6 +52,37 @@ __global__ __launch_bounds__(256, 2) void dense_gacc_kernel(IGemmArgs p) {
   const int M = p.M, N = p.N, K = p.Ktot;
   const int ktiles = K / BK;
 
+  // ---- epilogue operands first: this thread's 8 columns (cg) x rows r0, r0 + 16, ...,
+  // r0 + 112 of x and G do not depend on the GEMM, so their loads are in flight under it
+  // (the first ring wait then waits for them too: one exposed latency, not two)
+  const int cg = tid & 15, r0 = tid >> 4;
+  const int n = n0 + cg * 8;
+  const bool nok = n < N;  // N % 8 == 0: a group is all in or all out
+  float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = nok ? n + j : 0;
+    mu[j] = p.ep_mean[c];
+    rs[j] = p.ep_rstd[c];
+    sc[j] = p.ep_gamma[c] * rs[j];
+    sh[j] = __builtin_fmaf(-mu[j], sc[j], p.ep_beta[c]);
+  }
+  const size_t ld = (size_t)p.ldc;
+  uint4 zq[8], gq[8], gq2[F32 ? 8 : 1];
+#pragma unroll
+  for (int pss = 0; pss < 8; ++pss) {  // every load of the thread in flight first
+    const int m = m0 + r0 + 16 * pss;
+    const bool ok = nok && m < M;
+    const size_t o = (size_t)(ok ? m : 0) * ld + (ok ? n : 0);
+    zq[pss] = ok ? *(const uint4*)(p.ep_z + o) : make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (F32) {
+      const uint4* gp = (const uint4*)((const float*)p.ep_gacc + o);
+      gq[pss] = ok ? gp[0] : make_uint4(0u, 0u, 0u, 0u);
+      gq2[pss] = ok ? gp[1] : make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      gq[pss] = ok ? *(const uint4*)((const bf16_t*)p.ep_gacc + o) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
   // ---- GEMM: DMA lanes (rows past M / columns past N clamp; their results are dropped)
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, 0x7fffffffu);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, 0x7fffffffu);
@@ -111,43 +143,12 @@ __global__ __launch_bounds__(256, 2) void dense_gacc_kernel(IGemmArgs p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = wrow0 + i * 16 + (lane & 15), col = wcol0 + j * 16 + nl;
-        *LDS_PTR(uint2, (char*)(tg + row * GB_TP + col)) =
+        *(uint2*)(tg + row * GB_TP + col) =
             make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
       }
   }
   __syncthreads();
 
-  // ---- sweep: thread = 8 columns (cg) x rows r0, r0 + 16, ..., r0 + 112
-  const int cg = tid & 15, r0 = tid >> 4;
-  const int n = n0 + cg * 8;
-  const bool nok = n < N;  // N % 8 == 0: a group is all in or all out
-  float sc[8], sh[8], mu[8], rs[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = nok ? n + j : 0;
-    mu[j] = p.ep_mean[c];
-    rs[j] = p.ep_rstd[c];
-    sc[j] = p.ep_gamma[c] * rs[j];
-    sh[j] = __builtin_fmaf(-mu[j], sc[j], p.ep_beta[c]);
-  }
-  const bool f32 = p.ep_gacc_f32 != 0;
-  const size_t ld = (size_t)p.ldc;
-  uint4 zq[8], gq[8], gq2[8];
-#pragma unroll
-  for (int pss = 0; pss < 8; ++pss) {  // every load of the thread in flight first
-    const int m = m0 + r0 + 16 * pss;
-    const bool ok = nok && m < M;
-    const size_t o = (size_t)(ok ? m : 0) * ld + (ok ? n : 0);
-    zq[pss] = ok ? *(const uint4*)(p.ep_z + o) : make_uint4(0u, 0u, 0u, 0u);
-    if (f32) {
-      const uint4* gp = (const uint4*)((const float*)p.ep_gacc + o);
-      gq[pss] = ok ? gp[0] : make_uint4(0u, 0u, 0u, 0u);
-      gq2[pss] = ok ? gp[1] : make_uint4(0u, 0u, 0u, 0u);
-    } else {
-      gq[pss] = ok ? *(const uint4*)((const bf16_t*)p.ep_gacc + o) : make_uint4(0u, 0u, 0u, 0u);
-      gq2[pss] = make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -156,7 +157,8 @@ __global__ __launch_bounds__(256, 2) void dense_gacc_kernel(IGemmArgs p) {
     const int row = r0 + 16 * pss, m = m0 + row;
     if (!nok || m >= M) continue;
     float g[8], z[8];
-    unpack8(*LDS_PTR(const uint4, (const char*)(tg + row * GB_TP + cg * 8)), g);
+    const uint4 gl = *(const uint4*)(tg + row * GB_TP + cg * 8);
+    unpack8(gl, g);
     unpack8(zq[pss], z);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void dense_gacc_kernel(IGemmArgs p) {
       q[j] += g[j] * (z[j] - mu[j]) * rs[j];
     }
     const size_t o = (size_t)m * ld + n;
-    if (f32) {
+    if constexpr (F32) {
       f32x4 a = __builtin_bit_cast(f32x4, gq[pss]), b = __builtin_bit_cast(f32x4, gq2[pss]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -233,7 +235,10 @@ void dense_gacc(IGemmArgs a, float* slab, float* sums, hipStream_t s) {
   a.tiles_total = tiles_m * a.tiles_n;
   a.stats = slab;
   a.stats_sums = sums;
-  hipLaunchKernelGGL(dense_gacc_kernel, dim3(a.tiles_total), dim3(256), 0, s, a);
+  if (a.ep_gacc_f32)
+    hipLaunchKernelGGL(dense_gacc_kernel<true>, dim3(a.tiles_total), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(dense_gacc_kernel<false>, dim3(a.tiles_total), dim3(256), 0, s, a);
   slab_reduce(slab, tiles_m, 2 * a.N, sums, false, s);
 }
 

@@ -319,66 +319,6 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
         }
         const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
         if (mok) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              if (n + r < p.N) {
-                zr[r] = bf2f(p.ep_z[orow + n + r]);
-                if (p.ep_y) live[r] = bf2f(p.ep_y[orow + n + r]) > 0.f;
-              }
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float d = bf2f(f2bf(acc[i][j][r]));
-            v[r] = live[r] ? d : 0.f;
-          }
-        } else {
-          float old[4] = {0.f, 0.f, 0.f, 0.f};
-          if (p.beta && mok) {
-            if (n + 3 < p.N) {
-              const uint2 oo = oldv[i][j];
-              old[0] = bf2f(oo.x & 0xffff); old[1] = bf2f(oo.x >> 16);
-              old[2] = bf2f(oo.y & 0xffff); old[3] = bf2f(oo.y >> 16);
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (n + r < p.N) old[r] = bf2f(out[orow + n + r]);
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float t = acc[i][j][r] + bias[j][r] + old[r];
-            if (p.relu) t = fmaxf(t, 0.f);
-            v[r] = t;
-          }
-        }
-        const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-        if (mok && gacc) {
-          // block-gradient accumulate: G += gamma*rstd * g (the deferred BN-backward form)
-          if (p.ep_gacc_f32) {
-            float* gp = (float*)p.ep_gacc + orow + n;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) gp[r] += msc[j][r] * v[r];
-          } else if (n + 3 < p.N) {
-            const uint2 oo = oldv[i][j];
-            const float a0 = bf2f(oo.x & 0xffff) + msc[j][0] * v[0];
-            const float a1 = bf2f(oo.x >> 16) + msc[j][1] * v[1];
-            const float a2 = bf2f(oo.y & 0xffff) + msc[j][2] * v[2];
-            const float a3 = bf2f(oo.y >> 16) + msc[j][3] * v[3];
-            *(uint2*)((bf16_t*)p.ep_gacc + orow + n) = make_uint2(pack2(a0, a1), pack2(a2, a3));
-          } else {
-            bf16_t* gp = (bf16_t*)p.ep_gacc + orow + n;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) gp[r] = f2bf(bf2f(gp[r]) + msc[j][r] * v[r]);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {  // BN backward's reduction, as below
-            s[j][r] += v[r];
-            q[j][r] += v[r] * (zr[r] - bias[j][r]) * shift[j][r];
-          }
-        } else if (mok) {
           if (n + 3 < p.N) {
             *(uint2*)(out + orow + n) = make_uint2(lo, hi);
           } else {

@@ -54,7 +54,7 @@ _GRAD_BF16 = os.environ.get("MPA_DENSE_GRAD_BF16", "1") == "1"
 # rest of every layer's BN backward is summed and applied once per channel.  No dy
 # tensor, no norm1 reduce / apply passes over the O(L^2) channel prefixes.
 # MPA_DENSE_DEFER=0 restores the per-layer bn_bwd(gacc=G).
-_DEFER = os.environ.get("MPA_DENSE_DEFER", "0") == "1"
+_DEFER = os.environ.get("MPA_DENSE_DEFER", "1") == "1"
 
 
 def _defer_ok(c0: int, growth: int) -> bool:

@@ -2,7 +2,7 @@
 # deferred DenseNet norm1 backward: A/B bench + kernel trace breakdown
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O; R=$(pwd)
-timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread -k "dense or bnred" > $O/t_defer.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread -k "dense or bnred or halo_fwd or splitk" > $O/t_defer.log 2>&1
 rc=$?; tail -1 $O/t_defer.log; [ $rc -eq 0 ] || { grep -E "^E |Error|FAILED" $O/t_defer.log | head -20; exit $rc; }
 for d in 1 0; do
 MPA_DENSE_DEFER=$d timeout -k 10 300 python bench.py --model densenet --batch 256 --steps 10 --warmup 3 --small-batch 0 > $O/b_dn$d.json 2> $O/b_dn$d.err || { tail -5 $O/b_dn$d.err; exit 1; }

@@ -338,11 +338,14 @@ def test_inception_grouped_heads_equal_separate_convs():
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
 
 
-def test_densenet_feature_buffer_blocks_equal_plain_autograd():
+@pytest.mark.parametrize("defer", [True, False])
+def test_densenet_feature_buffer_blocks_equal_plain_autograd(monkeypatch, defer):
     """DenseNet blocks on one feature buffer (norm1 on the channel prefix with per-feature
-    statistics taken once, input gradients added into one fp32 accumulator) == per-layer
-    concat + plain autograd, in fp32 on the CPU (train and eval forward, gradients, running
-    statistics)."""
+    statistics taken once, input gradients added into one accumulator - with the deferred
+    per-channel norm1 corrections, or the per-layer BN backward) == per-layer concat + plain
+    autograd, in fp32 on the CPU (train and eval forward, gradients, running statistics)."""
+    from mpi_pytorch_amd.models import densenet as dn
+    monkeypatch.setattr(dn, "_DEFER", defer)
     torch.manual_seed(0)
     model, _o, _s, _ = build_training("densenet", 10, torch.device("cpu"), World(), 1e-3)
     a = model._mpa_arena
