@@ -761,7 +761,9 @@ __device__ __forceinline__ void bn_coeffs(const float* __restrict__ mean,
   }
 }
 
-template <bool K3S2>
+// MODE 0: any window; 1: 3x3 / stride 2 / pad 1; 2: 3x3 / stride 2 / pad 0 (Inception's
+// valid pools: every window lies inside the image, no clamp, no mask)
+template <int MODE>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const bf16_t* __restrict__ z, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
@@ -808,11 +810,11 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     int bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; bz[j] = 0.f; }
-    if constexpr (K3S2) {
+    if constexpr (MODE != 0) {
       // 3x3 / stride 2 / pad 1: all nine loads issued before any is consumed (out-of-range
       // taps read a clamped in-range pixel and are masked).  (Prefetching the next
       // output's nine loads ahead of this output's stores measured slower: 300 -> 384 us.)
-      const int h0 = 2 * p - 1, w0 = 2 * q - 1;
+      const int h0 = 2 * p - (MODE == 1 ? 1 : 0), w0 = 2 * q - (MODE == 1 ? 1 : 0);
       uint4 v9[9];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -825,7 +827,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const bool ok = (unsigned)(h0 + i) < (unsigned)g.H && (unsigned)(w0 + k) < (unsigned)g.W;
+          const bool ok = MODE == 2 ||
+                          ((unsigned)(h0 + i) < (unsigned)g.H && (unsigned)(w0 + k) < (unsigned)g.W);
           float f[8];
           unpack8(v9[i * 3 + k], f);
 #pragma unroll
@@ -1021,12 +1024,15 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(
   }
 }
 
-// 3x3 / stride 2 / pad 1 pool over an even H x W (H == 2P, W == 2Q): thread = one 2x2 input
-// cell (2p..2p+1, 2q..2q+1) x 8 channels.  Row 2p is covered only by window row p (tap 1),
-// row 2p+1 by window p (tap 2) and p+1 (tap 0); same for columns.  So the cell needs the
-// four pooled positions (p|p+1, q|q+1), and every load is independent.
+// 3x3 / stride 2 pool, thread = one 2x2 input cell (2p..2p+1, 2q..2q+1) x 8 channels.
+// PAD 1 over an even H x W (H == 2P, W == 2Q; ResNet / DenseNet stems): row 2p is covered
+// only by window row p (tap 1), row 2p+1 by window p (tap 2) and p+1 (tap 0), so the cell
+// needs the pooled positions (p|p+1, q|q+1).  PAD 0 over H == 2P+1, W == 2Q+1 (Inception's
+// valid pools): row 2p by window p (tap 0) and p-1 (tap 2), row 2p+1 by window p (tap 1)
+// only; cells run over (P+1) x (Q+1) so the last row / column (2P, 2Q) is covered, and the
+// pooled positions are (p-1|p, q-1|q).  Every load is independent.
 // APPLY = false: reduce (sum g, sum g*xhat) into the slab; true: write dz.
-template <bool APPLY>
+template <bool APPLY, int PAD = 1>
 __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
     const bf16_t* __restrict__ dp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -1061,20 +1067,29 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) { zsums[c0 + j] = 0.f; zsums[C + c0 + j] = 0.f; }
     }
-    const int cells = g.N * g.P * g.Q;
-    // pooled neighbours (dp, idx): [0]=(p,q) [1]=(p,q+1) [2]=(p+1,q) [3]=(p+1,q+1); out-of-
-    // range neighbours load (p,q) and are masked in proc.  Register image per cell: dp 0..3,
-    // idx pairs 4..5, z 6..9.  The next cell's loads are issued before this cell's dz stores
-    // (sweep_rows_pl: a load after a store would wait for the store in the in-order vmcnt).
+    // cell grid: P x Q (PAD 1) or (P+1) x (Q+1) (PAD 0)
+    const int CP = g.P + (PAD ? 0 : 1), CQ = g.Q + (PAD ? 0 : 1);
+    const int cells = g.N * CP * CQ;
+    // pooled neighbours (dp, idx) at window rows p + dp0 + (u >> 1), cols q + dq0 + (u & 1)
+    // with dp0 = dq0 = 0 (PAD 1) or -1 (PAD 0); out-of-range neighbours load an in-range
+    // one and are masked in proc.  Register image per cell: dp 0..3, idx pairs 4..5, z 6..9
+    // (pixels past the image load a clamped one, never stored).  The next cell's loads are
+    // issued before this cell's dz stores (sweep_rows_pl: a load after a store would wait
+    // for the store in the in-order vmcnt).
+    constexpr int D0 = PAD ? 0 : -1;
+    auto nb_ok = [&](int p, int q, int u) {
+      const int pp = p + D0 + (u >> 1), qq = q + D0 + (u & 1);
+      return (unsigned)pp < (unsigned)g.P && (unsigned)qq < (unsigned)g.Q;
+    };
     auto load = [&](int r, uint4 (&v)[10]) {
-      const int q = r % g.Q, t = r / g.Q, p = t % g.P, n = t / g.P;
-      const bool pn = p + 1 < g.P, qn = q + 1 < g.Q;
+      const int q = r % CQ, t = r / CQ, p = t % CP, n = t / CP;
       uint2 iv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int pp = p + (u >> 1), qq = q + (u & 1);
-        const bool ok = (!(u >> 1) || pn) && (!(u & 1) || qn);
-        const size_t o = (((size_t)n * g.P + (ok ? pp : p)) * g.Q + (ok ? qq : q)) * C + c0;
+        const bool ok = nb_ok(p, q, u);
+        const int pp = ok ? p + D0 + (u >> 1) : min(p, g.P - 1);
+        const int qq = ok ? q + D0 + (u & 1) : min(q, g.Q - 1);
+        const size_t o = (((size_t)n * g.P + pp) * g.Q + qq) * C + c0;
         v[u] = *(const uint4*)(dp + o);
         iv[u] = *(const uint2*)(idx + o);
       }
@@ -1082,36 +1097,44 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
       v[5] = make_uint4(iv[2].x, iv[2].y, iv[3].x, iv[3].y);
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
-        const int h = 2 * p + (w4 >> 1), w = 2 * q + (w4 & 1);
+        const int h = min(2 * p + (w4 >> 1), g.H - 1), w = min(2 * q + (w4 & 1), g.W - 1);
         v[6 + w4] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
       }
     };
     auto proc = [&](int r, uint4 (&v)[10]) {
-      const int q = r % g.Q, t = r / g.Q, p = t % g.P, n = t / g.P;
-      const bool pn = p + 1 < g.P, qn = q + 1 < g.Q;
+      const int q = r % CQ, t = r / CQ, p = t % CP, n = t / CP;
       uint2 iv[4] = {make_uint2(v[4].x, v[4].y), make_uint2(v[4].z, v[4].w),
                      make_uint2(v[5].x, v[5].y), make_uint2(v[5].z, v[5].w)};
       float d[4][8];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const bool ok = (!(u >> 1) || pn) && (!(u & 1) || qn);
-        if (!ok) iv[u] = make_uint2(~0u, ~0u);  // argmax 255 never matches a tap
+        if (!nb_ok(p, q, u)) iv[u] = make_uint2(~0u, ~0u);  // argmax 255 never matches a tap
         unpack8(v[u], d[u]);
       }
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
         const int a0 = w4 >> 1, b0 = w4 & 1;  // input pixel (2p+a0, 2q+b0)
+        if (2 * p + a0 >= g.H || 2 * q + b0 >= g.W) continue;  // PAD 0: past the last row
         float zr[8], gr[8];
         unpack8(v[6 + w4], zr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float acc = 0.f;
-          // covering windows: rows {p: tap 1+a0} (+ {p+1: tap 0} if a0), cols likewise
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int du = u >> 1, eu = u & 1;
-            if ((du && !a0) || (eu && !b0)) continue;
-            const int ti = du ? 0 : 1 + a0, tk = eu ? 0 : 1 + b0;
+            int ti, tk;
+            if constexpr (PAD) {
+              // rows {p: tap 1+a0} (+ {p+1: tap 0} if a0), cols likewise
+              if ((du && !a0) || (eu && !b0)) continue;
+              ti = du ? 0 : 1 + a0;
+              tk = eu ? 0 : 1 + b0;
+            } else {
+              // rows {p: tap a0} (+ {p-1: tap 2} if !a0), cols likewise
+              if ((!du && a0) || (!eu && b0)) continue;
+              ti = du ? a0 : 2;
+              tk = eu ? b0 : 2;
+            }
             const uint32_t word = j < 4 ? iv[u].x : iv[u].y;
             if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[u][j];
           }
@@ -1149,6 +1172,11 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_cell_kernel(
 static bool pool_k3s2p1_even(const PoolGeom& g) {
   return g.kh == 3 && g.kw == 3 && g.sh == 2 && g.sw == 2 && g.ph == 1 && g.pw == 1 &&
          g.H == 2 * g.P && g.W == 2 * g.Q;
+}
+
+static bool pool_k3s2p0_odd(const PoolGeom& g) {
+  return g.kh == 3 && g.kw == 3 && g.sh == 2 && g.sw == 2 && g.ph == 0 && g.pw == 0 &&
+         g.H == 2 * g.P + 1 && g.W == 2 * g.Q + 1;
 }
 
 // --------------------------------------- deferred BN-backward corrections (DenseNet)
@@ -1333,8 +1361,12 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
                          int ph, int pw, bf16_raw* y, uint8_t* idx, float* mean, float* rstd,
                          int64_t* counter, hipStream_t s, bf16_raw* zsel) {
   const PoolGeom g{N, H, W, P, Q, kh, kw, sh, sw, ph, pw};
-  const bool k3 = kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1;
-  hipLaunchKernelGGL(k3 ? bn_relu_maxpool_fwd_kernel<true> : bn_relu_maxpool_fwd_kernel<false>,
+  const bool k3 = kh == 3 && kw == 3 && sh == 2 && sw == 2;
+  const int mode = (k3 && ph == 1 && pw == 1) ? 1
+                   : (k3 && ph == 0 && pw == 0 && 2 * P + 1 <= H && 2 * Q + 1 <= W) ? 2 : 0;
+  hipLaunchKernelGGL(mode == 1   ? bn_relu_maxpool_fwd_kernel<1>
+                     : mode == 2 ? bn_relu_maxpool_fwd_kernel<2>
+                                 : bn_relu_maxpool_fwd_kernel<0>,
                      grid_for(N * P * Q, C, stem_grid(0)), dim3(256), 0, s, z, stats, gamma, beta,
                      rmean, rvar, momentum, eps, C, g, y, idx, mean, rstd,
                      (unsigned long long*)counter, zsel);
@@ -1370,6 +1402,20 @@ void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, c
       slab_reduce(slab, gr.x, 2 * C, ws, false, s);
     }
     hipLaunchKernelGGL(maxpool_bn_bwd_cell_kernel<true>, grid_for(cells, C, stem_grid(2)),
+                       dim3(256), 0, s, dp, idx, z, mean, rstd, gamma, beta, ws, dgamma, dbeta, C,
+                       g, nullptr, nullptr, dz);
+    return;
+  }
+  if (pool_k3s2p0_odd(g)) {
+    const int cells = N * (P + 1) * (Q + 1);
+    if (!reduced) {
+      const dim3 gr = grid_for(cells, C, stem_grid(1));
+      hipLaunchKernelGGL((maxpool_bn_bwd_cell_kernel<false, 0>), gr, dim3(256), 0, s, dp, idx, z,
+                         mean, rstd, gamma, beta, nullptr, nullptr, nullptr, C, g, slab, ws,
+                         nullptr);
+      slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+    }
+    hipLaunchKernelGGL((maxpool_bn_bwd_cell_kernel<true, 0>), grid_for(cells, C, stem_grid(2)),
                        dim3(256), 0, s, dp, idx, z, mean, rstd, gamma, beta, ws, dgamma, dbeta, C,
                        g, nullptr, nullptr, dz);
     return;

@@ -831,6 +831,8 @@ def _global_idx(idx, H, W, kh, kw, sh, sw, ph, pw):
 @pytest.mark.parametrize("case", [(4, 112, 112, 64, 3, 3, 2, 2, 1, 1, False),  # resnet stem
                                   (2, 55, 55, 96, 3, 3, 2, 2, 0, 0, True),     # ceil mode
                                   (2, 71, 71, 192, 3, 3, 2, 2, 0, 0, False),   # inception pool2
+                                  (1, 147, 147, 64, 3, 3, 2, 2, 0, 0, False),  # inception pool1
+                                  (2, 9, 13, 16, 3, 3, 2, 2, 0, 0, False),     # valid, H != W
                                   (2, 21, 17, 16, 3, 3, 2, 2, 1, 1, False)])
 def test_bn_relu_maxpool_fused(gpu, case):
     """Fused stem BN+ReLU+max-pool (forward) and pool-gather+BN backward vs the oracle's
