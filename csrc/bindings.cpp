@@ -62,8 +62,11 @@ Tensor empty_like_shape(const Tensor& ref, at::IntArrayRef shape, torch::Dtype d
 }
 
 // ------------------------------------------------------------------------------- conv
-Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                bool relu, Tensor stats, Tensor shift) {
+// out (optional): a bf16 channel-window view [N, P, Q, K] of a wider NHWC buffer (DenseNet's
+// block buffer) the output is written into (row stride out.stride(2)); stats may then be a
+// [2, K] window of a wider statistics table (row stride stats.stride(0))
+static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
+                            int64_t pw, bool relu, Tensor stats, Tensor shift, const Tensor* out) {
   CHECK_ACT(x);
   CHECK_ACT(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: x NHWC, w KRSC");
@@ -74,9 +77,32 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
   const int P = (H + 2 * ph - R) / sh + 1, Q = (W + 2 * pw - S) / sw + 1;
   TORCH_CHECK(P > 0 && Q > 0, "conv_fwd: empty output");
   if (has(bias)) TORCH_CHECK(bias.numel() == K, "conv_fwd: bias size");
-  if (has(stats)) TORCH_CHECK(stats.numel() == 2 * K, "conv_fwd: stats size");
+  int stats_ld = 0;
+  if (has(stats)) {
+    TORCH_CHECK(stats.numel() == 2 * K, "conv_fwd: stats size");
+    if (out) {
+      TORCH_CHECK(stats.dim() == 2 && stats.size(0) == 2 && stats.stride(1) == 1 &&
+                      stats.stride(0) >= K,
+                  "conv_fwd_into: stats must be a [2, K] row-window");
+      stats_ld = (int)stats.stride(0);
+    }
+  }
   const c10::OptionalDeviceGuard g(device_of(x));
-  Tensor y = empty_like_shape(x, {N, P, Q, K}, torch::kBFloat16);
+  Tensor y;
+  int ldc = K;
+  if (out) {
+    CHECK_CUDA((*out));
+    CHECK_BF16((*out));
+    TORCH_CHECK(out->dim() == 4 && out->size(0) == N && out->size(1) == P && out->size(2) == Q &&
+                    out->size(3) == K && out->stride(3) == 1 &&
+                    out->stride(1) == (int64_t)Q * out->stride(2) &&
+                    out->stride(0) == (int64_t)P * out->stride(1) && out->stride(2) % 8 == 0,
+                "conv_fwd_into: out must be a channel window [N, P, Q, K] of an NHWC buffer");
+    y = *out;
+    ldc = (int)out->stride(2);
+  } else {
+    y = empty_like_shape(x, {N, P, Q, K}, torch::kBFloat16);
+  }
   mpa::IGemmArgs a{};
   a.A = bp(x); a.aH = H; a.aW = W; a.aC = C;
   a.oH = P; a.oW = Q; a.M = N * P * Q;
@@ -103,21 +129,39 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
     a.Ktot = t * 32;
     a.stap = 1;
   }
-  a.C = y.data_ptr(); a.ldc = K;
+  a.C = y.data_ptr(); a.ldc = ldc;
   a.dH = P; a.dW = Q; a.Uoh = 1; a.Uow = 1; a.Poh = 0; a.Pow = 0;
   a.bias = fopt(bias);
-  a.stats = fopt_mut(stats);
+  if (stats_ld) {  // a checked [2, K] row-window of a wider table
+    CHECK_CUDA(stats);
+    CHECK_F32(stats);
+    a.stats = stats.data_ptr<float>();
+  } else {
+    a.stats = fopt_mut(stats);
+  }
+  a.stats_ld = stats_ld;
   a.stats_shift = fopt(shift);
   if (a.stats_shift) TORCH_CHECK(shift.numel() == K, "conv_fwd: shift size");
   a.relu = relu ? 1 : 0;
   Tensor ws;
-  float* wsp = alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot));
+  // (split-K's finalize writes dense [M][N] rows: none into a window)
+  float* wsp = ldc == K ? alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot)) : nullptr;
   Tensor slab;
   if (a.stats)
     slab = torch::empty({mpa::igemm_slab_floats(a.M, a.N)}, x.options().dtype(torch::kFloat32));
   mpa::igemm_rows(a, vec_width(C), wsp, a.stats ? slab.data_ptr<float>() : nullptr,
                   cur_stream());
   return y;
+}
+
+Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                bool relu, Tensor stats, Tensor shift) {
+  return conv_fwd_impl(x, w, bias, sh, sw, ph, pw, relu, stats, shift, nullptr);
+}
+
+void conv_fwd_into(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
+                   int64_t pw, bool relu, Tensor stats, Tensor shift, Tensor out) {
+  conv_fwd_impl(x, w, bias, sh, sw, ph, pw, relu, stats, shift, &out);
 }
 
 // wt (optional): the transposed weight [C][R*S][K] (arena shadow_t) - the dgrad GEMM then
@@ -326,8 +370,10 @@ Tensor conv_dgrad_bnred_gacc(Tensor dz, Tensor w, Tensor wt, Tensor zbuf, Tensor
 
 // see mpa::bn_defer_step (bn.hip): fold layer sums into the block's deferred-correction
 // table k12 [2, Ctot] and apply the final correction to G's channels [s0, Ci)
+// out (optional, bf16 contiguous [..., Ci - s0]): also receives the finished slice (the
+// gradient its consumer reads), so no separate slice copy is needed
 void bn_defer_step(Tensor sums, Tensor gamma, Tensor mean, Tensor rstd, int64_t s0, Tensor k12,
-                   Tensor dgamma, Tensor dbeta, Tensor G, Tensor x) {
+                   Tensor dgamma, Tensor dbeta, Tensor G, Tensor x, c10::optional<Tensor> out) {
   CHECK_CUDA(G);
   CHECK_CONTIG(G);
   CHECK_ACT(x);
@@ -345,11 +391,18 @@ void bn_defer_step(Tensor sums, Tensor gamma, Tensor mean, Tensor rstd, int64_t 
     CHECK_F32(*t);
     TORCH_CHECK(t->numel() >= Ci, "bn_defer_step: per-channel vector size");
   }
+  const bool into = out && out->defined() && out->numel() > 0;
+  if (into) {
+    CHECK_ACT((*out));
+    TORCH_CHECK(out->is_contiguous() && out->size(-1) == Ci - s0 && out->numel() / (Ci - s0) == M,
+                "bn_defer_step: out must be a contiguous bf16 [..., Ci - s0]");
+  }
   const c10::OptionalDeviceGuard g(device_of(x));
   mpa::bn_defer_step(sums.data_ptr<float>(), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), Ci, (int)s0, M, k12.data_ptr<float>(), ctot,
                      fopt_mut(dgamma), fopt_mut(dbeta), G.data_ptr(),
-                     G.scalar_type() == torch::kFloat32, ctot, bp(x), ctot, cur_stream());
+                     G.scalar_type() == torch::kFloat32, ctot, bp(x), ctot,
+                     into ? bpm(*out) : nullptr, cur_stream());
 }
 
 std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd,
@@ -1260,7 +1313,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred_gacc", &conv_dgrad_bnred_gacc);
-  m.def("bn_defer_step", &bn_defer_step);
+  m.def("bn_defer_step", &bn_defer_step, py::arg("sums"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("s0"), py::arg("k12"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("G"), py::arg("x"), py::arg("out") = py::none());
+  m.def("conv_fwd_into", &conv_fwd_into);
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, py::arg("dy"), py::arg("w"), py::arg("H"),
         py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt"),
         py::arg("z"), py::arg("y"), py::arg("mean"), py::arg("rstd"),

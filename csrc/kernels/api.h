@@ -62,6 +62,7 @@ struct IGemmArgs {
   float* stats;              // [2][N]: finalized (mean, biased var) of the bf16 output
   const float* stats_shift;  // per-column shift K for the sums (BN running mean) or null
   float* stats_sums;         // [2][N] final sums: zeroed by the epilogue's mt == 0 blocks
+  int stats_ld;              // row stride of the finalized [2][N] statistics (0: N)
   int relu;
   int ktiles_per_split;
   int tiles_n;
@@ -190,7 +191,8 @@ bool dense_gacc_ok(const IGemmArgs& a);
 void dense_gacc(IGemmArgs a, float* slab, float* sums, hipStream_t s);
 void bn_defer_step(const float* sums, const float* gamma, const float* mean, const float* rstd,
                    int Ci, int s0, int M, float* k12, int ldk, float* dgamma, float* dbeta,
-                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, hipStream_t s);
+                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, bf16_raw* out,
+                   hipStream_t s);
 // MPA_DETERMINISTIC: fixed-order cross-block reductions, no timing-based tile autotuning
 void set_deterministic(int on);
 bool deterministic();
@@ -198,7 +200,7 @@ bool deterministic();
 // slab [S][2C] of shifted (sum, sumsq) rows -> sums [2C] and out [mean(C), var(C)] (the
 // slab may be folded in place); replaces slab_reduce + stats_finalize
 void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sums, float* out,
-                hipStream_t s);
+                hipStream_t s, int out_ld = 0);
 void stats_finalize(const float* sums, const float* shift, int M, int C, float* out,
                     hipStream_t s);
 void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats, float* ws,

@@ -698,7 +698,7 @@ __global__ __launch_bounds__(64 * SG) void slab_stats_kernel(const float* __rest
                                                               int S, int rstep, int C,
                                                               const float* __restrict__ shift,
                                                               int M, float* __restrict__ sums,
-                                                              float* __restrict__ out) {
+                                                              float* __restrict__ out, int ld) {
   __shared__ float red[2][64 * SG];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -721,12 +721,12 @@ __global__ __launch_bounds__(64 * SG) void slab_stats_kernel(const float* __rest
     const float d = a * inv;  // mean of (x - K)
     const float k = shift ? shift[c] : 0.f;
     out[c] = k + d;
-    out[C + c] = fmaxf(b * inv - d * d, 0.f);
+    out[ld + c] = fmaxf(b * inv - d * d, 0.f);
   }
 }
 
 void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sums, float* out,
-                hipStream_t s) {
+                hipStream_t s, int out_ld) {
   int rstep = 1, rows = S;
   if (S > 256) {  // fold to <= 64 chunk heads (one launch up to 256 rows: halo-conv slabs)
     const int chunk = (S + 63) / 64;
@@ -736,7 +736,7 @@ void slab_stats(float* slab, int S, int C, const float* shift, int M, float* sum
                        S, 2 * C, chunk);
   }
   hipLaunchKernelGGL(slab_stats_kernel, dim3((C + 63) / 64), dim3(64 * SG), 0, s, slab, rows,
-                     rstep, C, shift, M, sums, out);
+                     rstep, C, shift, M, sums, out, out_ld > 0 ? out_ld : C);
 }
 
 // ----------------------------------------------- BN + ReLU + max-pool (network stems)
@@ -1197,7 +1197,7 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
     const float* __restrict__ mean, const float* __restrict__ rstd, int Ci, int s0, int M,
     float invM, float* __restrict__ k12, int ldk, float* __restrict__ dgamma,
     float* __restrict__ dbeta, void* __restrict__ G, int ldg, const bf16_t* __restrict__ x,
-    int ldx) {
+    int ldx, bf16_t* __restrict__ out) {
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < Ci; c += 256) {
       const float sg = sums[c], sgx = sums[Ci + c];
@@ -1235,13 +1235,19 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
       for (int j = 0; j < 4; ++j) { g0[j] += d[j]; g1[j] += d[4 + j]; }
       gp[0] = g0;
       gp[1] = g1;
+      if (out) {
+        float gv[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        *(uint4*)(out + (size_t)m * (Ci - s0) + (c0 - s0)) = pack8(gv);
+      }
     } else {
       uint4* gp = (uint4*)((bf16_t*)G + (size_t)m * ldg + c0);
       float gv[8];
       unpack8(*gp, gv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] += d[j];
-      *gp = pack8(gv);
+      const uint4 pk = pack8(gv);
+      *gp = pk;
+      if (out) *(uint4*)(out + (size_t)m * (Ci - s0) + (c0 - s0)) = pk;
     }
   }
 }
@@ -1435,16 +1441,17 @@ void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, c
 namespace mpa {
 void bn_defer_step(const float* sums, const float* gamma, const float* mean, const float* rstd,
                    int Ci, int s0, int M, float* k12, int ldk, float* dgamma, float* dbeta,
-                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, hipStream_t s) {
+                   void* G, bool g_f32, int ldg, const bf16_raw* x, int ldx, bf16_raw* out,
+                   hipStream_t s) {
   const int cg = (Ci - s0) / 8, rpp = 256 / cg;
   const int blocks = std::max(1, std::min(2048, (M + rpp - 1) / rpp));
   if (g_f32)
     hipLaunchKernelGGL(bn_defer_step_kernel<true>, dim3(blocks), dim3(256), 0, s, sums, gamma,
                        mean, rstd, Ci, s0, M, 1.f / (float)M, k12, ldk, dgamma, dbeta, G, ldg,
-                       (const bf16_t*)x, ldx);
+                       (const bf16_t*)x, ldx, (bf16_t*)out);
   else
     hipLaunchKernelGGL(bn_defer_step_kernel<false>, dim3(blocks), dim3(256), 0, s, sums, gamma,
                        mean, rstd, Ci, s0, M, 1.f / (float)M, k12, ldk, dgamma, dbeta, G, ldg,
-                       (const bf16_t*)x, ldx);
+                       (const bf16_t*)x, ldx, (bf16_t*)out);
 }
 }  // namespace mpa

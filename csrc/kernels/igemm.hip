@@ -811,6 +811,7 @@ static void tuned_rows_tile(const IGemmArgs& a, bool bkc, int vw, bool allow_spl
     b.C = scr;
     float* slab = (float*)(scr + cbytes);
     if (a.stats) b.stats = slab + igemm_slab_floats(a.M, a.N);  // [2][N] after the slab
+    b.stats_ld = 0;
     float* ws = sp > 1 ? (float*)(scr + cbytes + sbytes) : nullptr;
     if (!allow_split) ws = nullptr;
     else if (!ws) ws = (float*)(scr + cbytes + sbytes);  // (unused: no split)
@@ -830,7 +831,7 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     float* sums = stats ? slab + slab_rows_max(a.M) * 2 * a.N : nullptr;
     a.stats = stats ? slab : nullptr;
     const int rows = conv_stem(a, s);
-    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s);
+    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s, a.stats_ld);
     return;
   }
   if (dma && bkc && conv3_halo_ok(a)) {  // 3x3 / stride 1: halo-staged direct conv
@@ -839,7 +840,7 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     a.stats = stats ? slab : nullptr;
     a.stats_sums = sums;
     const int rows = conv3_halo(a, s);
-    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s);
+    if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s, a.stats_ld);
     return;
   }
   int tbm = 0, tbn = 0;
@@ -892,7 +893,7 @@ static void rows_run_plan(IGemmArgs a, bool bkc, int vw, float* ws, float* slab,
                          stats ? slab : (float*)nullptr, a.stats_shift, sums, a.beta);
     slab_rows = gy;
   }
-  if (stats) slab_stats(slab, slab_rows, a.N, a.stats_shift, a.M, sums, stats, s);
+  if (stats) slab_stats(slab, slab_rows, a.N, a.stats_shift, a.M, sums, stats, s, a.stats_ld);
 }
 
 // `a.stats` (if set) receives the finalized per-column statistics [mean(N), var(N)]

@@ -30,14 +30,15 @@ class _DenseLayer(nn.Module):
         x = feats[0] if len(feats) == 1 else Fn.cat_channels(feats)
         return self.tail(self.norm1(x, relu=True))
 
-    def tail(self, x, stats=None, shift=None, link=None):
+    def tail(self, x, stats=None, shift=None, link=None, out=None):
         """conv1 -> norm2 -> relu -> conv2 of the normalised input; ``stats`` receives the
         output's [mean | var] from conv2's epilogue; ``link`` (Fn.BNLink) describes norm1 for
-        the fused conv1-dgrad / norm1-backward hand-off."""
+        the fused conv1-dgrad / norm1-backward hand-off; ``out``: a channel window of the
+        block buffer conv2 writes into."""
         z = Fn.conv_bn_act(x, self.conv1, self.norm2, relu=True, link_in=link)
         if stats is None:
             return self.conv2(z)
-        return Fn.conv_act(z, self.conv2, stats=stats, shift=shift)
+        return Fn.conv_act(z, self.conv2, stats=stats, shift=shift, out=out)
 
 
 # MPA_DENSE_BLOCK_GRAD=0: per-layer concats under plain autograd (one split and one
@@ -55,6 +56,19 @@ _GRAD_BF16 = os.environ.get("MPA_DENSE_GRAD_BF16", "1") == "1"
 # tensor, no norm1 reduce / apply passes over the O(L^2) channel prefixes.
 # MPA_DENSE_DEFER=0 restores the per-layer bn_bwd(gacc=G).
 _DEFER = os.environ.get("MPA_DENSE_DEFER", "1") == "1"
+# conv2 writes each new feature (and its statistics) into the block buffer / table in place,
+# and bn_defer_step hands the finished gradient slice to its consumer - no channel inserts
+# or slice copies.  MPA_DENSE_DIRECT=0 restores the copies.
+_DIRECT = os.environ.get("MPA_DENSE_DIRECT", "1") == "1"
+
+
+def _window(buf: torch.Tensor, c0: int, n: int) -> torch.Tensor:
+    """buf[..., c0:c0 + n] as a plain alias of buf's storage, not an autograd view: conv2's
+    custom Function returns it as its output, and the other layers' writes into buf must
+    not count as in-place modifications of that output's base."""
+    v = buf[..., c0:c0 + n]
+    return torch.empty(0, dtype=buf.dtype, device=buf.device).set_(
+        buf.untyped_storage(), v.storage_offset(), v.shape, v.stride())
 
 
 def _defer_ok(c0: int, growth: int) -> bool:
@@ -157,7 +171,10 @@ class _DenseBlockGrad(torch.autograd.Function):
                                             channels=ci)
             leaf = y1.requires_grad_(True)
             g = layer.conv2.weight.shape[0]
-            st = torch.empty(2, g, dtype=torch.float32, device=x.device)
+            # conv2 writes its output and its statistics straight into the buffer / table
+            direct = _DIRECT and g % 8 == 0
+            st = S[:, ci:ci + g] if direct else torch.empty(2, g, dtype=torch.float32,
+                                                             device=x.device)
             nxt = layers[li + 1].norm1.running_mean[ci:ci + g] if li + 1 < len(layers) else None
             link = None
             if defer and n1.weight is not None and n1.bias is not None:
@@ -165,9 +182,10 @@ class _DenseBlockGrad(torch.autograd.Function):
                 link.z, link.mean, link.rstd = buf, mean, rstd
                 link.gamma, link.beta = n1.weight, n1.bias
             with torch.enable_grad():  # the new feature's statistics from conv2's epilogue
-                out = layer.tail(leaf, st, nxt, link)
-            k.chan_insert(buf, ci, out.detach())
-            k.chan_insert(S, ci, st)
+                out = layer.tail(leaf, st, nxt, link, _window(buf, ci, g) if direct else None)
+            if not direct:
+                k.chan_insert(buf, ci, out.detach())
+                k.chan_insert(S, ci, st)
             recs.append((leaf, out, mean, rstd, ci, link))
             ci += g
         ctx.block = block
@@ -196,11 +214,15 @@ class _DenseBlockGrad(torch.autograd.Function):
         if any(r[5] is not None for r in ctx.recs):
             k12 = torch.empty(2, G.shape[-1], dtype=torch.float32, device=G.device)
             k.zero_f32(k12)
+        ready = dx_ready = None  # finished slices handed over by bn_defer_step
         for i in range(len(ctx.recs) - 1, -1, -1):
             leaf, out, mean, rstd, ci, link = ctx.recs[i]
             g = out.shape[-1]
-            g_out = (k.chan_slice(G, ci, g) if _GRAD_BF16 else
-                     k.chan_extract(G, ci, g).to(out.dtype))
+            if ready is not None:
+                g_out, ready = ready, None
+            else:
+                g_out = (k.chan_slice(G, ci, g) if _GRAD_BF16 else
+                         k.chan_extract(G, ci, g).to(out.dtype))
             if link is not None:
                 link.gacc = G
             torch.autograd.backward(out, g_out)
@@ -212,8 +234,15 @@ class _DenseBlockGrad(torch.autograd.Function):
                 # corrections and finish the channels no earlier layer reads: layer i-1's
                 # output (ci - growth .. ci), or the block input for layer 0
                 s0 = 0 if i == 0 else ci - ctx.recs[i - 1][1].shape[-1]
+                nxt = None
+                if _DIRECT and _GRAD_BF16:  # the finished slice, contiguous, for its consumer
+                    nxt = G.new_empty(G.shape[:-1] + (ci - s0,))
                 k.bn_defer_step(link.sums, gamma, mean, rstd, s0, k12, Fn._sink(gamma, G),
-                                Fn._sink(beta, G), G, buf)
+                                Fn._sink(beta, G), G, buf, nxt)
+                if i > 0:
+                    ready = nxt
+                else:
+                    dx_ready = nxt
                 link.sums = link.gacc = link.z = None
             elif link is not None:
                 raise RuntimeError("dense block: conv1's fused BN-backward hand-off did not run "
@@ -223,8 +252,11 @@ class _DenseBlockGrad(torch.autograd.Function):
                          Fn._sink(gamma, dy), Fn._sink(beta, dy), True, False, beta, gacc=G)
             Fn._done(gamma, beta)
             ctx.recs[i] = None
-        dx = (k.chan_slice(G, 0, ctx.c0) if _GRAD_BF16 else
-              k.chan_extract(G, 0, ctx.c0).to(gy.dtype))
+        if dx_ready is not None:
+            dx = dx_ready
+        else:
+            dx = (k.chan_slice(G, 0, ctx.c0) if _GRAD_BF16 else
+                  k.chan_extract(G, 0, ctx.c0).to(gy.dtype))
         ctx.buf = None
         return (dx, None) + (None,) * ctx.nparams
 

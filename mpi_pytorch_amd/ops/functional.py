@@ -490,11 +490,16 @@ def conv_bn_relu_maxpool(x, conv, bn, pool):
 # ============================================================================ conv + bias
 class _ConvAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, conv, relu, join=None, stats=None, shift=None):
+    def forward(ctx, x, w, b, conv, relu, join=None, stats=None, shift=None, out=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
-        y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu,
-                       _or_empty(stats, x), _or_empty(shift, x))
+        if out is not None:  # written straight into a channel window of a wider buffer
+            k.conv_fwd_into(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu,
+                            _or_empty(stats, x), _or_empty(shift, x), out)
+            y = out
+        else:
+            y = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, relu,
+                           _or_empty(stats, x), _or_empty(shift, x))
         ctx.conv = conv
         ctx.relu = relu
         ctx.params = (w, b)
@@ -520,17 +525,20 @@ class _ConvAct(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _dgrad_joined(k, ctx.join, g, weight_of(w), ctx.in_hw, conv, weight_t_of(w))
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def conv_act(x, conv, relu: bool = False, join: Optional[GradJoin] = None,
-             stats: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None):
+             stats: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None):
     """act(conv(x) + b); ``join``: x's gradient is summed with its other consumers' (see
     GradJoin); ``stats`` ([2, N] fp32, training): receives the output's per-channel
-    [mean | var] from the GEMM epilogue (sums shifted by ``shift`` for precision)."""
+    [mean | var] from the GEMM epilogue (sums shifted by ``shift`` for precision); ``out``
+    (training): a channel window of a wider NHWC buffer the output is written into (the
+    result is that window; ``stats`` may then be a [2, N] window of a wider table)."""
     x = conv.fit_input(x)
     if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
-        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu, join, stats, shift)
+        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu, join, stats, shift, out)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,

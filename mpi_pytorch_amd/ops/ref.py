@@ -261,7 +261,7 @@ def conv_dgrad_bnred_gacc(dz, w, wt, zbuf, mean, rstd, gamma, beta, G):
     return torch.cat([g.sum(0), (g * xhat).sum(0)])
 
 
-def bn_defer_step(sums, gamma, mean, rstd, s0, k12, dgamma, dbeta, G, x):
+def bn_defer_step(sums, gamma, mean, rstd, s0, k12, dgamma, dbeta, G, x, out=None):
     """Fold a dense layer's norm1 sums into the block's deferred corrections k12 [2, Ctot]
     (channels < s0) and the (gamma, beta) gradients, and apply the final correction
     G += K1 + K2 * xhat to the channels [s0, Ci)."""
@@ -282,6 +282,19 @@ def bn_defer_step(sums, gamma, mean, rstd, s0, k12, dgamma, dbeta, G, x):
     xhat = (xs - mean[s0:Ci]) * rstd[s0:Ci]
     Gv = G[..., s0:Ci]
     Gv.copy_((Gv.float() + k1 + k2 * xhat).to(G.dtype))
+    if out is not None and out.numel():
+        out.copy_(Gv.to(out.dtype))
+
+
+def conv_fwd_into(x, w, bias, sh, sw, ph, pw, relu, stats, shift, out):
+    """conv_fwd writing into ``out`` (a channel window of a wider buffer); ``stats`` may be
+    a [2, K] window of a wider table."""
+    st = _opt(stats)
+    tmp = torch.empty(2, w.shape[0], dtype=torch.float32) if st is not None else stats
+    y = conv_fwd(x, w, bias, sh, sw, ph, pw, relu, tmp, shift)
+    out.copy_(y)
+    if st is not None:
+        st.copy_(tmp)
 
 
 # ---------------------------------------------------------------------------------- pool
