@@ -60,6 +60,8 @@ _DEFER = os.environ.get("MPA_DENSE_DEFER", "1") == "1"
 # and bn_defer_step hands the finished gradient slice to its consumer - no channel inserts
 # or slice copies.  MPA_DENSE_DIRECT=0 restores the copies.
 _DIRECT = os.environ.get("MPA_DENSE_DIRECT", "1") == "1"
+# Transition: average-pool before the 1x1 conv (MPA_DENSE_POOL_FIRST=0: torchvision order)
+_POOL_FIRST = os.environ.get("MPA_DENSE_POOL_FIRST", "1") == "1"
 
 
 def _window(buf: torch.Tensor, c0: int, n: int) -> torch.Tensor:
@@ -270,7 +272,13 @@ class _Transition(nn.Sequential):
         self.pool = AvgPool2d(2, 2)
 
     def forward(self, x, stats=None):
+        """norm -> relu -> conv1x1 -> avgpool2x2 as torchvision, with the (linear) average
+        pool commuted ahead of the (linear, bias-free) 1x1 conv: the same function, and the
+        conv's forward / dgrad / wgrad run on a quarter of the pixels (the pool then sees
+        the wider input - 2x the channels - which costs far less)."""
         x = self.norm(x, relu=True, stats=stats)
+        if _POOL_FIRST:
+            return self.conv(self.pool(x))
         return self.pool(self.conv(x))
 
 

@@ -394,3 +394,25 @@ def test_inception_fused_stem_pools_equal_modules():
     assert torch.allclose(o1, o2, atol=1e-5)
     assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
+def test_densenet_transition_pool_first_equals_torchvision_order(monkeypatch):
+    """The transition's average pool commuted ahead of its bias-free 1x1 conv (both linear)
+    gives torchvision's norm -> relu -> conv -> pool output and gradients (fp32, CPU)."""
+    from mpi_pytorch_amd.models import densenet as dn
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("densenet", 10, torch.device("cpu"), World(), 1e-3)
+    tr = model.features.transition1
+    x0 = torch.randn(2, 8, 8, tr.norm.num_features)
+    res = []
+    for first in (True, False):
+        monkeypatch.setattr(dn, "_POOL_FIRST", first)
+        model._mpa_arena.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        y = tr(x)
+        y.square().sum().backward()
+        res.append((y.detach(), x.grad.clone(), model._mpa_arena.grad.clone()))
+    (y1, gx1, g1), (y2, gx2, g2) = res
+    assert torch.allclose(y1, y2, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(gx1, gx2, atol=1e-5, rtol=1e-4)
+    assert float((g1 - g2).abs().max()) < 1e-4 * float(g2.abs().max())
