@@ -544,8 +544,14 @@ struct HaloWPlan {
 
 // W2T: the halo pitch as a compile-time constant (16 / 32 / 48 / 64: every ResNet and
 // Inception size), so a tap's row offset is an immediate DS offset; 0 = runtime pitch.
-template <int W2T>
+// ONECH (C == 32, images too wide for a 448-pixel halo, e.g. Inception's 147 x 147
+// Conv2d_2b): the partition's second channel chunk does not exist, so the two chunk areas
+// of a stage hold ONE 896-pixel halo image of the first chunk (14 DMA instructions per
+// wave instead of 2 x 7).  Waves 2 and 3 then read chunk 0 as well; their partials are
+// duplicates of waves 0 / 1 and are not stored.
+template <int W2T, bool ONECH = false>
 __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
+  constexpr int HIW = ONECH ? 2 * HW_HIW : HW_HIW;  // halo DMA instructions per wave (chunk)
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -571,10 +577,10 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   }
   // halo: instruction j = pixels 16 (7 wave + j) + lane/4 of the image; chunk 1 of the
   // partition is the same lanes with the descriptor base 64 B further
-  uint32_t hsc[HW_HIW];
+  uint32_t hsc[HIW];
 #pragma unroll
-  for (int j = 0; j < HW_HIW; ++j) {
-    const uint32_t hp = 16 * (wave * HW_HIW + j) + (lane >> 2);
+  for (int j = 0; j < HIW; ++j) {
+    const uint32_t hp = 16 * (wave * HIW + j) + (lane >> 2);
     const uint32_t sl = udiv(hp, h.mag_w2);
     const uint32_t colp = hp - sl * W2;
     const uint32_t lc = (lane & 3) ^ (((hp >> 3) & 1) << 1);
@@ -586,7 +592,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   // (C % 64 == 32: the last channel partition's second chunk is an empty buffer: zeros)
   const __amdgpu_buffer_rsrc_t rx1 =
       make_rsrc((const char*)p.x + 64, c0 + 32 < C ? h.x_bytes : 0u);
-  uint32_t hv[HW_HIW], dv[4];
+  uint32_t hv[HIW], dv[4];
   // this wave's 16 channels: chunk (wave >> 1) of the halo, 16-B chunks 2 (wave & 1) + pp/2
   const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
   // B-row addresses per (k-step, lo/hi, column tap dw): the swizzle bit is pixel bit 3,
@@ -599,7 +605,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     const int r0 = m0 - img0 * HW;
     const int oh0 = r0 / W;
 #pragma unroll
-    for (int j = 0; j < HW_HIW; ++j) {
+    for (int j = 0; j < HIW; ++j) {
       const int sl = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
       const int v = sl + oh0 - 1;
       const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;
@@ -638,6 +644,9 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     const uint32_t st = sw + stage * HW_STAGE;
     if (j < 4) {
       buf_lds16_at(rdy, st + j * 1024, dv[j]);
+    } else if constexpr (ONECH) {
+      const int jj = j - 4;
+      buf_lds16_at(rx0, st - wave * 4096 + HW_DBYTES + (wave * HIW + jj) * 1024, hv[jj]);
     } else {
       const int ch = (j - 4) / HW_HIW, jj = (j - 4) % HW_HIW;
       buf_lds16_at(ch ? rx1 : rx0, st - wave * 4096 + HW_DBYTES + ch * HW_HBYTES +
@@ -655,7 +664,7 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[km][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int hoff = HW_DBYTES + (wave >> 1) * HW_HBYTES;
+  const int hoff = HW_DBYTES + (ONECH ? 0 : (wave >> 1) * HW_HBYTES);
   if (ntiles > 0) {
     prep(z);
     issue(0);
@@ -920,7 +929,16 @@ static bool halo_wgrad_geom(const WGradArgs& a) {
     return false;
   const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
   const int64_t seps = (HW_BM - 1) / HW + 1;
-  return (rows + 2 + seps) * halo_wgrad_pitch(a.W) <= HW_HPX;
+  // 32-channel partitions may use both chunk areas for one wider halo image (ONECH)
+  return (rows + 2 + seps) * halo_wgrad_pitch(a.W) <= (a.C == 32 ? 2 : 1) * HW_HPX;
+}
+
+// one 32-channel chunk whose halo needs the combined image
+static bool halo_wgrad_onech(const WGradArgs& a) {
+  const int64_t HW = (int64_t)a.H * a.W;
+  const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
+  const int64_t seps = (HW_BM - 1) / HW + 1;
+  return a.C == 32 && (rows + 2 + seps) * halo_wgrad_pitch(a.W) > HW_HPX;
 }
 
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols) {
@@ -951,6 +969,10 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
   h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
   const dim3 grid(h.parts * h.Z), blk(256);
+  if (halo_wgrad_onech(a)) {
+    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, true>), grid, blk, 0, s, a, h);
+    return h.Z;
+  }
   switch (W2) {
     case 16: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<16>, grid, blk, 0, s, a, h); break;
     case 32: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<32>, grid, blk, 0, s, a, h); break;

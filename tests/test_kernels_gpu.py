@@ -224,6 +224,8 @@ HALO_CASES = [
     (3, 7, 7, 128, 32),      # DenseNet block 4: 32-wide, tiles across many 7x7 images
     (2, 17, 17, 32, 64),     # 32-channel wgrad partition (second halo chunk empty)
     (2, 9, 9, 96, 96),       # wgrad K and C with a 32-wide remainder partition
+    (2, 40, 70, 32, 64),     # 32-channel wgrad, halo wider than one chunk area (ONECH)
+    (1, 147, 147, 32, 64),   # Inception Conv2d_2b (ONECH wgrad)
 ]
 
 

@@ -17,7 +17,8 @@ CATS = [
     ("conv (stem)", r"conv_stem"),
     ("conv fwd/dgrad (halo)", r"conv3_halo_kernel"),
     ("conv/GEMM fwd/dgrad (igemm)", r"igemm_rows|igemm_kernel|igemm_dma|gemm"),
-    ("BN backward", r"bn_bwd|maxpool_bn_bwd|slab_reduce|act_bwd"),
+    ("conv1 dgrad + norm1 bwd (dense_gacc)", r"dense_gacc"),
+    ("BN backward", r"bn_bwd|maxpool_bn_bwd|slab_reduce|act_bwd|bn_defer"),
     ("BN forward + stats", r"bn_fwd|bn_stats|slab_stats|slab_fold|bn_relu_maxpool|relu_kernel"),
     ("concat / channel copy", r"concat|chan_accum|chan_extract"),
     ("pooling", r"pool|adaptive"),
