@@ -773,10 +773,19 @@ static std::string rows_key(const IGemmArgs& a, bool bkc, bool split) {
   return key;
 }
 
-static const int kRowsCands[][2] = {{128, 128}, {256, 128}, {128, 64}, {256, 64}, {128, 32}};
+static const int kRowsCands[][2] = {{128, 128}, {256, 128}, {128, 64}, {256, 64}, {128, 32},
+                                    {256, 256}};
+
+// MPA_TUNE_256=1 adds the 8-wave 256 x 256 tile to the rows autotuner's candidates.  Off:
+// same-box A/B, round 3 - ResNet-18 b1024 47.73k/47.89k vs 47.67k/47.85k img/s, Inception
+// 7.24k vs 7.26k, ResNet-34 25.35k vs 25.39k (noise), for a longer first-step tuning pass.
+static const bool g_tune256 = [] {
+  const char* e = getenv("MPA_TUNE_256");
+  return e && atoi(e) == 1;
+}();
 
 static bool rows_cand_ok(int bm, int bn, int N) {
-  (void)bm;
+  if (bm == 256 && bn == 256 && (!g_tune256 || N <= 128)) return false;
   if (bn == 128 && N <= 64) return false;  // half-empty tiles
   if (bn == 64 && (N <= 32 || N > 1024)) return false;
   if (bn == 32 && N > 32) return false;
