@@ -370,8 +370,9 @@ Tensor conv_dgrad_bnred_gacc(Tensor dz, Tensor w, Tensor wt, Tensor zbuf, Tensor
 
 // see mpa::bn_defer_step (bn.hip): fold layer sums into the block's deferred-correction
 // table k12 [2, Ctot] and apply the final correction to G's channels [s0, Ci)
-// out (optional, bf16 contiguous [..., Ci - s0]): also receives the finished slice (the
-// gradient its consumer reads), so no separate slice copy is needed
+// out (optional, bf16 contiguous [..., Ci - s0]): receives the finished slice (the gradient
+// its consumer reads) INSTEAD of G's channels [s0, Ci), which nothing reads again - no
+// separate slice copy, no write-back
 void bn_defer_step(Tensor sums, Tensor gamma, Tensor mean, Tensor rstd, int64_t s0, Tensor k12,
                    Tensor dgamma, Tensor dbeta, Tensor G, Tensor x, c10::optional<Tensor> out) {
   CHECK_CUDA(G);

@@ -1233,11 +1233,12 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
       f32x4 g0 = gp[0], g1 = gp[1];
 #pragma unroll
       for (int j = 0; j < 4; ++j) { g0[j] += d[j]; g1[j] += d[4 + j]; }
-      gp[0] = g0;
-      gp[1] = g1;
-      if (out) {
+      if (out) {  // the finished slice goes to its consumer only: G's copy is never read again
         float gv[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
         *(uint4*)(out + (size_t)m * (Ci - s0) + (c0 - s0)) = pack8(gv);
+      } else {
+        gp[0] = g0;
+        gp[1] = g1;
       }
     } else {
       uint4* gp = (uint4*)((bf16_t*)G + (size_t)m * ldg + c0);
@@ -1246,8 +1247,8 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) gv[j] += d[j];
       const uint4 pk = pack8(gv);
-      *gp = pk;
       if (out) *(uint4*)(out + (size_t)m * (Ci - s0) + (c0 - s0)) = pk;
+      else *gp = pk;
     }
   }
 }

@@ -281,9 +281,11 @@ def bn_defer_step(sums, gamma, mean, rstd, s0, k12, dgamma, dbeta, G, x, out=Non
     xs = _f(x[..., s0:Ci])
     xhat = (xs - mean[s0:Ci]) * rstd[s0:Ci]
     Gv = G[..., s0:Ci]
-    Gv.copy_((Gv.float() + k1 + k2 * xhat).to(G.dtype))
-    if out is not None and out.numel():
-        out.copy_(Gv.to(out.dtype))
+    fin = (Gv.float() + k1 + k2 * xhat).to(G.dtype)
+    if out is not None and out.numel():  # the consumer's copy only (G's is never read again)
+        out.copy_(fin.to(out.dtype))
+    else:
+        Gv.copy_(fin)
 
 
 def conv_fwd_into(x, w, bias, sh, sw, ph, pw, relu, stats, shift, out):

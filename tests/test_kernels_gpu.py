@@ -415,6 +415,7 @@ def test_dense_deferred_norm1_backward(gpu, gdt):
     assert torch.equal(G[..., Ci:], G0[..., Ci:])  # channels past the prefix untouched
     for s0 in (224, 0):  # a 32-channel slice (layer i > 0), the whole prefix (layer 0)
         k12 = torch.randn(2, ctot, device=gpu)
+        k12_0 = k12.clone()
         dg, db = torch.zeros(Ci, device=gpu), torch.zeros(Ci, device=gpu)
         k12r, dgr, dbr = k12.clone(), dg.clone(), db.clone()
         G1, G1r = G.clone(), G.clone()
@@ -424,6 +425,13 @@ def test_dense_deferred_norm1_backward(gpu, gdt):
         assert rel(G1, G1r) < 1e-2 and rel(k12, k12r) < 1e-5
         assert rel(dg, dgr) < 1e-5 and rel(db, dbr) < 1e-5
         assert torch.equal(G1[..., :s0], G[..., :s0]) and torch.equal(G1[..., Ci:], G[..., Ci:])
+        # handover form: the finished slice goes to `out` (G's copy left as it was)
+        G2 = G.clone()
+        o = torch.empty(N, H, W, Ci - s0, device=gpu, dtype=torch.bfloat16)
+        e = torch.empty(0, device=gpu)
+        C().bn_defer_step(sums, gamma, mean, rstd, s0, k12_0, e, e, G2, buf, o)
+        torch.cuda.synchronize()
+        assert torch.equal(G2, G) and rel(o, G1r[..., s0:Ci]) < 1e-2
 
 
 def test_conv_halo_repeatable(gpu):
