@@ -520,10 +520,12 @@ static std::vector<int64_t> with_last(const Tensor& x, int64_t c) {
   return shape;
 }
 
+// res_affine (optional, fp32 [2, C] = scale | shift): the residual's own BN applied as it
+// is read (bn_stats_affine of a deferred BN), so res holds that BN's raw input
 std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
                                  Tensor rvar, double momentum, double eps, Tensor res, bool relu,
                                  c10::optional<Tensor> counter, c10::optional<Tensor> mask,
-                                 int64_t channels) {
+                                 int64_t channels, c10::optional<Tensor> res_affine) {
   int C, ldx, M;
   bn_prefix(x, channels, &C, &ldx, &M);
   const c10::OptionalDeviceGuard g(device_of(x));
@@ -550,6 +552,11 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
   }
   Tensor y = torch::empty(with_last(x, C), x.options());
   if (has(res)) TORCH_CHECK(res.numel() == y.numel(), "bn_fwd_train: residual shape");
+  const float* raff = nullptr;
+  if (res_affine && res_affine->defined() && res_affine->numel() > 0) {
+    TORCH_CHECK(has(res) && res_affine->numel() == 2 * C, "bn_fwd_train: res_affine [2, C]");
+    raff = fopt(*res_affine);
+  }
   Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
   Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
   mpa::bn_fwd_train(bp(x), st.data_ptr<float>(), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
@@ -557,8 +564,31 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
                     mean.data_ptr<float>(), rstd.data_ptr<float>(),
                     (counter && counter->defined() && counter->numel() == 1)
                         ? counter->data_ptr<int64_t>() : nullptr,
-                    cur_stream(), ymask_ptr(mask, y), ldx, lds);
+                    cur_stream(), ymask_ptr(mask, y), ldx, lds, raff);
   return {y, mean, rstd};
+}
+
+// a train-mode BN's statistics half (see mpa::bn_stats_affine): returns mean, rstd and the
+// [2, C] affine its consumer applies (bn_fwd_train(res_affine=)).  x is the BN input
+// (unused here: the statistics are finalized already; the CPU oracle recomputes them)
+std::vector<Tensor> bn_stats_affine(Tensor x, Tensor stats, Tensor gamma, Tensor beta,
+                                    Tensor rmean, Tensor rvar, double momentum, double eps,
+                                    c10::optional<Tensor> counter) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(has(stats) && stats.numel() == 2 * C, "bn_stats_affine: stats [2, C]");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor mean = torch::empty({C}, x.options().dtype(torch::kFloat32));
+  Tensor rstd = torch::empty({C}, x.options().dtype(torch::kFloat32));
+  Tensor aff = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
+  mpa::bn_stats_affine(fopt(stats), fopt(gamma), fopt(beta), fopt_mut(rmean), fopt_mut(rvar),
+                       (float)momentum, (float)eps, M, C, mean.data_ptr<float>(),
+                       rstd.data_ptr<float>(), aff.data_ptr<float>(),
+                       (counter && counter->defined() && counter->numel() == 1)
+                           ? counter->data_ptr<int64_t>() : nullptr,
+                       cur_stream());
+  return {mean, rstd, aff};
 }
 
 // per-channel batch statistics [2, C] = [mean | biased var] of x [..., C] (shift: optional
@@ -1327,7 +1357,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
         py::arg("res"), py::arg("relu"), py::arg("counter") = py::none(),
-        py::arg("mask") = py::none(), py::arg("channels") = 0);
+        py::arg("mask") = py::none(), py::arg("channels") = 0,
+        py::arg("res_affine") = py::none());
+  m.def("bn_stats_affine", &bn_stats_affine, py::arg("x"), py::arg("stats"), py::arg("gamma"),
+        py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
+        py::arg("eps"), py::arg("counter") = py::none());
   m.def("bn_stats", &bn_stats, "[mean | biased var] of x [..., C]");
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("eps"), py::arg("res"), py::arg("relu"),

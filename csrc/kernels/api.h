@@ -211,7 +211,13 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
                   int64_t* counter, hipStream_t s,  // counter (num_batches_tracked) += 1
                   uint8_t* ymask = nullptr,  // optional ReLU bit mask of y ([M*C/8] bytes)
                   int ldx = 0,   // x row stride (0: C) - a channel prefix of a wider buffer
-                  int lds = 0);  // stats = [mean | var] rows lds apart (0: C)
+                  int lds = 0,   // stats = [mean | var] rows lds apart (0: C)
+                  const float* res_aff = nullptr);  // [2][C]: res enters as res * aff0 + aff1
+// mean / rstd / running stats / num_batches_tracked of a train-mode BN whose apply pass is
+// deferred to its consumer; aff [2][C] = [gamma rstd | beta - mean gamma rstd]
+void bn_stats_affine(const float* stats, const float* gamma, const float* beta, float* rmean,
+                     float* rvar, float momentum, float eps, int M, int C, float* mean,
+                     float* rstd, float* aff, int64_t* counter, hipStream_t s);
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s, int ldx = 0);

@@ -209,13 +209,18 @@ __device__ __forceinline__ uint32_t posmask8(uint4 p) {
 // y = relu?(x * sc + sh (+ res)) over this thread's rows; ym (optional): the ReLU mask of y,
 // one bit per element (byte r * C/8 + c0/8), which the backward reads instead of y.  x rows
 // have stride ldx >= C (a channel prefix of a wider buffer: DenseNet's block features)
+// rsc / rsh (optional, this thread's 8 channels): the residual enters as res * rsc + rsh -
+// a residual branch's own BN (ResNet's downsample) applied while it is read, so that BN's
+// output is never written
 template <int UNR, bool YM = false>
 __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, int ldx, int c0,
                                               const float* sc, const float* sh,
                                               const bf16_t* __restrict__ x,
                                               const bf16_t* __restrict__ res, int relu,
                                               bf16_t* __restrict__ y,
-                                              uint8_t* __restrict__ ym = nullptr) {
+                                              uint8_t* __restrict__ ym = nullptr,
+                                              const float* rsc = nullptr,
+                                              const float* rsh = nullptr) {
   sweep_rows_pl<UNR, 2>(
       cm, M,
       [&](int r, uint4 (&v)[2]) {
@@ -231,8 +236,13 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
         if (res) {
           float g[8];
           unpack8(v[1], g);
+          if (rsc) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] += g[j];
+            for (int j = 0; j < 8; ++j) f[j] += __builtin_fmaf(g[j], rsc[j], rsh[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] += g[j];
+          }
         }
         if (relu) {
 #pragma unroll
@@ -251,12 +261,20 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask, int ldx, int lds) {
+    unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask, int ldx, int lds,
+    const float* __restrict__ res_aff) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
+  if (res_aff) {  // [2][C]: the residual's BN scale | shift
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      rsc[j] = res_aff[c0 + j];
+      rsh[j] = res_aff[C + c0 + j];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float mu = stats[c0 + j];       // finalized (mean, biased var); rows lds apart
@@ -272,7 +290,34 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
       rvar[c0 + j] = (1.f - momentum) * rvar[c0 + j] + momentum * unb;
     }
   }
-  bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask);
+  if (res_aff)
+    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask, rsc, rsh);
+  else
+    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask);
+}
+
+// Train-mode BN whose apply pass is deferred to its consumer (bn_fwd_train's res_aff): the
+// batch mean / rstd from finalized statistics, the running-stat update, num_batches_tracked,
+// and the affine [scale | shift] = [gamma rstd | beta - mean gamma rstd] - one thread per
+// channel, same arithmetic as bn_fwd_train
+__global__ __launch_bounds__(256) void bn_stats_affine_kernel(
+    const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, int M, int C, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, float* __restrict__ aff, unsigned long long* __restrict__ counter) {
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float mu = stats[c], var = stats[C + c];
+  const float rs = rsqrtf(var + eps);
+  const float sc = gamma[c] * rs;
+  mean_out[c] = mu;
+  rstd_out[c] = rs;
+  aff[c] = sc;
+  aff[C + c] = __builtin_fmaf(-mu, sc, beta[c]);
+  const float unb = var * ((float)M / (float)max(M - 1, 1));
+  rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+  rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
 }
 
 // -------------------------------------------------------------------- forward (eval)
@@ -1265,17 +1310,26 @@ void bn_stats(const bf16_raw* x, int M, int C, const float* shift, float* stats,
 void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
-                  int64_t* counter, hipStream_t s, uint8_t* ymask, int ldx, int lds) {
+                  int64_t* counter, hipStream_t s, uint8_t* ymask, int ldx, int lds,
+                  const float* res_aff) {
   if (ldx <= 0) ldx = C;
   if (lds <= 0) lds = C;
   if (ymask)
     BN_LAUNCH_T(bn_fwd_train_kernel, true, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
                 momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
-                ldx, lds);
+                ldx, lds, res_aff);
   else
     BN_LAUNCH_T(bn_fwd_train_kernel, false, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
                 momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
-                ldx, lds);
+                ldx, lds, res_aff);
+}
+
+void bn_stats_affine(const float* stats, const float* gamma, const float* beta, float* rmean,
+                     float* rvar, float momentum, float eps, int M, int C, float* mean,
+                     float* rstd, float* aff, int64_t* counter, hipStream_t s) {
+  hipLaunchKernelGGL(bn_stats_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats,
+                     gamma, beta, rmean, rvar, momentum, eps, M, C, mean, rstd, aff,
+                     (unsigned long long*)counter);
 }
 
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,

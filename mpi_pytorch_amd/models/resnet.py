@@ -23,6 +23,8 @@ from ..ops import functional as Fn
 _LINK = os.environ.get("MPA_BN_LINK", "0") == "1"
 # MPA_GRAD_JOIN=0 restores autograd's separate add of the two input-gradient contributions
 _JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
+# MPA_DS_DEFER=0: the downsample BN writes its output (instead of bn2 applying it on read)
+_DS_DEFER = os.environ.get("MPA_DS_DEFER", "1") == "1"
 
 
 class BasicBlock(nn.Module):
@@ -44,15 +46,18 @@ class BasicBlock(nn.Module):
         # x's gradient = conv1's dgrad + the shortcut's: summed inside the second dgrad
         join = Fn.GradJoin() if (self.bn1.training and _JOIN and x.requires_grad) else None
         out = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True, link_out=link, join_x=join)
+        dsd = None
         if self.downsample is not None:
+            # the downsample's BN is applied by bn2 while it reads the residual (Fn.BNDefer)
+            dsd = Fn.BNDefer() if (self.bn2.training and _DS_DEFER) else None
             identity = Fn.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False,
-                                      join_x=join)
+                                      join_x=join, defer=dsd)
             join_res = None
         else:
             identity = x
             join_res = join
         return Fn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=identity,
-                              link_in=link, join_res=join_res)
+                              link_in=link, join_res=join_res, res_defer=dsd)
 
 
 class Downsample(nn.Sequential):

@@ -96,6 +96,20 @@ class BNLink:
         self.gacc = None
 
 
+class BNDefer:
+    """A train-mode BN whose apply pass runs in its one consumer (ResNet's downsample BN,
+    read as bn2's residual): the producing op computes only the statistics half
+    (``bn_stats_affine``: mean, rstd, running stats) and returns the raw conv output; ``aff``
+    ([2, C] scale | shift) is what the consumer's ``bn_fwd_train(res_affine=)`` applies while
+    reading it.  The tensor then stands for the BN output in autograd: the consumer hands
+    back d/d(BN output), which the producer's backward turns into its own BN backward."""
+
+    __slots__ = ("aff",)
+
+    def __init__(self):
+        self.aff = None
+
+
 class GradJoin:
     """Several gradient contributions to ONE activation, summed without separate add passes.
 
@@ -200,7 +214,7 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None,
-                join_x=None, join_res=None):
+                join_x=None, join_res=None, defer=None, res_affine=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
@@ -213,10 +227,17 @@ class _ConvBNAct(torch.autograd.Function):
         ymask = None
         if relu and residual is not None and not _NO_YMASK:
             ymask = torch.empty(z.numel() // 8, device=z.device, dtype=torch.uint8)
-        y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean, bn.running_var,
-                                       bn.momentum_value(), bn.eps,
-                                       _or_empty(residual, x), relu, bn.num_batches_tracked,
-                                       mask=ymask)
+        if defer is not None:  # statistics only; the consumer applies this BN (BNDefer)
+            mean, rstd, defer.aff = k.bn_stats_affine(z, stats, gamma, beta, bn.running_mean,
+                                                      bn.running_var, bn.momentum_value(),
+                                                      bn.eps, bn.num_batches_tracked)
+            y = z
+        else:
+            y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean,
+                                           bn.running_var, bn.momentum_value(), bn.eps,
+                                           _or_empty(residual, x), relu,
+                                           bn.num_batches_tracked, mask=ymask,
+                                           res_affine=res_affine)
         ctx.conv = conv
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -287,12 +308,14 @@ class _ConvBNAct(torch.autograd.Function):
                 dx = _join_grad(ctx.join_x, dx)
             else:
                 dx = _dgrad_joined(k, ctx.join_x, dz, weight_of(w), ctx.in_hw, conv, wt)
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+        return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
+                None)
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None,
                 link_in: Optional[BNLink] = None, link_out: Optional[BNLink] = None,
-                join_x: Optional[GradJoin] = None, join_res: Optional[GradJoin] = None):
+                join_x: Optional[GradJoin] = None, join_res: Optional[GradJoin] = None,
+                defer: Optional[BNDefer] = None, res_defer: Optional[BNDefer] = None):
     """relu(bn(conv(x)) [+ residual]); BN in train or eval mode per ``bn.training``.
 
     A conv bias in front of a train-mode BN (VGG11_bn) is added before the statistics, so
@@ -301,8 +324,13 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
     rounding noise."""
     x = conv.fit_input(x)
     if bn.training:
+        # (defer: bn(conv(x)) without ReLU or residual, a train-mode affine BN)
+        if defer is not None and (relu or residual is not None or bn.weight is None
+                                  or bn.bias is None):
+            defer = None
+        raff = res_defer.aff if res_defer is not None else None
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
-                                bn, relu, link_in, link_out, join_x, join_res)
+                                bn, relu, link_in, link_out, join_x, join_res, defer, raff)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,

@@ -112,8 +112,27 @@ def bitmask_unpack(m, shape):
     return ((m.to(torch.int32).unsqueeze(1) >> bits) & 1).bool().reshape(shape)
 
 
+def bn_stats_affine(x, stats, gamma, beta, rmean, rvar, momentum, eps, counter=None):
+    """Statistics half of a train-mode BN whose apply runs in its consumer: (mean, rstd,
+    [2, C] affine = [gamma rstd | beta - mean gamma rstd]); updates the running stats."""
+    C = x.shape[-1]
+    xf = _f(x).reshape(-1, C)
+    M = xf.shape[0]
+    mean = xf.mean(0)
+    var = xf.var(0, unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    sc = gamma.float() * rstd
+    with torch.no_grad():
+        unbiased = var * (M / max(M - 1, 1))
+        rmean.mul_(1 - momentum).add_(mean, alpha=momentum)
+        rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+        if _opt(counter) is not None:
+            counter.add_(1)
+    return mean, rstd, torch.stack([sc, beta.float() - mean * sc])
+
+
 def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu,
-                 counter=None, mask=None, channels=0):
+                 counter=None, mask=None, channels=0, res_affine=None):
     # the oracle always uses exact two-pass statistics (``stats`` from a fused producer
     # epilogue is accepted for API parity but not needed); channels > 0: BN of the first
     # ``channels`` channels of a wider buffer
@@ -127,7 +146,10 @@ def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, re
     rstd = torch.rsqrt(var + eps)
     y = (xf - mean) * (rstd * gamma) + beta
     if _opt(residual) is not None:
-        y = y + _f(residual).reshape(-1, C)
+        r = _f(residual).reshape(-1, C)
+        if _opt(res_affine) is not None:  # the residual's deferred BN
+            r = r * res_affine[0] + res_affine[1]
+        y = y + r
     if relu:
         y = torch.relu(y)
     with torch.no_grad():

@@ -416,3 +416,31 @@ def test_densenet_transition_pool_first_equals_torchvision_order(monkeypatch):
     assert torch.allclose(y1, y2, atol=1e-5, rtol=1e-5)
     assert torch.allclose(gx1, gx2, atol=1e-5, rtol=1e-4)
     assert float((g1 - g2).abs().max()) < 1e-4 * float(g2.abs().max())
+
+
+def test_resnet_deferred_downsample_bn_equals_materialized(monkeypatch):
+    """The downsample BN applied by bn2 while it reads the residual (Fn.BNDefer: statistics
+    half only in the downsample op) == the materialized downsample BN output: logits,
+    gradients, running statistics and num_batches_tracked (fp32, CPU)."""
+    from mpi_pytorch_amd.models import resnet as rn
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("resnet18", 10, torch.device("cpu"), World(), 1e-3)
+    a = model._mpa_arena
+    x = torch.randn(2, 64, 64, 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    for defer in (True, False):
+        monkeypatch.setattr(rn, "_DS_DEFER", defer)
+        model.load_state_dict(sd)
+        model.train()
+        a.zero_grad()
+        out = model(x)
+        loss_fn(out, y).backward()
+        res.append((out.detach(), a.grad.clone(),
+                    [v.clone() for k, v in model.state_dict().items()
+                     if "running" in k or "num_batches" in k]))
+    (o1, g1, r1), (o2, g2, r2) = res
+    assert torch.allclose(o1, o2, atol=1e-5)
+    assert all(torch.allclose(u.float(), v.float(), atol=1e-5) for u, v in zip(r1, r2))
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
