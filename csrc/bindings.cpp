@@ -591,6 +591,19 @@ std::vector<Tensor> bn_stats_affine(Tensor x, Tensor stats, Tensor gamma, Tensor
   return {mean, rstd, aff};
 }
 
+// avgpool2x2/s2(relu(bn(z))) with the BN as its [2, C] affine (bn_stats_affine)
+Tensor bn_relu_avgpool2_fwd(Tensor z, Tensor aff) {
+  CHECK_ACT(z);
+  TORCH_CHECK(z.dim() == 4 && z.size(1) % 2 == 0 && z.size(2) % 2 == 0 && z.size(3) % 8 == 0,
+              "bn_relu_avgpool2_fwd: z [N, H, W, C] with even H, W and C % 8 == 0");
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  TORCH_CHECK(aff.numel() == 2 * C, "bn_relu_avgpool2_fwd: aff [2, C]");
+  const c10::OptionalDeviceGuard g(device_of(z));
+  Tensor y = empty_like_shape(z, {N, H / 2, W / 2, C}, torch::kBFloat16);
+  mpa::bn_relu_avgpool2_fwd(bp(z), fopt(aff), N, H, W, C, bpm(y), cur_stream());
+  return y;
+}
+
 // per-channel batch statistics [2, C] = [mean | biased var] of x [..., C] (shift: optional
 // per-channel value subtracted before the sums, e.g. the running mean, for precision)
 Tensor bn_stats(Tensor x, Tensor shift) {
@@ -1363,6 +1376,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter") = py::none());
   m.def("bn_stats", &bn_stats, "[mean | biased var] of x [..., C]");
+  m.def("bn_relu_avgpool2_fwd", &bn_relu_avgpool2_fwd);
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("eps"), py::arg("res"), py::arg("relu"),
         py::arg("channels") = 0);

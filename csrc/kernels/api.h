@@ -218,6 +218,9 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
 void bn_stats_affine(const float* stats, const float* gamma, const float* beta, float* rmean,
                      float* rvar, float momentum, float eps, int M, int C, float* mean,
                      float* rstd, float* aff, int64_t* counter, hipStream_t s);
+// avgpool2x2/s2(relu(z * aff0 + aff1)) without writing the BN output (H, W even, C % 8 == 0)
+void bn_relu_avgpool2_fwd(const bf16_raw* z, const float* aff, int N, int H, int W, int C,
+                          bf16_raw* y, hipStream_t s);
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s, int ldx = 0);

@@ -320,6 +320,46 @@ __global__ __launch_bounds__(256) void bn_stats_affine_kernel(
   rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
 }
 
+// relu(bn(z)) -> 2x2 / stride-2 average pool in one pass (DenseNet transitions, whose pool
+// runs ahead of the 1x1 conv): thread = 8 channels of one pooled pixel, the four inputs
+// loaded together; the BN output is never written.  aff [2][C] = scale | shift
+// (bn_stats_affine).  The backward reuses avgpool_bwd + bn_bwd (mask recomputed from z).
+__global__ __launch_bounds__(256) void bn_relu_avgpool2_fwd_kernel(
+    const bf16_t* __restrict__ z, const float* __restrict__ aff, int N, int H, int W, int C,
+    bf16_t* __restrict__ y) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = aff[c0 + j];
+    sh[j] = aff[C + c0 + j];
+  }
+  const int P = H / 2, Q = W / 2, MP = N * P * Q;
+  for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
+    const int q = r % Q, t = r / Q, p = t % P, n = t / P;
+    const size_t i00 = (((size_t)n * H + 2 * p) * W + 2 * q) * C + c0;
+    const uint4 v0 = *(const uint4*)(z + i00), v1 = *(const uint4*)(z + i00 + C);
+    const uint4 v2 = *(const uint4*)(z + i00 + (size_t)W * C);
+    const uint4 v3 = *(const uint4*)(z + i00 + (size_t)W * C + C);
+    float a[8], b[8], acc[8];
+    unpack8(v0, a);
+    unpack8(v1, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[j] = fmaxf(__builtin_fmaf(a[j], sc[j], sh[j]), 0.f) +
+               fmaxf(__builtin_fmaf(b[j], sc[j], sh[j]), 0.f);
+    unpack8(v2, a);
+    unpack8(v3, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[j] = 0.25f * (acc[j] + fmaxf(__builtin_fmaf(a[j], sc[j], sh[j]), 0.f) +
+                        fmaxf(__builtin_fmaf(b[j], sc[j], sh[j]), 0.f));
+    *(uint4*)(y + (size_t)r * C + c0) = pack8(acc);
+  }
+}
+
 // -------------------------------------------------------------------- forward (eval)
 template <int UNR>
 __global__ __launch_bounds__(256) void bn_fwd_eval_kernel(
@@ -1508,5 +1548,13 @@ void bn_defer_step(const float* sums, const float* gamma, const float* mean, con
     hipLaunchKernelGGL(bn_defer_step_kernel<false>, dim3(blocks), dim3(256), 0, s, sums, gamma,
                        mean, rstd, Ci, s0, M, 1.f / (float)M, k12, ldk, dgamma, dbeta, G, ldg,
                        (const bf16_t*)x, ldx, (bf16_t*)out);
+}
+}  // namespace mpa
+
+namespace mpa {
+void bn_relu_avgpool2_fwd(const bf16_raw* z, const float* aff, int N, int H, int W, int C,
+                          bf16_raw* y, hipStream_t s) {
+  hipLaunchKernelGGL(bn_relu_avgpool2_fwd_kernel, grid_for(N * (H / 2) * (W / 2), C), dim3(256),
+                     0, s, (const bf16_t*)z, aff, N, H, W, C, (bf16_t*)y);
 }
 }  // namespace mpa

@@ -62,6 +62,8 @@ _DEFER = os.environ.get("MPA_DENSE_DEFER", "1") == "1"
 _DIRECT = os.environ.get("MPA_DENSE_DIRECT", "1") == "1"
 # Transition: average-pool before the 1x1 conv (MPA_DENSE_POOL_FIRST=0: torchvision order)
 _POOL_FIRST = os.environ.get("MPA_DENSE_POOL_FIRST", "1") == "1"
+# ... and its norm + ReLU applied inside the pool pass (MPA_DENSE_FUSE_POOL=0: separate)
+_FUSE_POOL = os.environ.get("MPA_DENSE_FUSE_POOL", "1") == "1"
 
 
 def _window(buf: torch.Tensor, c0: int, n: int) -> torch.Tensor:
@@ -276,6 +278,9 @@ class _Transition(nn.Sequential):
         pool commuted ahead of the (linear, bias-free) 1x1 conv: the same function, and the
         conv's forward / dgrad / wgrad run on a quarter of the pixels (the pool then sees
         the wider input - 2x the channels - which costs far less)."""
+        if _POOL_FIRST and _FUSE_POOL and self.norm.training:
+            # BN + ReLU applied while pooling: the normalized activation is never written
+            return self.conv(Fn.bn_relu_avgpool2(x, self.norm, stats))
         x = self.norm(x, relu=True, stats=stats)
         if _POOL_FIRST:
             return self.conv(self.pool(x))

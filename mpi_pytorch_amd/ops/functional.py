@@ -606,6 +606,45 @@ def bn_act(x, bn, relu: bool = True, stats: Optional[torch.Tensor] = None):
                             _empty(x), relu)
 
 
+class _BNReluAvgPool2(torch.autograd.Function):
+    """avg_pool2d(relu(bn(x)), 2, 2), train mode, the BN output never written: the
+    statistics half (bn_stats_affine) then one pass that applies BN + ReLU while pooling.
+    Backward: avgpool_bwd, then the BN backward with the mask recomputed from x."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, stats=None):
+        k = K(x)
+        if stats is None:
+            stats = k.bn_stats(x, bn.running_mean)
+        mean, rstd, aff = k.bn_stats_affine(x, stats, gamma, beta, bn.running_mean,
+                                            bn.running_var, bn.momentum_value(), bn.eps,
+                                            bn.num_batches_tracked)
+        ctx.params = (gamma, beta)
+        ctx.hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, mean, rstd)
+        return k.bn_relu_avgpool2_fwd(x, aff)
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.params
+        k = K(dp)
+        dy = k.avgpool_bwd(dp.contiguous(), ctx.hw[0], ctx.hw[1], 2, 2, 2, 2, 0, 0, False, True)
+        dx, _g = k.bn_bwd(dy, x, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
+                          _sink(beta, dy), bool(ctx.needs_input_grad[0]), False, beta)
+        _done(gamma, beta)
+        return dx, None, None, None, None
+
+
+def bn_relu_avgpool2(x, bn, stats: Optional[torch.Tensor] = None):
+    """avg_pool2d(relu(bn(x)), 2, 2) (DenseNet transitions with the pool ahead of the conv);
+    train mode with an affine BN, even H and W; other cases compose the two ops."""
+    if (bn.training and bn.weight is not None and bn.bias is not None and x.shape[1] % 2 == 0
+            and x.shape[2] % 2 == 0 and x.shape[3] % 8 == 0):
+        return _BNReluAvgPool2.apply(x, bn.weight, bn.bias, bn, stats)
+    return avg_pool2d(bn_act(x, bn, True, stats), (2, 2), (2, 2))
+
+
 # ================================================================================ linear
 class _LinearAct(torch.autograd.Function):
     """y = act(x W^T + b) over the layer's padded output width; returns the first

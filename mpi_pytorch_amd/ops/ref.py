@@ -388,6 +388,12 @@ def avgpool_bwd(dy, H, W, kh, kw, sh, sw, ph, pw, ceil, count_include_pad, dx_ou
     return gx
 
 
+def bn_relu_avgpool2_fwd(z, aff):
+    """avg_pool2d(relu(z * aff[0] + aff[1]), 2, 2) over NHWC z."""
+    y = torch.relu(_f(z) * aff[0] + aff[1])
+    return _nhwc(F.avg_pool2d(_nchw(y), 2, 2)).to(z.dtype)
+
+
 def adaptive_avgpool_fwd(x, oh, ow):
     return _nhwc(F.adaptive_avg_pool2d(_nchw(_f(x)), (oh, ow))).to(x.dtype)
 

@@ -434,6 +434,31 @@ def test_dense_deferred_norm1_backward(gpu, gdt):
         assert torch.equal(G2, G) and rel(o, G1r[..., s0:Ci]) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 56, 56, 256), (3, 14, 10, 64)])
+def test_bn_relu_avgpool2(gpu, shape):
+    """relu(bn(z)) -> 2x2/s2 average pool in one pass (DenseNet transitions): statistics
+    half + fused pool == the oracle; running stats and num_batches_tracked updated once."""
+    torch.manual_seed(43)
+    N, H, W, Cc = shape
+    z = bf(N, H, W, Cc, dev=gpu, scale=1.5)
+    st = torch.stack([z.float().reshape(-1, Cc).mean(0),
+                      z.float().reshape(-1, Cc).var(0, unbiased=False)])
+    g = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu) * 0.5
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    rm2, rv2 = rm.clone(), rv.clone()
+    cnt = torch.tensor(3, dtype=torch.long, device=gpu)
+    mean, rstd, aff = C().bn_stats_affine(z, st, g, b, rm, rv, 0.1, 1e-5, cnt)
+    meanr, rstdr, affr = ref.bn_stats_affine(z, st, g, b, rm2, rv2, 0.1, 1e-5)
+    y = C().bn_relu_avgpool2_fwd(z, aff)
+    yr = ref.bn_relu_avgpool2_fwd(z, affr)
+    torch.cuda.synchronize()
+    assert int(cnt) == 4
+    assert rel(mean, meanr) < 1e-3 and rel(rstd, rstdr) < 1e-3 and rel(aff, affr) < 1e-3
+    assert rel(rm, rm2) < 1e-3 and rel(rv, rv2) < 1e-3
+    assert y.shape == yr.shape and rel(y, yr) < 1e-2
+
+
 def test_conv_halo_repeatable(gpu):
     """Persistent 2-stage ring: repeated launches are bitwise identical (race screen)."""
     torch.manual_seed(23)
