@@ -1307,13 +1307,14 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
     mu[j] = mean[c];
     rs[j] = rstd[c];
   }
-  for (int m = blockIdx.x * rpp + (int)threadIdx.x / cg; m < M; m += gridDim.x * rpp) {
-    float xv[8];
-    unpack8(*(const uint4*)(x + (size_t)m * ldx + c0), xv);
-    float d[8];
+  const int rstep = gridDim.x * rpp;
+  if constexpr (F32) {
+    for (int m = blockIdx.x * rpp + (int)threadIdx.x / cg; m < M; m += rstep) {
+      float xv[8];
+      unpack8(*(const uint4*)(x + (size_t)m * ldx + c0), xv);
+      float d[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = k1[j] + k2[j] * ((xv[j] - mu[j]) * rs[j]);
-    if constexpr (F32) {
+      for (int j = 0; j < 8; ++j) d[j] = k1[j] + k2[j] * ((xv[j] - mu[j]) * rs[j]);
       f32x4* gp = (f32x4*)((float*)G + (size_t)m * ldg + c0);
       f32x4 g0 = gp[0], g1 = gp[1];
 #pragma unroll
@@ -1325,15 +1326,30 @@ __global__ __launch_bounds__(256) void bn_defer_step_kernel(
         gp[0] = g0;
         gp[1] = g1;
       }
-    } else {
-      uint4* gp = (uint4*)((bf16_t*)G + (size_t)m * ldg + c0);
-      float gv[8];
-      unpack8(*gp, gv);
+    }
+  } else {
+    // two rows per iteration, both rows' loads issued before either is used
+    auto fin = [&](int m, uint4 xq, uint4 gq) {
+      float xv[8], gv[8];
+      unpack8(xq, xv);
+      unpack8(gq, gv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) gv[j] += d[j];
+      for (int j = 0; j < 8; ++j) gv[j] += k1[j] + k2[j] * ((xv[j] - mu[j]) * rs[j]);
       const uint4 pk = pack8(gv);
       if (out) *(uint4*)(out + (size_t)m * (Ci - s0) + (c0 - s0)) = pk;
-      else *gp = pk;
+      else *(uint4*)((bf16_t*)G + (size_t)m * ldg + c0) = pk;
+    };
+    for (int m = blockIdx.x * rpp + (int)threadIdx.x / cg; m < M; m += 2 * rstep) {
+      const int m2 = m + rstep;
+      const uint4 xa = *(const uint4*)(x + (size_t)m * ldx + c0);
+      const uint4 ga = *(const uint4*)((const bf16_t*)G + (size_t)m * ldg + c0);
+      uint4 xb = make_uint4(0u, 0u, 0u, 0u), gb = xb;
+      if (m2 < M) {
+        xb = *(const uint4*)(x + (size_t)m2 * ldx + c0);
+        gb = *(const uint4*)((const bf16_t*)G + (size_t)m2 * ldg + c0);
+      }
+      fin(m, xa, ga);
+      if (m2 < M) fin(m2, xb, gb);
     }
   }
 }
