@@ -107,6 +107,10 @@ def parse_args(argv=None):
                         "BLOCKS CUs for US microseconds on a side stream (a stand-in for the "
                         "data-parallel all-reduce overlapping backward); the optimizer waits "
                         "for it like for the real collective")
+    p.add_argument("--decisions", type=int, default=1,
+                   help="more than one GPU: after the headline, also time the capped-communicator "
+                        "+ reservation and bf16-wire variants and probe the all-reduce bandwidth "
+                        "('multi_gpu' in the JSON; 0: off)")
     args = p.parse_args(argv)
     return args
 
@@ -156,6 +160,118 @@ def _timed(step, data, args, world, sync) -> float:
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return args.steps * data.batch * world.world_size / float(t.item())
+
+
+def _variant(step, data, args, world, sync, configure, restore) -> dict:
+    """Re-time the headline step under another communication setting (``configure()``
+    applies it on every rank, ``restore()`` undoes it): img/s over ``args.steps`` steps
+    bracketed like the headline, with the per-bucket comm stats and - on GPUs - the phase
+    times (``comm_wait`` is the exposed all-reduce).  Decision data for the multi-GPU
+    defaults, recorded beside the headline rather than instead of it."""
+    from mpi_pytorch_amd.parallel import barrier
+    from mpi_pytorch_amd.engine import steps_without_gc
+    info = configure() or {}
+    try:
+        for _ in range(max(min(args.warmup, 3), 1)):
+            x, y = data.next()
+            step(x, y)
+        if step.timer is not None:
+            step.timer.summary()  # (drop the warm-up steps)
+        step.bucketer.enable_comm_stats()
+        with steps_without_gc():
+            sync()
+            barrier()
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                x, y = data.next()
+                step(x, y)
+            sync()
+            barrier()
+            sync()
+            dt = time.perf_counter() - t0
+        t = torch.tensor([dt], dtype=torch.float64, device=world.device)
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        out = dict(info)
+        out.update(img_per_s=round(args.steps * data.batch * world.world_size / dt, 2),
+                   ms_per_step=round(dt * 1000.0 / args.steps, 3))
+        if step.timer is not None:
+            out["phases_ms"] = step.timer.summary()
+        comm = step.bucketer.comm_stats()
+        if comm is not None:
+            out["comm"] = comm
+        return out
+    finally:
+        restore()
+
+
+def _allreduce_probe(world, mb: float = 126.0, iters: int = 10, group=None) -> dict:
+    """Standalone all-reduce of one ``mb`` MiB fp32 buffer (ResNet-18's 126 MiB classifier
+    bucket) outside the training step: mean time over ``iters`` back-to-back collectives
+    (max over ranks), algorithm bandwidth and ring bus bandwidth (algbw * 2(n-1)/n, the
+    per-link figure nccl-tests reports; xGMI: ~153 GB/s per link)."""
+    import torch.distributed as dist
+    from mpi_pytorch_amd.parallel import barrier
+    dev = world.device
+    n = max(int(mb * 2**20) // 4, 1)
+    buf = torch.ones(n, dtype=torch.float32, device=dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(3):
+        dist.all_reduce(buf, group=group)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(buf, group=group)
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) * 1e3 / iters
+    algbw = n * 4 / (ms * 1e-3) / 1e9
+    ws = world.world_size
+    del buf
+    return {"mb": round(n * 4 / 2**20, 2), "iters": iters, "ms": round(ms, 4),
+            "algbw_gbs": round(algbw, 2), "busbw_gbs": round(algbw * 2.0 * (ws - 1) / ws, 2)}
+
+
+def _multi_gpu_decisions(step, data, args, world, sync) -> dict:
+    """world_size > 1: the headline's communication alternatives, each timed like it - a
+    CTA-capped communicator for the overlapped buckets plus the persistent-grid
+    reservation (parallel/ddp.py ``comm_ctas``), and the bf16 wire format - and the raw
+    all-reduce bandwidth of the default (and capped) communicator."""
+    b = step.bucketer
+    res = {}
+    orig_ctas, orig_dtype = b.comm_ctas, b.comm_dtype
+    probe = {"default": _allreduce_probe(world)}
+
+    def capped_on():
+        ok = b.set_comm_ctas(8 if orig_ctas == 0 else 0)
+        if ok and b.overlap_group is not None:
+            probe["capped"] = _allreduce_probe(world, group=b.overlap_group)
+        return {"comm_ctas": b.comm_ctas, "capped_communicator": bool(ok)}
+
+    res["comm_ctas8" if orig_ctas == 0 else "comm_ctas0"] = _variant(
+        step, data, args, world, sync, capped_on, lambda: b.set_comm_ctas(orig_ctas))
+
+    def bf16_on():
+        b.comm_dtype = "bf16" if orig_dtype != "bf16" else "fp32"
+        return {"comm_dtype": b.comm_dtype, "wire_mb": b.wire_mb()}
+
+    def bf16_off():
+        b.comm_dtype = orig_dtype
+
+    res["comm_bf16" if orig_dtype != "bf16" else "comm_fp32"] = _variant(
+        step, data, args, world, sync, bf16_on, bf16_off)
+    res["allreduce_probe"] = probe
+    return res
 
 
 def run(args) -> None:
@@ -219,6 +335,8 @@ def run(args) -> None:
         step.bucketer.enable_comm_stats()
     mk = step.markers
     step.mean_loss()  # the reported loss is the timed steps' mean
+    data_stats = getattr(data, "ring_stats", lambda reset=True: None)
+    data_stats(True)  # starvation counters of the timed steps only
     sync()
     barrier()
     sync()
@@ -244,6 +362,10 @@ def run(args) -> None:
     dt = float(t.item())
     imgs = args.steps * args.batch * world.world_size
     value = imgs / dt
+    ring = data_stats(True)
+    decisions = None
+    if world.world_size > 1 and not args.emulate_comm and args.decisions:
+        decisions = _multi_gpu_decisions(step, data, args, world, sync)
     small = None
     if args.small_batch and args.small_batch != args.batch and cuda and not args.emulate_comm:
         step.timer = None
@@ -299,6 +421,13 @@ def run(args) -> None:
             rec["comm_ctas"] = step.bucketer.comm_ctas if step.bucketer.overlap_group else 0
         if comm is not None:
             rec["comm"] = comm
+        if ring is not None:
+            rec["data_ring"] = ring
+        from mpi_pytorch_amd.parallel.dist import affinity
+        if affinity() is not None:
+            rec["host_affinity"] = affinity()
+        if decisions is not None:
+            rec["multi_gpu"] = decisions
         if small is not None:
             rec["small_batch"] = small
         print(json.dumps(rec), flush=True)

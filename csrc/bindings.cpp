@@ -1163,12 +1163,22 @@ Tensor preprocess_pil(Tensor img, Tensor ext, Tensor sel, Tensor hb, Tensor hk, 
   return out;
 }
 
-std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset) {
+// counter: optional device int32 [1] added to offset and advanced by one per call on the
+// stream (graph-replay-safe dropout streams, ops/functional.py DropoutRNG)
+std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset,
+                                c10::optional<Tensor> counter) {
   CHECK_ACT(x);
   const c10::OptionalDeviceGuard g(device_of(x));
+  uint32_t* ctr = nullptr;
+  if (counter && counter->defined() && counter->numel()) {
+    TORCH_CHECK(counter->is_cuda() && counter->scalar_type() == torch::kInt32 &&
+                    counter->numel() == 1 && counter->device() == x.device(),
+                "dropout_fwd: counter must be one int32 on the input's device");
+    ctr = reinterpret_cast<uint32_t*>(counter->data_ptr<int>());
+  }
   Tensor y = torch::empty_like(x);
   Tensor mask = torch::empty(x.sizes(), x.options().dtype(torch::kUInt8));
-  mpa::dropout_fwd(bp(x), x.numel(), p, seed, offset, bpm(y), mask.data_ptr<uint8_t>(),
+  mpa::dropout_fwd(bp(x), x.numel(), p, seed, offset, ctr, bpm(y), mask.data_ptr<uint8_t>(),
                    cur_stream());
   return {y, mask};
 }
@@ -1328,8 +1338,12 @@ std::vector<Tensor> split_channels(Tensor dy, std::vector<int64_t> sizes) {
 
 }  // namespace
 
+extern "C" const char* mpa_src_hash();  // build/src_hash.cpp (setup.py)
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mpi_pytorch_amd native gfx950 kernels + runtime";
+  m.def("src_hash", [] { return std::string(mpa_src_hash()); },
+        "hash of the csrc/ sources this binary was built from (setup.py source_hash)");
   m.def("igemm_engine", &mpa::igemm_engine, "GEMM staging engine: 1 LDS-DMA, 0 register");
   m.def("igemm_set_engine", &mpa::igemm_set_engine);
   m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
@@ -1431,7 +1445,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("preprocess", &preprocess, py::arg("img"), py::arg("OH"), py::arg("OW"), py::arg("mean"),
         py::arg("std"), py::arg("mode"), py::arg("cpad"),
         py::arg("pad") = std::vector<int64_t>{}, py::arg("ext") = py::none());
-  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"),
+        py::arg("offset"), py::arg("counter") = py::none());
   m.def("dropout_bwd", &dropout_bwd);
   m.def("concat_channels", &concat_channels);
   m.def("split_channels", &split_channels);

@@ -354,8 +354,9 @@ void preprocess_pil(const uint8_t* img, int B, int Hp, int Wp, const int* ext, c
                     const int* hb, const int* hk, int kh, const int* vb, const int* vk, int kv,
                     int OH, int OW, Norm3 nrm, int cpad, OutPad pd, uint32_t* tmp, bf16_raw* out,
                     hipStream_t s);
+// counter (optional, device uint32): added to offset and incremented after the launch
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,
-                 bf16_raw* y, uint8_t* mask, hipStream_t s);
+                 uint32_t* counter, bf16_raw* y, uint8_t* mask, hipStream_t s);
 void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,
                  hipStream_t s);
 

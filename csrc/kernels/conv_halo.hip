@@ -162,13 +162,32 @@ __device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, u
   }
 }
 
+// Sum over the 16 lanes of a DPP row (the 16 pixel lanes of one column group), result in
+// every lane of the row: quad swaps, then the half-row and row mirrors (4 VALU ops).
+__device__ __forceinline__ float row16_sum(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x),
+                                                              decltype(ctrl)::value, 0xF, 0xF,
+                                                              true));
+  };
+  v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+  v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+  v += dpp(v, std::integral_constant<int, 0x141>{});  // row_half_mirror
+  v += dpp(v, std::integral_constant<int, 0x140>{});  // row_mirror
+  return v;
+}
+
 // Block-level statistics: reduce the per-lane sums of the block's tiles and write slab row
 // blockIdx.x ([2][N]: the block's 64 columns, zeros elsewhere, so every row is complete);
 // block 0 zeroes the final-sum vector the slab reduction accumulates into.
+// PRE: the per-wave sums are already in `red` (per-tile LDS accumulation, see TRED).
+template <bool PRE = false>
 __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)[4][4],
                                                  float (&sq)[4][4], char* red, int n0, int wave,
                                                  int tid) {
   const int lane = tid & 63, nl = (lane >> 4) * 4;
+  float* rd = (float*)red;
+  if constexpr (!PRE) {
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
@@ -182,7 +201,6 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
       ss[jn][r] = a;
       sq[jn][r] = b;
     }
-  float* rd = (float*)red;
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int jn = 0; jn < 4; ++jn)
@@ -191,6 +209,7 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
         rd[(wave * 64 + jn * 16 + nl + r) * 2] = ss[jn][r];
         rd[(wave * 64 + jn * 16 + nl + r) * 2 + 1] = sq[jn][r];
       }
+  }
   }
   __syncthreads();
   float* row = p.stats + (size_t)blockIdx.x * 2 * p.N;
@@ -354,6 +373,13 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       cst[3 * HB_BN + tid] = __builtin_fmaf(-b, sc, p.ep_beta[n0 + tid]);
     }
   }
+  // TRED (fused BN-backward reduction): the column sums are reduced per TILE (DPP over the
+  // 16 pixel lanes) and accumulated in this wave's slot of `red`, so no sums live in
+  // registers through the MFMA stream.  Holding them for the block's life (as the
+  // statistics flavours do) put this flavour at 256 VGPRs with 344-556 B/lane of scratch
+  // spills - the round-2/3 "BN link is slower" measurements were those spills.
+  constexpr bool TRED = (EPI & EP_BNRED) != 0;
+  if constexpr (TRED) ((float2*)red)[tid] = make_float2(0.f, 0.f);  // own wave's slot
   float ss[4][4], sq[4][4];
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn)
@@ -371,7 +397,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   f32x4 acc[4][4];
 
   // Epilogue of fragment (i, jn) of the tile at m0e (operands from epi_preload).
-  auto epi_fr = [&](int i, int jn, int m0e, auto full) {
+  auto epi_fr = [&](int i, int jn, int m0e, auto full, float (&es)[4][4], float (&eq)[4][4]) {
     constexpr bool F = decltype(full)::value;
     const int m = m0e + wave * 64 + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
@@ -390,8 +416,60 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       colb = *(const f32x4*)(cst + c);
       cols = *(const f32x4*)(cst + HB_BN + c);
     }
-    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh, ss[jn],
-                     sq[jn]);
+    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh, es[jn],
+                     eq[jn]);
+  };
+  // Epilogue of a whole tile (see TRED)
+  auto epi_tile = [&](int m0e, auto full) {
+    if constexpr (TRED) {
+      float ts[4][4], tq[4][4];
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { ts[jn][r] = 0.f; tq[jn][r] = 0.f; }
+      constexpr bool F = decltype(full)::value;
+#pragma unroll
+      for (int jn = 0; jn < NJ; ++jn) {
+        // this column group's mean / rstd / mask affine, read from LDS per tile (an empty
+        // asm memory clobber keeps the compiler from hoisting 64 VGPRs of them out of the
+        // tile loop)
+        asm volatile("" ::: "memory");
+        const int c = jn * 16 + jq * 4;
+        const f32x4 colb = *LDS_PTR(const f32x4, cst + c);
+        const f32x4 cols = *LDS_PTR(const f32x4, cst + HB_BN + c);
+        const f32x4 mc = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
+        const f32x4 mh = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0e + wave * 64 + i * 16 + l15;
+          const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
+          epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh,
+                           ts[jn], tq[jn]);
+        }
+      }
+      float* rd = (float*)red;
+#pragma unroll
+      for (int jn = 0; jn < NJ; ++jn) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ts[jn][r] = row16_sum(ts[jn][r]);
+          tq[jn][r] = row16_sum(tq[jn][r]);
+        }
+        if (l15 == 0) {  // columns jn*16 + 4 jq .. +3 of this wave: [sum, sum2] pairs
+          f32x4* q = (f32x4*)(rd + (wave * 64 + jn * 16 + jq * 4) * 2);
+          f32x4 q0 = q[0], q1 = q[1];
+          q0[0] += ts[jn][0]; q0[1] += tq[jn][0]; q0[2] += ts[jn][1]; q0[3] += tq[jn][1];
+          q1[0] += ts[jn][2]; q1[1] += tq[jn][2]; q1[2] += ts[jn][3]; q1[3] += tq[jn][3];
+          q[0] = q0;
+          q[1] = q1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0e, full, ss, sq);
+    }
   };
 
   // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + 4 B fragments (the next
@@ -481,12 +559,8 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       } else {
         mma_chunk(st, cc, std::false_type{}, nd);
       }
-      if (cc == CC - 1 && tk + 1 < ntiles) {  // full tile (only the last can end past M)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0, std::true_type{});
-      }
+      if (cc == CC - 1 && tk + 1 < ntiles)  // full tile (only the last can end past M)
+        epi_tile(m0, std::true_type{});
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
       // after its top barrier, which every wave passes only once done reading stage st)
     }
@@ -501,14 +575,8 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   } else {
     stager([&](auto& prep_tile, auto& dma, auto&) { tiles(prep_tile, dma); });
   }
-  if (ntiles > 0) {
-    const int m0l = m0_of(ntiles - 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0l, std::integral_constant<bool, FULL>{});
-  }
-  if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush(p, ss, sq, red, n0, wave, tid);
+  if (ntiles > 0) epi_tile(m0_of(ntiles - 1), std::integral_constant<bool, FULL>{});
+  if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush<TRED>(p, ss, sq, red, n0, wave, tid);
 }
 
 // ======================================================================================
@@ -858,10 +926,20 @@ static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPla
                        a, h);
 }
 
+// The fused BN-backward reduction runs in 4-wave blocks (MPA_HALO_BNRED_PROD=1: producer
+// waves): with 8 waves per CU a wave has 256 registers in all, and that flavour's
+// preloaded z tile + reduction epilogue spilled 250-550 B/lane to scratch there
+// (-Rpass-analysis=kernel-resource-usage); a 4-wave block's waves also get the AGPR half.
+static const bool g_halo_bnred_prod = [] {
+  const char* e = getenv("MPA_HALO_BNRED_PROD");
+  return e && atoi(e) != 0;
+}();
+
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  if (g_halo_prod) launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
+  const bool prod = (EPI & EP_BNRED) ? g_halo_bnred_prod : g_halo_prod;
+  if (prod) launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
   else launch_halo_k<EPI, false, 4>(wres, grid, a, h, s);
 }
 

@@ -298,10 +298,14 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
+// offset: host part of the stream position; dev_off (optional): a device counter added to
+// it, advanced by dropout_counter_inc after every call - a HIP graph replays the read and
+// the increment, so every replay draws a fresh mask (a host offset is frozen at capture)
 __global__ void dropout_fwd_kernel(const bf16_t* __restrict__ x, int64_t n, float p, uint32_t seed,
-                                   uint32_t offset, bf16_t* __restrict__ y,
-                                   uint8_t* __restrict__ mask) {
+                                   uint32_t offset, const uint32_t* __restrict__ dev_off,
+                                   bf16_t* __restrict__ y, uint8_t* __restrict__ mask) {
   const float scale = 1.f / (1.f - p);
+  if (dev_off) offset += *dev_off;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t h = hash3(seed, offset, (uint32_t)i);
@@ -311,6 +315,8 @@ __global__ void dropout_fwd_kernel(const bf16_t* __restrict__ x, int64_t n, floa
     y[i] = keep ? f2bf(bf2f(x[i]) * scale) : (bf16_t)0;
   }
 }
+
+__global__ void dropout_counter_inc_kernel(uint32_t* c) { c[0] += 1u; }
 
 __global__ void dropout_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
                                    int64_t n, float p, bf16_t* __restrict__ dx) {
@@ -464,9 +470,10 @@ void preprocess(const uint8_t* img, int B, int H, int W, int OH, int OW, Norm3 n
 }
 
 void dropout_fwd(const bf16_raw* x, int64_t n, float p, uint64_t seed, uint64_t offset,
-                 bf16_raw* y, uint8_t* mask, hipStream_t s) {
+                 uint32_t* counter, bf16_raw* y, uint8_t* mask, hipStream_t s) {
   hipLaunchKernelGGL(dropout_fwd_kernel, dim3(blocks_n(n)), dim3(256), 0, s, x, n, p,
-                     (uint32_t)seed, (uint32_t)offset, y, mask);
+                     (uint32_t)seed, (uint32_t)offset, (const uint32_t*)counter, y, mask);
+  if (counter) hipLaunchKernelGGL(dropout_counter_inc_kernel, dim3(1), dim3(1), 0, s, counter);
 }
 
 void dropout_bwd(const bf16_raw* dy, const uint8_t* mask, int64_t n, float p, bf16_raw* dx,

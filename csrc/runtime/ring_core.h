@@ -16,6 +16,7 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -48,9 +49,19 @@ class RingCore {
   }
 
   // Consumer: block until the slot holding the next batch index is ready; -1 once stopped.
+  // (starvation counters: calls that found their batch not ready yet, and the time they
+  // blocked - read by stats())
   int acquire() {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return find_ready() >= 0 || stopping_; });
+    ++acquires_;
+    if (find_ready() < 0 && !stopping_) {
+      ++waits_;
+      const auto t0 = std::chrono::steady_clock::now();
+      cv_.wait(lk, [&] { return find_ready() >= 0 || stopping_; });
+      blocked_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now() - t0)
+                         .count();
+    }
     const int id = find_ready();
     if (id < 0) return -1;
     ready_.erase(std::find(ready_.begin(), ready_.end(), id));
@@ -110,6 +121,16 @@ class RingCore {
 
   bool producing() const { return !workers_.empty(); }
 
+  // consumer starvation since the last reset: {acquire calls, calls that had to wait for
+  // a producer, nanoseconds spent waiting}
+  void stats(int64_t out[3], bool reset) {
+    std::lock_guard<std::mutex> lk(mu_);
+    out[0] = acquires_;
+    out[1] = waits_;
+    out[2] = blocked_ns_;
+    if (reset) acquires_ = waits_ = blocked_ns_ = 0;
+  }
+
  private:
   int find_ready() const {  // the ready slot holding batch next_consume_, or -1
     for (int id : ready_)
@@ -145,6 +166,7 @@ class RingCore {
   mutable std::mutex mu_;
   std::condition_variable cv_;
   bool stopping_ = false;
+  int64_t acquires_ = 0, waits_ = 0, blocked_ns_ = 0;
   std::vector<std::thread> workers_;
 };
 

@@ -46,6 +46,12 @@ int main(int argc, char** argv) {
         if (buf[id][i] != k * 31 + i) return fail("phase1 payload", buf[id][i], k * 31 + i);
       ring.release(id);
     }
+    int64_t st[3];
+    ring.stats(st, true);  // every acquire counted; waits / blocked time consistent
+    if (st[0] != nbatch || st[1] < 0 || st[1] > nbatch || (st[1] == 0) != (st[2] == 0))
+      return fail("phase1 stats", st[0], st[1]);
+    ring.stats(st, false);
+    if (st[0] != 0) return fail("phase1 stats reset", st[0], 0);
     ring.stop();
   }
   {  // phase 2: external producers claiming indices out of order

@@ -162,6 +162,13 @@ class BatchRing {
 
   int depth() const { return core_.depth(); }
 
+  // consumer starvation counters (acquires, waits, blocked ms) since the last reset
+  std::tuple<int64_t, int64_t, double> stats(bool reset) {
+    int64_t v[3];
+    core_.stats(v, reset);
+    return {v[0], v[1], v[2] * 1e-6};
+  }
+
  private:
   torch::Tensor view_img(int id) {
     auto opt = torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true);
@@ -259,7 +266,8 @@ void register_bindings(pybind11::module_& m) {
       .def("set_window_source", &BatchRing::set_window_source)
       .def("num_batches", &BatchRing::num_batches)
       .def("stop", &BatchRing::stop)
-      .def("depth", &BatchRing::depth);
+      .def("depth", &BatchRing::depth)
+      .def("stats", &BatchRing::stats, pybind11::arg("reset") = true);
   m.def("range_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); });
   m.def("range_pop", []() { return roctxRangePop(); });
   m.def("mark", [](const std::string& s) { roctxMarkA(s.c_str()); });

@@ -111,6 +111,15 @@ class DevicePrefetcher:
                               list(IMAGENET_STD), self.mode, self.cpad, self.pad)
         return x, lab_d
 
+    def ring_stats(self, reset: bool = True) -> Optional[dict]:
+        """Consumer starvation of the native ring since the last reset: ``acquires`` (batches
+        taken), ``waits`` (of them, how many found their batch not produced yet) and
+        ``blocked_ms`` (host time spent waiting for producers).  None on the CPU path."""
+        if not self.cuda:
+            return None
+        n, w, ms = self.ring.stats(reset)
+        return {"acquires": int(n), "waits": int(w), "blocked_ms": round(float(ms), 3)}
+
     def __iter__(self) -> Iterator:
         while True:
             yield self.next()

@@ -261,36 +261,56 @@ def make_ring(names: Sequence[str], labels: Sequence[int], batch: int, source, n
     return ring, nb
 
 
+_FEED_ERRORS = {}  # id(ring) -> decode exceptions of its feeder threads
+
+
+def feed_error(ring):
+    """The first exception a decode thread of ``ring`` hit (it then stopped the ring), or
+    None."""
+    errs = _FEED_ERRORS.get(id(ring))
+    return errs[0] if errs else None
+
+
 def _feed_external(ring, names, labels, batch, source, threads: int) -> None:
-    """PIL decode threads for real images: each takes the next batch index, an empty slot,
-    decodes its images straight into the slot (top-left, extent recorded) and commits it.
-    The ring hands batches to the consumer in index order."""
+    """PIL decode threads for real images: each takes an empty slot, THEN the next batch
+    index, decodes its images straight into the slot (top-left, extent recorded) and
+    commits it.  The ring hands batches to the consumer in index order, so a thread must
+    own a slot before it owns an index: otherwise later indices could fill every free slot
+    while the thread holding the next one waits for a slot forever.  A decode error stops
+    the ring (the consumer's acquire raises instead of hanging; ``feed_error`` has it)."""
     nb = (len(names) + batch - 1) // batch
     lock = threading.Lock()
     nxt = [0]
+    errors = _FEED_ERRORS.setdefault(id(ring), [])
 
     def worker():
         from PIL import Image
         while True:
-            with lock:
-                bi = nxt[0]
-                nxt[0] += 1
-            if bi >= nb:
-                return
             try:
                 slot, img, lab, ext = ring.acquire_empty()
             except RuntimeError:  # ring stopped
                 return
-            a = img.numpy()
-            e = ext.numpy()
-            lo, hi = bi * batch, min((bi + 1) * batch, len(names))
-            for b, j in enumerate(range(lo, hi)):
-                with Image.open(os.path.join(source.root, names[j])) as im:
-                    arr = np.asarray(im.convert("RGB"))
-                h, w = min(arr.shape[0], a.shape[1]), min(arr.shape[1], a.shape[2])
-                a[b, :h, :w] = arr[:h, :w]
-                e[b] = (h, w)
-                lab.numpy()[b] = labels[j]
+            with lock:
+                bi = nxt[0]
+                nxt[0] += 1
+            if bi >= nb:
+                ring.release(slot)
+                return
+            try:
+                a = img.numpy()
+                e = ext.numpy()
+                lo, hi = bi * batch, min((bi + 1) * batch, len(names))
+                for b, j in enumerate(range(lo, hi)):
+                    with Image.open(os.path.join(source.root, names[j])) as im:
+                        arr = np.asarray(im.convert("RGB"))
+                    h, w = min(arr.shape[0], a.shape[1]), min(arr.shape[1], a.shape[2])
+                    a[b, :h, :w] = arr[:h, :w]
+                    e[b] = (h, w)
+                    lab.numpy()[b] = labels[j]
+            except Exception as ex:  # noqa: BLE001 - reported through feed_error
+                errors.append(ex)
+                ring.stop()
+                return
             ring.commit(slot, bi, hi - lo)
 
     for _ in range(max(1, threads)):
@@ -346,8 +366,14 @@ def run_pipeline(cfg: Config, ckpt_path: Optional[str] = None, max_images: int =
                              threads=max(2, cfg.num_workers), pitch=pitch)
         try:
             counts = pipe.run_ring(ring, nb)
+        except RuntimeError as e:
+            fe = feed_error(ring)
+            if fe is not None:
+                raise RuntimeError("eval pipeline: image decode failed: %r" % (fe,)) from e
+            raise
         finally:
             ring.stop()
+            _FEED_ERRORS.pop(id(ring), None)
     else:
         counts = pipe.run(_batches(names, labels, cfg.eval_batch, source))
     dt = time.perf_counter() - t0

@@ -323,13 +323,46 @@ class TrainStep:
         return v
 
     # --------------------------------------------------------------------- HIP graphs
+    def _training_state(self):
+        """Everything a training step mutates besides the (per-step zeroed) gradients:
+        master / bf16 / transposed weights, optimizer moments and step counter, BN running
+        statistics and batch counts, the running loss sum, the dropout stream position."""
+        a = self.arena
+        dev = [t for t in (a.master, a.shadow, a.shadow_t, self.loss_sum) if t is not None]
+        dev += [v for v in vars(self.opt).values() if torch.is_tensor(v)]
+        dev += list(self.model.buffers())
+        bns = [m for m in self.model.modules() if hasattr(m, "_batches_host")]
+        return dev, bns
+
+    def snapshot(self):
+        """Device copies of the training state (see :meth:`restore`)."""
+        dev, bns = self._training_state()
+        return ([t.clone() for t in dev], [m._batches_host for m in bns], Fn.DropoutRNG.state(),
+                self.steps)
+
+    def restore(self, snap) -> None:
+        dev, bns = self._training_state()
+        with torch.no_grad():
+            for t, c in zip(dev, snap[0]):
+                t.copy_(c)
+        for m, n in zip(bns, snap[1]):
+            m._batches_host = n
+        Fn.DropoutRNG.set_state(snap[2])
+        self.steps = snap[3]
+
     def capture(self, x, y, warmup: int = 2) -> bool:
-        """Capture one full step into a HIP graph (world size 1 only)."""
+        """Capture one full step into a HIP graph (world size 1 only).
+
+        The warm-up steps that capture needs run on a snapshot of the training state and
+        are rolled back afterwards, so capturing does not train on ``x`` (the caller's
+        following ``step(x, y)`` - the first replay - is that batch's only update) and
+        adds nothing to the running loss."""
         if self.world.world_size != 1 or not x.is_cuda:
             return False
         self._static_x = x.clone()
         self._static_y = y.clone()
         self.timer = None  # replayed steps are not phase-timed
+        snap = self.snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -340,6 +373,7 @@ class TrainStep:
         with torch.cuda.graph(g):
             self._static_loss = self._eager(self._static_x, self._static_y)
         self._graph = g
+        self.restore(snap)
         return True
 
 

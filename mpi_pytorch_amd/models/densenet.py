@@ -95,8 +95,8 @@ class _DenseBlock(nn.ModuleDict):
                 params = [p for p in self.parameters() if p.requires_grad]
                 out = _DenseBlockGrad.apply(x, self, *params)
                 return out, self.__dict__.pop("_stats", None)
-            if not self.training:
-                return _block_eval(self, x), None
+            if not self.training and not (torch.is_grad_enabled() and x.requires_grad):
+                return _block_eval(self, x), None  # (raw kernels: inference only)
         feats = [x]
         for layer in self.values():
             feats.append(layer(feats))
@@ -128,7 +128,8 @@ def _block_eval(block, x):
 
 
 class _DenseBlockGrad(torch.autograd.Function):
-    """A dense block on ONE feature buffer, with ONE fp32 gradient accumulator.
+    """A dense block on ONE feature buffer, with ONE gradient accumulator G (bf16 by default,
+    each contribution added in fp32 and rounded once; fp32 with MPA_DENSE_GRAD_BF16=0).
 
     Forward: the block input and every layer's 32-channel output live in a buffer
     [N, H, W, C_total] at their channel offsets (``chan_insert``), so layer i reads its
@@ -208,7 +209,9 @@ class _DenseBlockGrad(torch.autograd.Function):
         layers = list(ctx.block.values())
         if _GRAD_BF16:
             # the block output's gradient comes from its one consumer's BN backward (the
-            # transition / norm5) as a fresh tensor: accumulate into it in place
+            # transition / norm5: bn_bwd returns a fresh dx that nothing else references)
+            # as a fresh tensor: accumulate into it in place; a view or a non-bf16 gradient
+            # is copied first
             G = gy if (gy._base is None and gy.dtype == torch.bfloat16) else gy.clone()
         else:
             G = torch.empty(gy.shape, dtype=torch.float32, device=gy.device)

@@ -54,6 +54,41 @@ class SyncedExt:
         return call
 
 
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def source_hash(root: str = _ROOT):
+    """setup.py's hash of the csrc/ tree next to this package (None without one)."""
+    if not os.path.isdir(os.path.join(root, "csrc")) or \
+            not os.path.exists(os.path.join(root, "setup.py")):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mpa_setup_hash", os.path.join(root, "setup.py"))
+    src = open(os.path.join(root, "setup.py")).read()
+    # only the hashing function: executing setup.py would run setup()
+    start = src.index("def source_hash(")
+    end = src.index("\n\n\n", start)
+    ns = {"os": os, "ROOT": root}
+    exec(compile(src[start:end], spec.origin, "exec"), ns)
+    return ns["source_hash"](root)
+
+
+def check_fresh(mod, root: str = _ROOT) -> None:
+    """Refuse a native binary built from other sources than the csrc/ tree beside it
+    (MPA_ALLOW_STALE=1 to override, e.g. while bisecting)."""
+    if os.environ.get("MPA_ALLOW_STALE", "0") == "1":
+        return
+    want = source_hash(root)
+    if want is None:
+        return
+    have = mod.src_hash() if hasattr(mod, "src_hash") else "<none>"
+    if have != want:
+        raise RuntimeError(
+            "mpi_pytorch_amd native extension {} was built from other sources (hash {}) than "
+            "{}/csrc (hash {}): rebuild with `python setup.py build_ext --inplace`".format(
+                getattr(mod, "__file__", "_C"), have, root, want))
+
+
 def load():
     global _ext, _err
     if _ext is not None:
@@ -61,12 +96,18 @@ def load():
     if _err is not None:
         raise _err
     try:
-        _ext = importlib.import_module("mpi_pytorch_amd._C")
+        mod = importlib.import_module("mpi_pytorch_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _err = RuntimeError(
             "mpi_pytorch_amd native extension (_C) is not importable: {}. Build it with "
             "`python setup.py build_ext --inplace` (PYTORCH_ROCM_ARCH=gfx950).".format(e))
         raise _err
+    try:
+        check_fresh(mod)
+    except RuntimeError as e:
+        _err = e
+        raise
+    _ext = mod
     return _ext
 
 

@@ -796,17 +796,46 @@ def cat_channels(xs):
 
 # =============================================================================== dropout
 class DropoutRNG:
-    """Per-device counter so every dropout call draws a fresh mask (graph-safe: the seed
-    is a host constant, the offset a per-call counter)."""
+    """Stream position of the dropout masks, so every call draws a fresh mask.
+
+    GPU: a device int32 counter per device, read by the dropout kernel as its offset and
+    advanced on the stream after every call.  A HIP graph replays both, so each replay of a
+    captured step draws new masks (a host-side offset would be frozen into the graph at
+    capture, and every replay would reuse one mask).  CPU: a host counter.  The seed is a
+    host constant.  ``state()`` / ``set_state()`` snapshot both (TrainStep.capture)."""
     seed = 0
     offset = 0
+    _counters = {}
+
+    @classmethod
+    def counter(cls, device: torch.device) -> torch.Tensor:
+        c = cls._counters.get(device)
+        if c is None:
+            c = cls._counters[device] = torch.zeros(1, dtype=torch.int32, device=device)
+        return c
+
+    @classmethod
+    def state(cls):
+        return cls.offset, {d: c.clone() for d, c in cls._counters.items()}
+
+    @classmethod
+    def set_state(cls, st) -> None:
+        cls.offset = st[0]
+        for d, c in st[1].items():
+            cls.counter(d).copy_(c)
+
+
+def _dropout_fwd(x, p):
+    if x.is_cuda:  # offset = the device counter (advanced by the kernel launch pair)
+        return K(x).dropout_fwd(x, p, DropoutRNG.seed, 0, DropoutRNG.counter(x.device))
+    DropoutRNG.offset += 1
+    return K(x).dropout_fwd(x, p, DropoutRNG.seed, DropoutRNG.offset)
 
 
 class _Dropout(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p):
-        DropoutRNG.offset += 1
-        y, mask = K(x).dropout_fwd(x, p, DropoutRNG.seed, DropoutRNG.offset)
+        y, mask = _dropout_fwd(x, p)
         ctx.p = p
         ctx.save_for_backward(mask)
         return y
@@ -822,8 +851,7 @@ def dropout(x, p: float, training: bool):
         return x
     if torch.is_grad_enabled() and x.requires_grad:
         return _Dropout.apply(x, p)
-    DropoutRNG.offset += 1
-    return K(x).dropout_fwd(x, p, DropoutRNG.seed, DropoutRNG.offset)[0]
+    return _dropout_fwd(x, p)[0]
 
 
 # ========================================================================= cross-entropy

@@ -141,7 +141,9 @@ class GradBucketer:
         self._pending = [0] * len(self.buckets)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._wire: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
-        self._stats: Optional[list] = None  # (bucket, wire bytes, work, host t0, host t1)
+        # [bucket, wire bytes, work (None once resolved), host t0, host t1 | resolved ms]
+        self._stats: Optional[list] = None
+        self._held = 0
         self.active = world_size > 1
         # RCCL reports each collective's own device time; other backends are host-timed
         self._host_timed = self.active and dist.is_initialized() and \
@@ -153,6 +155,24 @@ class GradBucketer:
                     and self.group is None):
                 self.overlap_group = capped_group(self.comm_ctas, arena.device)
         self.reset()
+
+    def set_comm_ctas(self, comm_ctas: int) -> bool:
+        """Switch the overlapped buckets to a CTA-capped communicator (``comm_ctas`` > 0, with
+        the persistent-grid reservation) or back to the default one (0).  Collective: every
+        rank must call it between steps.  Returns whether a capped communicator is in use
+        (False on host backends or if RCCL rejected the config)."""
+        if not self.active:
+            return False
+        self.comm_ctas = max(int(comm_ctas), 0)
+        old, self.overlap_group = self.overlap_group, None
+        if old is not None:
+            try:
+                dist.destroy_process_group(old)
+            except Exception:
+                pass
+        if self.comm_ctas > 0 and self.overlap and len(self.buckets) > 1 and self.group is None:
+            self.overlap_group = capped_group(self.comm_ctas, self.arena.device)
+        return self.overlap_group is not None
 
     def _split_tail(self, tail_elems: int) -> None:
         """Give the last parameters of the arena (the first layers, whose gradients land
@@ -212,6 +232,9 @@ class GradBucketer:
         if self._stats is not None and len(self._stats) < self._MAX_STATS:
             self._stats.append([bi, g.numel() * g.element_size(), self._works[bi],
                                 time.perf_counter(), None])
+            self._held += 1
+            if self._held > self._MAX_HELD:
+                self._resolve_old()
 
     def finish(self) -> None:
         """Issue any bucket not yet launched, then make the compute stream wait for all."""
@@ -259,6 +282,30 @@ class GradBucketer:
 
     # ------------------------------------------------------------------ comm statistics
     _MAX_STATS = 8192
+    _MAX_HELD = 64  # Work objects kept alive for their durations (see _resolve_old)
+
+    def _resolve_old(self) -> None:
+        """Turn the older half of the held Work records into durations and drop the Work
+        objects: a Work keeps its collective's output alive, and with the bf16 wire format
+        that is a fresh bucket-sized tensor per launch - holding every step's Works until
+        comm_stats() grew device memory by half the gradient size per step.  The records
+        resolved here are steps old, so reading their duration does not stall the step."""
+        held = [r for r in self._stats if r[2] is not None]
+        for rec in held[: len(held) // 2]:
+            rec[4] = self._duration_ms(rec)
+            rec[2] = None
+        self._held = sum(1 for r in self._stats if r[2] is not None)
+
+    def _duration_ms(self, rec) -> Optional[float]:
+        bi, nbytes, work, t0, t1 = rec
+        if t1 is not None and work is None:
+            return t1
+        if self._host_timed:
+            return (t1 - t0) * 1e3 if t1 is not None else None
+        try:
+            return float(work._get_duration())
+        except Exception:
+            return None
 
     def enable_comm_stats(self) -> None:
         """Record every bucket all-reduce of the following steps for :meth:`comm_stats`.
@@ -269,6 +316,7 @@ class GradBucketer:
         completion of ``wait()``.  Nothing is synchronised until :meth:`comm_stats`."""
         if self.active:
             self._stats = []
+            self._held = 0
 
     def comm_stats(self, reset: bool = True) -> Optional[dict]:
         """Per-bucket mean all-reduce time, algorithm and bus bandwidth (ring all-reduce:
@@ -278,15 +326,9 @@ class GradBucketer:
             return None
         n = self.world_size
         per = {}
-        for bi, nbytes, work, t0, t1 in self._stats:
-            ms = None
-            if t1 is not None:
-                ms = (t1 - t0) * 1e3
-            else:
-                try:
-                    ms = float(work._get_duration())
-                except Exception:
-                    ms = None
+        for rec in self._stats:
+            bi, nbytes = rec[0], rec[1]
+            ms = rec[4] if rec[2] is None else self._duration_ms(rec)
             d = per.setdefault(bi, {"bucket": bi, "bytes": nbytes, "ms": [], "n": 0})
             d["n"] += 1
             if ms is not None and ms > 0:
@@ -307,6 +349,7 @@ class GradBucketer:
             out.append(rec)
         if reset:
             self._stats = []
+            self._held = 0
         res = {"world": n, "steps": steps, "buckets": out,
                "mb_per_step": round(tot_bytes / 2**20, 2),
                "timed": any("ms" in r for r in out)}

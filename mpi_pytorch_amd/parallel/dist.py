@@ -73,6 +73,8 @@ def init_world(device: str = "auto", timeout_s: float = 1800.0,
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local % max(ndev, 1))
         torch.cuda.set_device(dev)
+        if world > 1:
+            pin_host_to_gpu(dev)
     else:
         dev = torch.device("cpu")
     be = "none"
@@ -91,6 +93,79 @@ def init_world(device: str = "auto", timeout_s: float = 1800.0,
             dist.init_process_group(**kw)
     _WORLD = World(rank=rank, world_size=world, local_rank=local, device=dev, backend=be)
     return _WORLD
+
+
+_AFFINITY: Optional[dict] = None
+
+
+def _pci_addr(dev: torch.device) -> Optional[str]:
+    """PCI address ("dddd:bb:dd.f") of a HIP device, or None if torch does not report it."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        dom = int(getattr(pr, "pci_domain_id", 0))
+        bus = int(getattr(pr, "pci_bus_id"))
+        slot = int(getattr(pr, "pci_device_id"))
+    except Exception:
+        return None
+    return "%04x:%02x:%02x.0" % (dom, bus, slot)
+
+
+def parse_cpulist(text: str) -> set:
+    """Linux cpulist ("0-3,8,10-11") -> {0,1,2,3,8,10,11}."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-", 1)
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def pin_host_to_gpu(dev: torch.device, sysfs: str = "/sys/bus/pci/devices",
+                    addr: Optional[str] = None) -> Optional[dict]:
+    """Restrict this rank's host threads (the caller and every thread started afterwards:
+    batch producers, copy hand-off) to the CPUs of its GPU's NUMA node, read from the
+    device's PCI ``local_cpulist``.  One process per GPU on a two-socket node otherwise lets
+    the scheduler place a rank's producers on the far socket, so its pinned ring slots and
+    H2D copies cross the inter-socket link.  Kept within the CPUs the process may already
+    use (container / cgroup limits); a no-op when sysfs does not say (MPA_NUMA_PIN=0: off).
+    Returns {"pci", "numa_node", "cpus"} or None."""
+    global _AFFINITY
+    if os.environ.get("MPA_NUMA_PIN", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return None
+    addr = addr or _pci_addr(dev)
+    if addr is None:
+        return None
+    base = os.path.join(sysfs, addr)
+    try:
+        with open(os.path.join(base, "local_cpulist")) as f:
+            local = parse_cpulist(f.read())
+        node = -1
+        try:
+            with open(os.path.join(base, "numa_node")) as f:
+                node = int(f.read().strip())
+        except OSError:
+            pass
+        allowed = os.sched_getaffinity(0)
+    except (OSError, ValueError):
+        return None
+    cpus = local & allowed
+    if not cpus or cpus == allowed:
+        return None
+    try:
+        os.sched_setaffinity(0, cpus)
+    except OSError:
+        return None
+    _AFFINITY = {"pci": addr, "numa_node": node, "cpus": len(cpus)}
+    return _AFFINITY
+
+
+def affinity() -> Optional[dict]:
+    """What :func:`pin_host_to_gpu` did for this rank (None: not pinned)."""
+    return _AFFINITY
 
 
 def get_world() -> World:

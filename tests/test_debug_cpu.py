@@ -59,3 +59,31 @@ def test_launcher_exports_serialization_env(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     for rank in (0, 1):
         assert (tmp_path / ("env.txt%d" % rank)).read_text() == "3 1"
+
+
+def test_stale_binary_guard(tmp_path):
+    """_ext.check_fresh compares the hash compiled into _C with setup.py's hash of the
+    csrc/ tree beside it: any source edit makes the old binary refuse to load."""
+    import shutil
+    import types
+    from mpi_pytorch_amd.ops import _ext as E
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shutil.copytree(os.path.join(root, "csrc"), tmp_path / "csrc")
+    shutil.copy(os.path.join(root, "setup.py"), tmp_path / "setup.py")
+    h = E.source_hash(str(tmp_path))
+    assert h == E.source_hash(root) and len(h) == 32
+    mod = types.SimpleNamespace(src_hash=lambda: h, __file__="_C.so")
+    E.check_fresh(mod, str(tmp_path))  # matching: loads
+    with open(tmp_path / "csrc" / "kernels" / "common.h", "a") as f:
+        f.write("\n// edited\n")
+    with pytest.raises(RuntimeError, match="other sources"):
+        E.check_fresh(mod, str(tmp_path))
+    old = os.environ.get("MPA_ALLOW_STALE")
+    os.environ["MPA_ALLOW_STALE"] = "1"
+    try:
+        E.check_fresh(mod, str(tmp_path))
+    finally:
+        if old is None:
+            del os.environ["MPA_ALLOW_STALE"]
+        else:
+            os.environ["MPA_ALLOW_STALE"] = old

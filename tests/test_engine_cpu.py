@@ -103,7 +103,7 @@ def test_training_driver_cpu(tmp_path):
               "_Training Dataset Object Created", "_Model Created: resnet18",
               "_Optimizer Created", "_Entering training Loop", "_Epoch: 0 | Train Loss: ",
               "_Creating a checkpoint at epoch 1", "_Checkpoint saved", "_Evaluating model",
-              "_Epoch: 1 | Acc: "):
+              "_Epoch: 1 | Acc: ", "INFO:Herbarium_R0:_Model loaded to CPU\n"):
         assert s in text, s
     recs = [json.loads(l) for l in (tmp_path / "m.jsonl").read_text().splitlines()]
     assert len(recs) == 2 and recs[1]["train_loss"] < recs[0]["train_loss"]

@@ -103,3 +103,50 @@ def test_real_jpeg_ring_pipeline(gpu, model, tmp_path):
     finally:
         ring.stop()
     assert sum(counts) == ref and sum(pipe.seen) == 37
+
+
+def test_real_jpeg_ring_many_threads_small_ring(gpu, model, tmp_path):
+    """More decode threads than free slots (depth 2, 6 threads, 40 batches): a thread owns a
+    slot before it takes a batch index, so the thread holding the next index can always
+    commit (the old index-first order could park it behind later batches and hang)."""
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    names, labels = [], []
+    for i in range(80):
+        arr = rng.integers(0, 256, (int(rng.integers(30, 70)), int(rng.integers(30, 70)), 3),
+                           dtype=np.uint8)
+        names.append("s%03d.png" % i)
+        Image.fromarray(arr).save(os.path.join(tmp_path, names[-1]))
+        labels.append(int(rng.integers(0, NC)))
+    src = FolderImages(str(tmp_path), 2)
+    ref = plain_eval(model, names, labels, 2, src, gpu, (64, 64))
+    ring, nb = make_ring(names, labels, 2, src, NC, depth=2, threads=6, pitch=(70, 70))
+    try:
+        pipe = StreamPipeline(model, gpu, (64, 64), lanes=2, assign="roundrobin")
+        counts = pipe.run_ring(ring, nb)
+    finally:
+        ring.stop()
+    assert sum(counts) == ref and sum(pipe.seen) == 80
+
+
+def test_real_jpeg_ring_decode_error_raises(gpu, model, tmp_path):
+    """A file PIL cannot decode stops the ring: the consumer raises instead of waiting for
+    a batch that never comes, and feed_error names the decode failure."""
+    from PIL import Image
+    from mpi_pytorch_amd.engine.eval_pipeline import feed_error
+    names = []
+    for i in range(12):
+        names.append("e%02d.png" % i)
+        if i == 7:
+            (tmp_path / names[-1]).write_bytes(b"not an image")
+        else:
+            Image.fromarray(np.zeros((20, 20, 3), np.uint8)).save(os.path.join(tmp_path, names[-1]))
+    src = FolderImages(str(tmp_path), 1)
+    ring, nb = make_ring(names, [0] * 12, 4, src, NC, depth=2, threads=2, pitch=(20, 20))
+    try:
+        pipe = StreamPipeline(model, gpu, (64, 64), lanes=1)
+        with pytest.raises(RuntimeError):
+            pipe.run_ring(ring, nb)
+        assert feed_error(ring) is not None
+    finally:
+        ring.stop()

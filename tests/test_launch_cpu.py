@@ -43,6 +43,16 @@ def test_bench_spawns_ranks_itself(tmp_path):
     assert len(comm["buckets"]) >= 2 and all(b["calls"] == 2 for b in comm["buckets"])
     assert rec["grad_allreduce_mb"] == pytest.approx(comm["mb_per_step"], rel=1e-3)
     assert "phases_ms" not in rec  # host runs have no HIP-event timers
+    # multi-GPU decision data: the comm alternatives timed like the headline + a raw probe
+    mg = rec["multi_gpu"]
+    for k in ("comm_ctas8", "comm_bf16"):
+        v = mg[k]
+        assert v["img_per_s"] > 0 and v["ms_per_step"] > 0
+        assert v["comm"]["world"] == 2 and v["comm"]["steps"] == 2
+    assert mg["comm_ctas8"]["capped_communicator"] is False  # (gloo: no RCCL CTA cap)
+    assert mg["comm_bf16"]["comm_dtype"] == "bf16"
+    pr = mg["allreduce_probe"]["default"]
+    assert pr["mb"] == pytest.approx(126.0) and pr["ms"] > 0 and pr["busbw_gbs"] > 0
 
 
 def test_bench_rejects_rank_count_mismatch(tmp_path):

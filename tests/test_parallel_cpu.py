@@ -188,3 +188,27 @@ def test_bucket_layout_resnet18():
     assert b.ranges[0][0] == 0 and b.ranges[-1][1] == a.n_train
     assert all(b.ranges[i][1] == b.ranges[i + 1][0] for i in range(len(b.ranges) - 1))
     assert sum(len(ps) for ps in b.buckets) == len(a.trainable)
+
+
+def test_numa_pin_from_sysfs(tmp_path):
+    """pin_host_to_gpu restricts the process to its GPU's local CPUs (sysfs local_cpulist),
+    within the CPUs it may already use, and restores nothing else; unknown devices are a
+    no-op."""
+    import os as _os
+    from mpi_pytorch_amd.parallel import dist as D
+    assert D.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    allowed = _os.sched_getaffinity(0)
+    if len(allowed) < 2:
+        pytest.skip("needs two CPUs")
+    keep = sorted(allowed)[: len(allowed) // 2]
+    dev = tmp_path / "0000:c1:00.0"
+    dev.mkdir()
+    (dev / "local_cpulist").write_text(",".join(str(c) for c in keep) + "\n")
+    (dev / "numa_node").write_text("1\n")
+    try:
+        info = D.pin_host_to_gpu(None, sysfs=str(tmp_path), addr="0000:c1:00.0")
+        assert info == {"pci": "0000:c1:00.0", "numa_node": 1, "cpus": len(keep)}
+        assert _os.sched_getaffinity(0) == set(keep)
+        assert D.pin_host_to_gpu(None, sysfs=str(tmp_path), addr="0000:c2:00.0") is None
+    finally:
+        _os.sched_setaffinity(0, allowed)
