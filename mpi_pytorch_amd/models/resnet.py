@@ -15,12 +15,13 @@ from .layers import Conv2d, BatchNorm2d, Linear, MaxPool2d, AdaptiveAvgPool2d, R
 from ..ops import functional as Fn
 
 
-# MPA_BN_LINK=1 enables the conv1 -> conv2 BN-backward hand-off (Fn.BNLink).  Off by
-# default: on ResNet-18 it removes 8 reduce passes (-335 us at batch 512) but the dgrad
-# epilogue that takes them over (z read, ReLU mask recomputed from z, two sums per
-# element) runs with the MFMA units idle, +350 us on the halo kernel alone (round-2
-# same-box A/B: 12.05 ms off vs 12.56 ms on; round 1 at batch 256: 11.45 vs 11.50).
-_LINK = os.environ.get("MPA_BN_LINK", "0") == "1"
+# The conv1 -> conv2 BN-backward hand-off (Fn.BNLink): conv2's halo dgrad epilogue does
+# bn1's backward reduction (mask recomputed from z, sums of g and g*xhat), so bn1's reduce
+# pass (8 per ResNet-18 step) disappears.  Rounds 1-3 measured it slower (-9 % at batch
+# 1024): that flavour spilled 250-550 B/lane to scratch in its 8-wave form.  Unspilled
+# (4-wave blocks, per-tile DPP reduction) it is +0.5 % (profiles/bn_link_ab_r4.txt).
+# MPA_BN_LINK=0 turns it off.
+_LINK = os.environ.get("MPA_BN_LINK", "1") == "1"
 # MPA_GRAD_JOIN=0 restores autograd's separate add of the two input-gradient contributions
 _JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
 # MPA_DS_DEFER=0: the downsample BN writes its output (instead of bn2 applying it on read)

@@ -62,9 +62,9 @@ def test_graph_replays_bitwise_equal_eager(det):
     gpu = det
     x, y = _batch(gpu)
     n = 100
-    # eager: the capture below runs 2 eager warmup steps before recording
+    # eager (capture's own warm-up steps are rolled back: TrainStep.capture)
     model, opt, step = _train(gpu)
-    ref = torch.stack([step(x, y).clone() for _ in range(n + 2)])[2:]
+    ref = torch.stack([step(x, y).clone() for _ in range(n)])
     torch.cuda.synchronize()
     ref_master = model._mpa_arena.master.clone()
     del model, opt, step
@@ -110,7 +110,7 @@ def _early_head_runs(gpu, x, y, nc):
     for u, v in zip(outs[0], outs[1]):
         assert torch.equal(torch.as_tensor(u), torch.as_tensor(v))
     model, opt, step = _train(gpu, nc=nc)
-    ref = torch.stack([step(x, y).clone() for _ in range(12)])[2:]
+    ref = torch.stack([step(x, y).clone() for _ in range(10)])
     torch.cuda.synchronize()
     ref_master = model._mpa_arena.master.clone()
     del model, opt, step
@@ -119,3 +119,52 @@ def _early_head_runs(gpu, x, y, nc):
     got = torch.stack([step(x, y).clone() for _ in range(10)])
     torch.cuda.synchronize()
     assert torch.equal(got, ref) and torch.equal(model._mpa_arena.master, ref_master)
+
+
+def test_dropout_graph_replays_draw_fresh_masks(gpu):
+    """Dropout's stream position lives in a device counter that the captured graph reads
+    and advances: two replays of the same captured dropout draw different masks (a
+    host-side offset would be frozen into the graph - one mask for every replay)."""
+    from mpi_pytorch_amd.ops import functional as Fn
+    x = torch.ones(64, 1024, device=gpu, dtype=torch.bfloat16)
+    Fn.dropout(x, 0.5, True)  # (warm the kernel outside capture)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = Fn.dropout(x, 0.5, True)
+    masks = []
+    for _ in range(3):
+        g.replay()
+        masks.append((y != 0).clone())
+    torch.cuda.synchronize()
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    for m in masks:  # still Bernoulli(0.5)
+        assert 0.45 < m.float().mean().item() < 0.55
+    # eager calls advance the same counter: two eager draws differ as well
+    a, b = Fn.dropout(x, 0.5, True), Fn.dropout(x, 0.5, True)
+    assert not torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,hw,B", [("alexnet", 64, 16), ("inception", 299, 4)])
+def test_dropout_models_graph_replays_bitwise_equal_eager(det, name, hw, B):
+    """Models with dropout (torchvision classifiers of AlexNet / Inception,
+    ``/root/reference/models.py:50,87``): replays of a captured step equal eager steps
+    bitwise in deterministic mode - every replay draws the mask the eager step would."""
+    from mpi_pytorch_amd.ops import functional as Fn
+    gpu = det
+    x, y = _batch(gpu, B=B, hw=hw, nc=100, seed=3)
+    n = 6
+    rng0 = Fn.DropoutRNG.state()
+    model, opt, step = _train(gpu, name=name, nc=100)
+    ref = torch.stack([step(x, y).clone() for _ in range(n)])
+    torch.cuda.synchronize()
+    ref_master = model._mpa_arena.master.clone()
+    del model, opt, step
+    Fn.DropoutRNG.set_state(rng0)
+    model, opt, step = _train(gpu, name=name, nc=100)
+    assert step.capture(x, y, warmup=2)
+    got = torch.stack([step(x, y).clone() for _ in range(n)])
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got, ref)
+    assert torch.equal(model._mpa_arena.master, ref_master)
