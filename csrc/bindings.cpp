@@ -406,20 +406,25 @@ void bn_defer_step(Tensor sums, Tensor gamma, Tensor mean, Tensor rstd, int64_t 
                      into ? bpm(*out) : nullptr, cur_stream());
 }
 
+static int row_stride(const Tensor& t);  // (below, with the BN helpers)
+
 std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rstd,
                                  Tensor gamma, Tensor dgamma, Tensor dbeta, Tensor sums,
                                  bool want_dx, bool want_g) {
-  CHECK_ACT(dy);
+  CHECK_CUDA(dy);
+  CHECK_BF16(dy);
+  const int lddy = row_stride(dy);  // (a channel window of a wider buffer, or contiguous)
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0 && sums.numel() == 2 * C, "bn_bwd_apply: shapes");
+  TORCH_CHECK(C % 8 == 0 && sums.numel() == 2 * C && dy.size(-1) == C && lddy % 8 == 0,
+              "bn_bwd_apply: shapes");
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor dx = want_dx ? torch::empty_like(x) : Tensor();
   Tensor gout = want_g ? torch::empty_like(x) : Tensor();
   mpa::bn_bwd_apply(bp(dy), bp(x), bopt(y), fopt(mean), fopt(rstd), fopt(gamma),
                     fopt_mut(dgamma), fopt_mut(dbeta), M, C, want_dx ? bpm(dx) : nullptr,
-                    want_g ? bpm(gout) : nullptr, fopt(sums), cur_stream());
+                    want_g ? bpm(gout) : nullptr, fopt(sums), cur_stream(), lddy);
   return {dx, gout};
 }
 
@@ -525,7 +530,8 @@ static std::vector<int64_t> with_last(const Tensor& x, int64_t c) {
 std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor beta, Tensor rmean,
                                  Tensor rvar, double momentum, double eps, Tensor res, bool relu,
                                  c10::optional<Tensor> counter, c10::optional<Tensor> mask,
-                                 int64_t channels, c10::optional<Tensor> res_affine) {
+                                 int64_t channels, c10::optional<Tensor> res_affine,
+                                 c10::optional<Tensor> out) {
   int C, ldx, M;
   bn_prefix(x, channels, &C, &ldx, &M);
   const c10::OptionalDeviceGuard g(device_of(x));
@@ -550,7 +556,23 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
     mpa::bn_stats(bp(x), M, C, fopt(rmean), st.data_ptr<float>(), ws.data_ptr<float>(),
                   cur_stream());
   }
-  Tensor y = torch::empty(with_last(x, C), x.options());
+  // out (optional): write y into this bf16 channel window of a wider NHWC buffer (a block
+  // output at the branch's channel offset: concat without a copy)
+  const bool into = out && out->defined() && out->numel() > 0;
+  int ldy = C;
+  Tensor y;
+  if (into) {
+    CHECK_CUDA(*out);
+    CHECK_BF16(*out);
+    TORCH_CHECK(out->sizes() == c10::IntArrayRef(with_last(x, C)) && !has(res) &&
+                    !(mask && mask->defined() && mask->numel()),
+                "bn_fwd_train: out must have the output's shape (no residual / mask)");
+    ldy = row_stride(*out);
+    TORCH_CHECK(ldy % 8 == 0, "bn_fwd_train: out row stride must be a multiple of 8");
+    y = *out;
+  } else {
+    y = torch::empty(with_last(x, C), x.options());
+  }
   if (has(res)) TORCH_CHECK(res.numel() == y.numel(), "bn_fwd_train: residual shape");
   const float* raff = nullptr;
   if (res_affine && res_affine->defined() && res_affine->numel() > 0) {
@@ -564,7 +586,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, Tensor stats, Tensor gamma, Tensor be
                     mean.data_ptr<float>(), rstd.data_ptr<float>(),
                     (counter && counter->defined() && counter->numel() == 1)
                         ? counter->data_ptr<int64_t>() : nullptr,
-                    cur_stream(), ymask_ptr(mask, y), ldx, lds, raff);
+                    cur_stream(), into ? nullptr : ymask_ptr(mask, y), ldx, lds, raff, ldy);
   return {y, mean, rstd};
 }
 
@@ -638,10 +660,15 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
                            Tensor dgamma, Tensor dbeta, bool want_dx, bool want_g,
                            c10::optional<Tensor> zmask_beta, c10::optional<Tensor> ymask,
                            c10::optional<Tensor> gacc, c10::optional<Tensor> dx_out) {
-  CHECK_ACT(dy);
+  // dy: contiguous or a channel window of a wider buffer (a branch's slice of a block
+  // output gradient), row stride lddy
+  CHECK_CUDA(dy);
+  CHECK_BF16(dy);
+  const int lddy = row_stride(dy);
   CHECK_CUDA(x);
   CHECK_BF16(x);
   const int C = dy.size(-1);
+  TORCH_CHECK(lddy % 8 == 0, "bn_bwd: dy row stride must be a multiple of 8");
   // x: same channels as dy (contiguous or a channel-window view), or a contiguous wider
   // buffer whose first C channels are the BN input (a DenseNet block prefix)
   const int ldx = (x.size(-1) > C) ? (x.is_contiguous() ? (int)x.size(-1) : -1) : row_stride(x);
@@ -670,8 +697,10 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
     TORCH_CHECK(lddx % 8 == 0, "bn_bwd: dx_out row stride must be a multiple of 8");
   }
   const c10::OptionalDeviceGuard g(device_of(x));
-  Tensor dx = (want_dx && !acc) ? (into ? *dx_out : torch::empty_like(dy)) : Tensor();
-  Tensor gout = want_g ? torch::empty_like(dy) : Tensor();
+  Tensor dx = (want_dx && !acc)
+                  ? (into ? *dx_out : torch::empty(dy.sizes(), dy.options()))
+                  : Tensor();
+  Tensor gout = want_g ? torch::empty(dy.sizes(), dy.options()) : Tensor();
   Tensor ws = torch::empty({mpa::bn_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
   const Tensor zb = (zmask_beta && zmask_beta->defined()) ? *zmask_beta : Tensor();
   if (has(zb)) TORCH_CHECK(zb.numel() == C, "bn_bwd: zmask beta size");
@@ -680,7 +709,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
               want_g ? bpm(gout) : nullptr, ws.data_ptr<float>(), cur_stream(), fopt(zb),
               ymask_ptr(ymask, dy), ldx, acc ? (float*)gacc->data_ptr() : nullptr,
               acc ? (int)gacc->size(-1) : 0, lddx,
-              acc && gacc->scalar_type() == torch::kBFloat16);
+              acc && gacc->scalar_type() == torch::kBFloat16, lddy);
   return {dx, gout};
 }
 
@@ -1068,6 +1097,17 @@ void zero_f32(Tensor t) {
   mpa::zero_f32(t.data_ptr<float>(), t.numel(), cur_stream());
 }
 
+void add_f32_(Tensor dst, Tensor src) {
+  CHECK_CUDA(dst);
+  CHECK_F32(dst);
+  CHECK_F32(src);
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous() && dst.numel() == src.numel() &&
+                  src.device() == dst.device(),
+              "add_f32_: contiguous fp32 tensors of equal size on one device");
+  const c10::OptionalDeviceGuard g(device_of(dst));
+  mpa::add_f32(dst.data_ptr<float>(), src.data_ptr<float>(), dst.numel(), cur_stream());
+}
+
 void step_inc(Tensor step) {
   CHECK_CUDA(step);
   CHECK_F32(step);
@@ -1385,7 +1425,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
         py::arg("res"), py::arg("relu"), py::arg("counter") = py::none(),
         py::arg("mask") = py::none(), py::arg("channels") = 0,
-        py::arg("res_affine") = py::none());
+        py::arg("res_affine") = py::none(), py::arg("out") = py::none());
   m.def("bn_stats_affine", &bn_stats_affine, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("counter") = py::none());
@@ -1436,6 +1476,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zero_f32", &zero_f32, "t.zero_() on the native path");
   m.def("zero_cols_f32", &zero_cols_f32, "zero columns [first, first+count) of t as [-1, period]");
   m.def("add_bf16_", &add_bf16_, "a += b (bf16, fp32 add)");
+  m.def("add_f32_", &add_f32_, "dst += src (fp32)");
   m.def("step_inc", &step_inc);
   m.def("chan_accum", &chan_accum, "fp32 G[..., off:off+C] (+)= bf16 src");
   m.def("chan_extract", &chan_extract, "bf16 copy of fp32 G[..., off:off+C]");

@@ -212,7 +212,8 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
                   uint8_t* ymask = nullptr,  // optional ReLU bit mask of y ([M*C/8] bytes)
                   int ldx = 0,   // x row stride (0: C) - a channel prefix of a wider buffer
                   int lds = 0,   // stats = [mean | var] rows lds apart (0: C)
-                  const float* res_aff = nullptr);  // [2][C]: res enters as res * aff0 + aff1
+                  const float* res_aff = nullptr,  // [2][C]: res enters as res * aff0 + aff1
+                  int ldy = 0);  // y row stride (0: C) - a channel window of a wider buffer
 // mean / rstd / running stats / num_batches_tracked of a train-mode BN whose apply pass is
 // deferred to its consumer; aff [2][C] = [gamma rstd | beta - mean gamma rstd]
 void bn_stats_affine(const float* stats, const float* gamma, const float* beta, float* rmean,
@@ -235,10 +236,12 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
             float* gacc = nullptr,   // non-null: dx ADDED in fp32 into gacc [M][ldg] (dx unused)
             int ldg = 0,
             int lddx = 0,            // dx row stride (0: C) - a channel window of a wider buffer
-            bool gacc_bf16 = false); // gacc holds bf16 (cast the pointer) instead of fp32
+            bool gacc_bf16 = false,  // gacc holds bf16 (cast the pointer) instead of fp32
+            int lddy = 0);           // dy row stride (0: C) - a channel window of a wider buffer
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
-                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s);
+                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s,
+                  int lddy = 0);
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,
              float* ws, hipStream_t s);
 void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s);
@@ -313,6 +316,7 @@ void ce_fwd_weighted(const bf16_raw* logits, const int64_t* labels, int B, int N
                      float* lse, hipStream_t s);
 // fp32 t[0:n) = 0 (n % 4 == 0, 16-B aligned); step[0] += 1
 void zero_f32(float* t, int64_t n, hipStream_t s);
+void add_f32(float* dst, const float* src, int64_t n, hipStream_t s);  // dst += src
 // t as [rows][period] fp32: zero columns [first, first + count)
 void zero_cols_f32(float* t, int64_t rows, int period, int first, int count, hipStream_t s);
 // a += b, bf16 [n] (n % 8 == 0, 16-B aligned)

@@ -220,7 +220,8 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
                                               bf16_t* __restrict__ y,
                                               uint8_t* __restrict__ ym = nullptr,
                                               const float* rsc = nullptr,
-                                              const float* rsh = nullptr) {
+                                              const float* rsh = nullptr, int ldy = 0) {
+  if (ldy <= 0) ldy = C;
   sweep_rows_pl<UNR, 2>(
       cm, M,
       [&](int r, uint4 (&v)[2]) {
@@ -249,7 +250,7 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
         const uint4 pk = pack8(f);
-        *(uint4*)(y + (size_t)r * C + c0) = pk;
+        *(uint4*)(y + (size_t)r * ldy + c0) = pk;
         if constexpr (YM) ym[(size_t)r * (C / 8) + c0 / 8] = (uint8_t)posmask8(pk);
       });
 }
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     float momentum, float eps, const bf16_t* __restrict__ res, int relu, int M, int C,
     bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
     unsigned long long* __restrict__ counter, uint8_t* __restrict__ ymask, int ldx, int lds,
-    const float* __restrict__ res_aff) {
+    const float* __restrict__ res_aff, int ldy) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
@@ -291,9 +292,10 @@ __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
     }
   }
   if (res_aff)
-    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask, rsc, rsh);
+    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask, rsc, rsh, ldy);
   else
-    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask);
+    bn_apply_rows<UNR, YM>(cm, M, C, ldx, c0, sc, sh, x, res, relu, y, ymask, nullptr, nullptr,
+                           ldy);
 }
 
 // Train-mode BN whose apply pass is deferred to its consumer (bn_fwd_train's res_aff): the
@@ -407,7 +409,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, int M, int C,
-    float* __restrict__ slab, float* __restrict__ sums, const uint8_t* __restrict__ ym, int ldx) {
+    float* __restrict__ slab, float* __restrict__ sums, const uint8_t* __restrict__ ym, int ldx,
+    int lddy) {
   __shared__ float red[256 * 8];
   const ColMap cm = colmap(C / 8);
   float sg[8], sgx[8];
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       for (int u = 0; u < UNR; ++u) {
         if (u < n) {
           const size_t off = (size_t)(r + u * st) * C + c0;
-          dv[u] = *(const uint4*)(dy + off);
+          dv[u] = *(const uint4*)(dy + (size_t)(r + u * st) * lddy + c0);
           xr[u] = *(const uint4*)(x + (size_t)(r + u * st) * ldx + c0);
           if (ym) mb[u] = ym[off / 8];
           else if (y) yr[u] = *(const uint4*)(y + off);
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ ws,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int M, int C,
     bf16_t* __restrict__ dx, bf16_t* __restrict__ gout, const uint8_t* __restrict__ ym, int ldx,
-    float* __restrict__ gacc, int ldg, int lddx) {
+    float* __restrict__ gacc, int ldg, int lddx, int lddy) {
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       cm, M,
       [&](int r, uint4 (&v)[ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)]) {
         const size_t off = (size_t)r * C + c0;
-        v[0] = *(const uint4*)(dy + off);
+        v[0] = *(const uint4*)(dy + (size_t)r * lddy + c0);
         if constexpr (YM) v[2].x = ym[off / 8];
         else if (y) v[2] = *(const uint4*)(y + off);
         if (need_x) v[1] = *(const uint4*)(x + (size_t)r * ldx + c0);
@@ -1367,17 +1370,18 @@ void bn_fwd_train(const bf16_raw* x, const float* stats, const float* gamma, con
                   float* rmean, float* rvar, float momentum, float eps, const bf16_raw* res,
                   int relu, int M, int C, bf16_raw* y, float* mean, float* rstd,
                   int64_t* counter, hipStream_t s, uint8_t* ymask, int ldx, int lds,
-                  const float* res_aff) {
+                  const float* res_aff, int ldy) {
   if (ldx <= 0) ldx = C;
   if (lds <= 0) lds = C;
+  if (ldy <= 0) ldy = C;
   if (ymask)
     BN_LAUNCH_T(bn_fwd_train_kernel, true, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
                 momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
-                ldx, lds, res_aff);
+                ldx, lds, res_aff, ldy);
   else
     BN_LAUNCH_T(bn_fwd_train_kernel, false, grid_for(M, C), s, x, stats, gamma, beta, rmean, rvar,
                 momentum, eps, res, relu, M, C, y, mean, rstd, (unsigned long long*)counter, ymask,
-                ldx, lds, res_aff);
+                ldx, lds, res_aff, ldy);
 }
 
 void bn_stats_affine(const float* stats, const float* gamma, const float* beta, float* rmean,
@@ -1398,16 +1402,18 @@ void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const
 void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
             const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M, int C,
             bf16_raw* dx, bf16_raw* g, float* ws, hipStream_t s, const float* zmask_beta,
-            const uint8_t* ymask, int ldx, float* gacc, int ldg, int lddx, bool gacc_bf16) {
+            const uint8_t* ymask, int ldx, float* gacc, int ldg, int lddx, bool gacc_bf16,
+            int lddy) {
   // ws layout: [2C] final sums | [gx][2C] per-block partials
   if (ldx <= 0) ldx = C;
   if (lddx <= 0) lddx = C;
+  if (lddy <= 0) lddy = C;
   const dim3 gr = grid_for(M, C);
   float* slab = ws + 2 * C;
   const float* zb = (y || ymask) ? nullptr : zmask_beta;
   if (ymask) y = nullptr;
   BN_LAUNCH(bn_bwd_reduce_kernel, gr, s, dy, x, y, mean, rstd, gamma, zb, M, C, slab, ws, ymask,
-            ldx);
+            ldx, lddy);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
   if (gacc) {  // dense-block accumulator: dx added into gacc (no ymask, no g)
     const int u = bn_unr();
@@ -1415,7 +1421,7 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
 #define BN_ACC_LAUNCH(U, A)                                                                 \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<U, false, A>), ga, dim3(256), 0, s, dy, x, y, mean, \
                      rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,             \
-                     (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C)
+                     (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C, lddy)
     if (gacc_bf16) {
       if (u == 4) BN_ACC_LAUNCH(4, 2);
       else if (u == 2) BN_ACC_LAUNCH(2, 2);
@@ -1428,20 +1434,21 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
 #undef BN_ACC_LAUNCH
   } else if (ymask)
     BN_LAUNCH_T(bn_bwd_apply_kernel, true, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb, ws,
-                dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx);
+                dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx, lddy);
   else
     BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb,
-                ws, dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx);
+                ws, dgamma, dbeta, M, C, dx, g, ymask, ldx, (float*)nullptr, 0, lddx, lddy);
 }
 
 // apply pass only, with the reduction sums [sum g | sum g*xhat] already in `sums` (e.g.
 // from the fused dgrad epilogue, igemm_rows_dgrad_bnred)
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
-                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s) {
+                  int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s, int lddy) {
+  if (lddy <= 0) lddy = C;
   BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
               (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr, C,
-              (float*)nullptr, 0, C);
+              (float*)nullptr, 0, C, lddy);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,

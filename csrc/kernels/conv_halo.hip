@@ -373,11 +373,12 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       cst[3 * HB_BN + tid] = __builtin_fmaf(-b, sc, p.ep_beta[n0 + tid]);
     }
   }
-  // TRED (fused BN-backward reduction): the column sums are reduced per TILE (DPP over the
-  // 16 pixel lanes) and accumulated in this wave's slot of `red`, so no sums live in
-  // registers through the MFMA stream.  Holding them for the block's life (as the
-  // statistics flavours do) put this flavour at 256 VGPRs with 344-556 B/lane of scratch
-  // spills - the round-2/3 "BN link is slower" measurements were those spills.
+  // TRED (fused BN-backward reduction): the column sums are reduced per tile and column
+  // group (DPP over the 16 pixel lanes) and accumulated in this wave's slot of `red`, so
+  // no sums live in registers through the MFMA stream and at most 8 through the epilogue.
+  // Holding them for the block's life (as the statistics flavours do) put this flavour at
+  // 256 VGPRs with 344-556 B/lane of scratch spills - the round-2/3 "BN link is slower"
+  // measurements were those spills.
   constexpr bool TRED = (EPI & EP_BNRED) != 0;
   if constexpr (TRED) ((float2*)red)[tid] = make_float2(0.f, 0.f);  // own wave's slot
   float ss[4][4], sq[4][4];
@@ -422,23 +423,22 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   // Epilogue of a whole tile (see TRED)
   auto epi_tile = [&](int m0e, auto full) {
     if constexpr (TRED) {
-      float ts[4][4], tq[4][4];
-#pragma unroll
-      for (int jn = 0; jn < 4; ++jn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { ts[jn][r] = 0.f; tq[jn][r] = 0.f; }
       constexpr bool F = decltype(full)::value;
+      float* rd = (float*)red;
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) {
         // this column group's mean / rstd / mask affine, read from LDS per tile (an empty
         // asm memory clobber keeps the compiler from hoisting 64 VGPRs of them out of the
-        // tile loop)
+        // tile loop); its sums live only across its 4 row fragments (32 live sums spilled)
         asm volatile("" ::: "memory");
         const int c = jn * 16 + jq * 4;
         const f32x4 colb = *LDS_PTR(const f32x4, cst + c);
         const f32x4 cols = *LDS_PTR(const f32x4, cst + HB_BN + c);
         const f32x4 mc = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
         const f32x4 mh = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+        float ts[4][4], tq[4][4];  // (only row jn is used)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { ts[jn][r] = 0.f; tq[jn][r] = 0.f; }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = m0e + wave * 64 + i * 16 + l15;
@@ -446,10 +446,6 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
           epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh,
                            ts[jn], tq[jn]);
         }
-      }
-      float* rd = (float*)red;
-#pragma unroll
-      for (int jn = 0; jn < NJ; ++jn) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           ts[jn][r] = row16_sum(ts[jn][r]);
@@ -926,19 +922,19 @@ static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPla
                        a, h);
 }
 
-// The fused BN-backward reduction runs in 4-wave blocks (MPA_HALO_BNRED_PROD=1: producer
-// waves): with 8 waves per CU a wave has 256 registers in all, and that flavour's
-// preloaded z tile + reduction epilogue spilled 250-550 B/lane to scratch there
-// (-Rpass-analysis=kernel-resource-usage); a 4-wave block's waves also get the AGPR half.
+// MPA_HALO_BNRED_PROD=0: the fused BN-backward reduction flavour in 4-wave blocks.  With
+// producer waves a wave has 256 registers in all; that flavour used to spill 250-550
+// B/lane there (its column sums lived across a whole tile's epilogue).  Reduced per column
+// group (TRED) it needs ~216 VGPRs and no scratch, so it follows MPA_HALO_PROD.
 static const bool g_halo_bnred_prod = [] {
   const char* e = getenv("MPA_HALO_BNRED_PROD");
-  return e && atoi(e) != 0;
+  return !(e && atoi(e) == 0);
 }();
 
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  const bool prod = (EPI & EP_BNRED) ? g_halo_bnred_prod : g_halo_prod;
+  const bool prod = g_halo_prod && (!(EPI & EP_BNRED) || g_halo_bnred_prod);
   if (prod) launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
   else launch_halo_k<EPI, false, 4>(wres, grid, a, h, s);
 }

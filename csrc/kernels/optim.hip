@@ -196,6 +196,14 @@ __global__ __launch_bounds__(256) void zero_f32_kernel(float4* __restrict__ t, i
 
 __global__ void step_inc_kernel(float* step) { *step += 1.f; }
 
+// dst[i] += src[i] (fp32; small vectors: a bias gradient from a fused reduction)
+__global__ __launch_bounds__(256) void add_f32_kernel(float* __restrict__ dst,
+                                                     const float* __restrict__ src, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+
 // t viewed as [rows][period] fp32: zero columns [first, first + count) of every row (the
 // pixel-pair stem's weight-gradient column past the kernel, layers.Conv2d.fix_grad)
 __global__ __launch_bounds__(256) void zero_cols_f32_kernel(float* __restrict__ t, int64_t rows,
@@ -241,6 +249,12 @@ void zero_f32(float* t, int64_t n, hipStream_t s) {
   const int64_t n4 = n / 4;
   if (n4 > 0)
     hipLaunchKernelGGL(zero_f32_kernel, dim3(blocks_for(n4)), dim3(256), 0, s, (float4*)t, n4);
+}
+
+void add_f32(float* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(add_f32_kernel, dim3(std::min<int64_t>((n + 255) / 256, 1024)), dim3(256),
+                       0, s, dst, src, n);
 }
 
 static void step_inc_launch(float* step, hipStream_t s) {

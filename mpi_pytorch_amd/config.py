@@ -80,6 +80,7 @@ class Config:
     eval_lanes: int = 1                    # predictor lanes in the eval pipeline
     eval_batch: int = 64
     eval_assign: str = "random"            # random (reference) | roundrobin
+    eval_src: int = 0                      # synthetic eval source side (0: the model input size)
     max_steps: int = 0                     # stop an epoch early (0 = full epoch)
     checksum_every: int = 0                # cross-rank replica checksum period (steps, 0=off)
     timeout_s: float = 1800.0              # rendezvous/collective timeout

@@ -352,7 +352,12 @@ def run_pipeline(cfg: Config, ckpt_path: Optional[str] = None, max_images: int =
     if not cfg.synthetic and images_available(cfg.TRAIN_DIR, names):
         source = FolderImages(cfg.TRAIN_DIR, cfg.num_workers)  # reads TRAIN_DIR like :59
     else:
-        source = SyntheticImages((2 * out_hw[0], 2 * out_hw[1]))
+        # synthetic sources at the model's input size by default (eval_src > 0: that side):
+        # the resize stage still runs (PIL-exact bicubic), but stage 0 copies and the H2D
+        # link carries 150 KB per 224^2 image instead of the 600 KB of a 448^2 source,
+        # which capped the pipeline near PCIe's ~50 GB/s / 600 KB = 83k img/s
+        side = cfg.eval_src
+        source = SyntheticImages((side, side) if side > 0 else tuple(out_hw))
     model = load_predictor(cfg, world.device, ckpt_path)
     pipe = StreamPipeline(model, world.device, out_hw, cfg.eval_lanes, assign=cfg.eval_assign,
                           seed=cfg.seed + world.rank)

@@ -31,8 +31,8 @@ class BasicConv2d(nn.Module):
         self.conv = Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False)
         self.bn = BatchNorm2d(out_channels, eps=0.001)
 
-    def forward(self, x, join=None):
-        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True, join_x=join)
+    def forward(self, x, join=None, out=None):
+        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True, join_x=join, out=out)
 
 
 def _avg3(x, join=None):
@@ -59,11 +59,11 @@ class PoolBranch(BasicConv2d):
     # (kh, kw, sh, sw, ph, pw, ceil, cip) for this member (Fn.conv1x1_group)
     pool_after = (3, 3, 1, 1, 1, 1, False, True)
 
-    def forward(self, x, join=None):
+    def forward(self, x, join=None, out=None):
         if _POOL_FIRST:
-            return super().forward(_avg3(x, join))
+            return super().forward(_avg3(x, join), out=out)
         return Fn.bn_act(_avg3(Fn.conv_act(x, self.conv, relu=False, join=join)), self.bn,
-                         relu=True)
+                         relu=True, out=out)
 
 
 def _max3s2(x, join=None):
@@ -72,6 +72,40 @@ def _max3s2(x, join=None):
 
 def _cat(xs):
     return Fn.cat_channels(xs)
+
+
+# MPA_CAT_INTO=0: branch outputs are separate tensors copied into the block output
+# (concat_kernel forward, split backward) instead of written at their channel offsets
+_CAT_INTO = os.environ.get("MPA_CAT_INTO", "1") == "1"
+
+
+def _buffer(mod, x, hw, widths):
+    """The block output every branch writes its result into at its channel offset (a
+    Fn.ChannelBuffer), in training; None otherwise (the branches' outputs are then
+    concatenated by a copy)."""
+    if not (_CAT_INTO and mod.training and torch.is_grad_enabled()):
+        return None
+    return Fn.ChannelBuffer(x, hw, widths)
+
+
+class _NoBuffer:
+    """Stand-in for a missing ChannelBuffer: no destination windows, concat by copy."""
+
+    @staticmethod
+    def window(i):
+        return None
+
+    @staticmethod
+    def gather(parts):
+        return _cat(parts)
+
+
+def _out(cb):
+    return cb if cb is not None else _NoBuffer
+
+
+def _half(n: int) -> int:
+    return (n - 3) // 2 + 1  # 3x3 / stride 2 / no padding
 
 
 def _heads(mod, x, heads):
@@ -110,15 +144,19 @@ class InceptionA(nn.Module):
         return [self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
+        cb = _out(_buffer(self, x, x.shape[1:3],
+                          [64, 64, 96, self.branch_pool.conv.out_channels]))
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
-            b1, b5, b3, bp = Fn.conv1x1_group(x, self.heads(), join)
+            b1, b5, b3, bp = Fn.conv1x1_group(x, self.heads(), join,
+                                              [cb.window(0), None, None, cb.window(3)])
         else:
             j = _join(self, x, 4, join)
-            b1, b5, b3 = self.branch1x1(x, j), self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
-            bp = self.branch_pool(x, j)
-        b5 = self.branch5x5_2(b5)
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(b3))
-        return _cat([b1, b5, b3, bp])
+            b1 = self.branch1x1(x, j, out=cb.window(0))
+            b5, b3 = self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
+            bp = self.branch_pool(x, j, out=cb.window(3))
+        b5 = self.branch5x5_2(b5, out=cb.window(1))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(b3), out=cb.window(2))
+        return cb.gather([b1, b5, b3, bp])
 
 
 class InceptionB(nn.Module):
@@ -131,9 +169,12 @@ class InceptionB(nn.Module):
 
     def forward(self, x, join=None):
         j = _join(self, x, 3, join)
-        b3 = self.branch3x3(x, j)
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)))
-        return _cat([b3, bd, _max3s2(x, j)])
+        cb = _out(_buffer(self, x, (_half(x.shape[1]), _half(x.shape[2])),
+                          [384, 96, x.shape[-1]]))
+        b3 = self.branch3x3(x, j, out=cb.window(0))
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)),
+                                 out=cb.window(1))
+        return cb.gather([b3, bd, _max3s2(x, j)])
 
 
 class InceptionC(nn.Module):
@@ -155,18 +196,20 @@ class InceptionC(nn.Module):
         return [self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
+        cb = _out(_buffer(self, x, x.shape[1:3], [192, 192, 192, 192]))
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
-            b1, b7, bd, bp = Fn.conv1x1_group(x, self.heads(), join)
+            b1, b7, bd, bp = Fn.conv1x1_group(x, self.heads(), join,
+                                              [cb.window(0), None, None, cb.window(3)])
         else:
             j = _join(self, x, 4, join)
-            b1, b7, bd = (self.branch1x1(x, j), self.branch7x7_1(x, j),
-                          self.branch7x7dbl_1(x, j))
-            bp = self.branch_pool(x, j)
-        b7 = self.branch7x7_3(self.branch7x7_2(b7))
-        for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
-                  self.branch7x7dbl_5):
+            b1 = self.branch1x1(x, j, out=cb.window(0))
+            b7, bd = self.branch7x7_1(x, j), self.branch7x7dbl_1(x, j)
+            bp = self.branch_pool(x, j, out=cb.window(3))
+        b7 = self.branch7x7_3(self.branch7x7_2(b7), out=cb.window(1))
+        for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4):
             bd = m(bd)
-        return _cat([b1, b7, bd, bp])
+        bd = self.branch7x7dbl_5(bd, out=cb.window(2))
+        return cb.gather([b1, b7, bd, bp])
 
 
 class InceptionD(nn.Module):
@@ -190,10 +233,13 @@ class InceptionD(nn.Module):
         else:
             j = _join(self, x, 3, join)
             b3, b7 = self.branch3x3_1(x, j), self.branch7x7x3_1(x, j)
-        b3 = self.branch3x3_2(b3)
-        for m in (self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4):
+        cb = _out(_buffer(self, x, (_half(x.shape[1]), _half(x.shape[2])),
+                          [320, 192, x.shape[-1]]))
+        b3 = self.branch3x3_2(b3, out=cb.window(0))
+        for m in (self.branch7x7x3_2, self.branch7x7x3_3):
             b7 = m(b7)
-        return _cat([b3, b7, _max3s2(x, j)])
+        b7 = self.branch7x7x3_4(b7, out=cb.window(1))
+        return cb.gather([b3, b7, _max3s2(x, j)])
 
 
 class InceptionE(nn.Module):
@@ -213,20 +259,25 @@ class InceptionE(nn.Module):
         return [self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1, self.branch_pool]
 
     def forward(self, x, join=None):
+        # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
+        # as one flat buffer of six windows
+        cb = _out(_buffer(self, x, x.shape[1:3], [320, 384, 384, 384, 384, 192]))
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
-            b1, b3, bd, bp = Fn.conv1x1_group(x, self.heads(), join)
+            b1, b3, bd, bp = Fn.conv1x1_group(x, self.heads(), join,
+                                              [cb.window(0), None, None, cb.window(5)])
         else:
             j = _join(self, x, 4, join)
-            b1, b3, bd = self.branch1x1(x, j), self.branch3x3_1(x, j), self.branch3x3dbl_1(x, j)
-            bp = self.branch_pool(x, j)
+            b1 = self.branch1x1(x, j, out=cb.window(0))
+            b3, bd = self.branch3x3_1(x, j), self.branch3x3dbl_1(x, j)
+            bp = self.branch_pool(x, j, out=cb.window(5))
         j3 = _join(self, b3, 2)  # b3 and bd each feed a (1x3) and a (3x1) conv
-        b3a, b3b = self.branch3x3_2a(b3, j3), self.branch3x3_2b(b3, j3)
+        b3a = self.branch3x3_2a(b3, j3, out=cb.window(1))
+        b3b = self.branch3x3_2b(b3, j3, out=cb.window(2))
         bd = self.branch3x3dbl_2(bd)
         jd = _join(self, bd, 2)
-        bda, bdb = self.branch3x3dbl_3a(bd, jd), self.branch3x3dbl_3b(bd, jd)
-        # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
-        # as one flat concat, which copies every branch once instead of twice
-        return _cat([b1, b3a, b3b, bda, bdb, bp])
+        bda = self.branch3x3dbl_3a(bd, jd, out=cb.window(3))
+        bdb = self.branch3x3dbl_3b(bd, jd, out=cb.window(4))
+        return cb.gather([b1, b3a, b3b, bda, bdb, bp])
 
 
 class InceptionAux(nn.Module):

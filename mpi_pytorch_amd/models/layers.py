@@ -432,6 +432,11 @@ class Flatten(nn.Module):
         return x.reshape(x.shape[0], -1)
 
 
+# MPA_SEQ_LINK=0: conv -> ReLU -> conv chains of the feature stacks run the separate ReLU
+# backward (act_bwd) / BN reduce pass instead of the consumer dgrad's fused reduction
+_LINK = os.environ.get("MPA_SEQ_LINK", "1") == "1"
+
+
 class FusedSequential(nn.Sequential):
     """``nn.Sequential`` with torchvision indices, executed with producer fusion:
     Conv(no bias)->BN[->ReLU] => conv_bn_act; Conv->ReLU => conv_act(relu); Linear->ReLU
@@ -457,18 +462,45 @@ class FusedSequential(nn.Sequential):
             i += k
         return out
 
-    def run_group(self, g, x):
-        """Execute fused group ``g`` = (first, end, kind) of :meth:`groups` on ``x``."""
+    def run_group(self, g, x, link_in=None, link_out=None):
+        """Execute fused group ``g`` = (first, end, kind) of :meth:`groups` on ``x``;
+        ``link_in`` / ``link_out``: BN-backward hand-offs (Fn.BNLink) with the neighbouring
+        conv group (see :meth:`links`)."""
         mods = list(self._modules.values())
         i, _e, kind = g
         if kind.startswith("conv_bn"):
-            return Fn.conv_bn_act(x, mods[i], mods[i + 1], relu=kind == "conv_bn_relu")
+            return Fn.conv_bn_act(x, mods[i], mods[i + 1], relu=kind == "conv_bn_relu",
+                                  link_in=link_in, link_out=link_out)
         if kind == "relu":
+            if isinstance(mods[i], Conv2d):
+                return Fn.conv_act(x, mods[i], relu=True, link_in=link_in, link_out=link_out)
             return mods[i](x, relu=True)
         return mods[i](x)
 
+    def links(self, gs):
+        """Which consecutive groups hand the backward over: a conv -> (BN ->) ReLU group
+        whose output feeds ONLY the next conv group (VGG / AlexNet feature stacks).  The
+        consumer's dgrad then applies the producer's ReLU mask and reduces its BN (or
+        bias) gradient sums in its epilogue - no reduce / act_bwd pass (Fn.BNLink)."""
+        mods = list(self._modules.values())
+        out = [False] * len(gs)
+        if not (self.training and torch.is_grad_enabled() and _LINK):
+            return out
+        for k in range(len(gs) - 1):
+            (i, _e, kind), (j, _f, kind2) = gs[k], gs[k + 1]
+            if (kind in ("relu", "conv_bn_relu") and isinstance(mods[i], Conv2d)
+                    and kind2 in ("relu", "conv_bn_relu", "conv_bn")
+                    and isinstance(mods[j], Conv2d) and not mods[j].pair):
+                out[k] = True
+        return out
+
     def forward(self, x):
         run = self.run_group
-        for g in self.groups():
-            x = run(g, x)
+        gs = self.groups()
+        lk = self.links(gs)
+        link = None
+        for k, g in enumerate(gs):
+            nxt = Fn.BNLink() if lk[k] else None
+            x = run(g, x, link_in=link, link_out=nxt)
+            link = nxt
         return x

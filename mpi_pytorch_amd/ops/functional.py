@@ -214,7 +214,7 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None,
-                join_x=None, join_res=None, defer=None, res_affine=None):
+                join_x=None, join_res=None, defer=None, res_affine=None, out=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
@@ -237,14 +237,16 @@ class _ConvBNAct(torch.autograd.Function):
                                            bn.running_var, bn.momentum_value(), bn.eps,
                                            _or_empty(residual, x), relu,
                                            bn.num_batches_tracked, mask=ymask,
-                                           res_affine=res_affine)
+                                           res_affine=res_affine, out=out)
         ctx.conv = conv
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.bias = b
         ctx.params = (w, gamma, beta)
         ctx.in_hw = (x.shape[1], x.shape[2])
-        ctx.save_for_backward(x, z, y if (relu and ymask is None) else None, mean, rstd, ymask)
+        # (relu(bn(z)) without a residual recomputes its mask from z: y is not kept)
+        keep_y = relu and ymask is None and not (residual is None and beta is not None)
+        ctx.save_for_backward(x, z, y if keep_y else None, mean, rstd, ymask)
         ctx.link_in = link_in
         ctx.link_out = link_out
         ctx.join_x = join_x
@@ -266,7 +268,7 @@ class _ConvBNAct(torch.autograd.Function):
         w, gamma, beta = ctx.params
         conv = ctx.conv
         k = K(dy)
-        dy = dy.contiguous()
+        dy = _rows(dy)
         want_g = bool(ctx.has_res and ctx.needs_input_grad[1])
         lo = ctx.link_out
         if lo is not None and lo.sums is not None:
@@ -309,14 +311,33 @@ class _ConvBNAct(torch.autograd.Function):
             else:
                 dx = _dgrad_joined(k, ctx.join_x, dz, weight_of(w), ctx.in_hw, conv, wt)
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
-                None)
+                None, None)
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """``t`` if its rows are uniformly strided with contiguous channels (a channel window
+    of a wider NHWC buffer, which the BN kernels read in place), else a contiguous copy."""
+    if t.is_contiguous():
+        return t
+    if t.dim() >= 2 and t.stride(-1) == 1:
+        ld, expect = t.stride(-2), t.stride(-2) * t.shape[-2]
+        ok = ld >= t.shape[-1] and ld % 8 == 0
+        for d in range(t.dim() - 3, -1, -1):
+            ok = ok and (t.shape[d] == 1 or t.stride(d) == expect)
+            expect *= t.shape[d]
+        if ok:
+            return t
+    return t.contiguous()
 
 
 def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor] = None,
                 link_in: Optional[BNLink] = None, link_out: Optional[BNLink] = None,
                 join_x: Optional[GradJoin] = None, join_res: Optional[GradJoin] = None,
-                defer: Optional[BNDefer] = None, res_defer: Optional[BNDefer] = None):
+                defer: Optional[BNDefer] = None, res_defer: Optional[BNDefer] = None,
+                out: Optional[torch.Tensor] = None):
     """relu(bn(conv(x)) [+ residual]); BN in train or eval mode per ``bn.training``.
+    ``out`` (train mode, no residual): a channel window of a wider NHWC buffer the result
+    is written into (see ``channel_buffer``).
 
     A conv bias in front of a train-mode BN (VGG11_bn) is added before the statistics, so
     forward and running stats are exact; its gradient is exactly zero in exact arithmetic
@@ -329,8 +350,10 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
                                   or bn.bias is None):
             defer = None
         raff = res_defer.aff if res_defer is not None else None
+        if out is not None and (residual is not None or defer is not None or link_out is not None):
+            out = None
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
-                                bn, relu, link_in, link_out, join_x, join_res, defer, raff)
+                                bn, relu, link_in, link_out, join_x, join_res, defer, raff, out)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,
@@ -356,12 +379,12 @@ class _ConvGroupBNAct(torch.autograd.Function):
     ``/root/reference/models.py:83-95``."""
 
     @staticmethod
-    def forward(ctx, x, W, mods, join, *params):
+    def forward(ctx, x, W, mods, join, outs, *params):
         k = K(x)
         ntot = W.shape[0]
         stats = torch.empty(2, ntot, device=x.device, dtype=torch.float32)
         z = k.conv_fwd(x, W, _empty(x), 1, 1, 0, 0, False, stats, _empty(x))
-        outs, saved, o = [], [], 0
+        res, saved, o = [], [], 0
         for m in mods:
             bn, n = m.bn, m.conv.weight.shape[0]
             pool = getattr(m, "pool_after", None)
@@ -370,17 +393,18 @@ class _ConvGroupBNAct(torch.autograd.Function):
                 st = _empty(x)
             else:
                 zin, st = z[..., o:o + n], stats[:, o:o + n]
+            dst = outs[len(res)] if outs is not None else None
             y, mean, rstd = k.bn_fwd_train(zin, st, bn.weight, bn.bias, bn.running_mean,
                                            bn.running_var, bn.momentum_value(), bn.eps,
-                                           _empty(x), True, bn.num_batches_tracked)
-            outs.append(y)
+                                           _empty(x), True, bn.num_batches_tracked, out=dst)
+            res.append(y)
             saved.append((mean, rstd, o, n, zin if pool is not None else None, pool))
             o += n
         ctx.mods, ctx.join, ctx.saved, ctx.W = mods, join, saved, W
         ctx.in_hw = (x.shape[1], x.shape[2])
         ctx.nparams = len(params)
         ctx.save_for_backward(x, z)
-        return tuple(outs)
+        return tuple(res)
 
     @staticmethod
     def backward(ctx, *dys):
@@ -390,11 +414,11 @@ class _ConvGroupBNAct(torch.autograd.Function):
         for m, (mean, rstd, o, n, zp, pool), dy in zip(ctx.mods, ctx.saved, dys):
             gamma, beta = m.bn.weight, m.bn.bias
             if pool is not None:
-                dzp, _g = k.bn_bwd(dy.contiguous(), zp, _empty(dy), mean, rstd, gamma,
+                dzp, _g = k.bn_bwd(_rows(dy), zp, _empty(dy), mean, rstd, gamma,
                                    _sink(gamma, dy), _sink(beta, dy), True, False, beta)
                 k.avgpool_bwd(dzp, z.shape[1], z.shape[2], *pool, dx_out=dz[..., o:o + n])
             else:
-                k.bn_bwd(dy.contiguous(), z[..., o:o + n], _empty(dy), mean, rstd, gamma,
+                k.bn_bwd(_rows(dy), z[..., o:o + n], _empty(dy), mean, rstd, gamma,
                          _sink(gamma, dy), _sink(beta, dy), True, False, beta,
                          dx_out=dz[..., o:o + n])
             _done(gamma, beta)
@@ -408,7 +432,7 @@ class _ConvGroupBNAct(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad_joined(k, ctx.join, dz, ctx.W, ctx.in_hw, ctx.mods[0].conv, None)
         ctx.W = None
-        return (dx, None, None, None) + (None,) * ctx.nparams
+        return (dx, None, None, None, None) + (None,) * ctx.nparams
 
 
 def conv1x1_group_ok(x, mods) -> bool:
@@ -428,16 +452,17 @@ def conv1x1_group_ok(x, mods) -> bool:
     return a.flat_view(ws, "master") is not None
 
 
-def conv1x1_group(x, mods, join: Optional[GradJoin] = None):
+def conv1x1_group(x, mods, join: Optional[GradJoin] = None, outs=None):
     """[relu(bn(conv(x))) for each BasicConv2d in mods] as one GEMM (see _ConvGroupBNAct);
-    ``join``: x's gradient is summed with its other consumers' (one contribution here)."""
+    ``join``: x's gradient is summed with its other consumers' (one contribution here);
+    ``outs``: per member, a channel window to write its output into, or None."""
     ws = [m.conv.weight for m in mods]
     a = ws[0]._mpa_arena
     W = a.flat_view(ws, "shadow" if a.shadow is not None else "master")
     ntot = sum(w.shape[0] for w in ws)
     W = W.view(ntot, 1, 1, ws[0].shape[-1])
     params = [p for m in mods for p in (m.conv.weight, m.bn.weight, m.bn.bias) if p is not None]
-    return _ConvGroupBNAct.apply(x, W, list(mods), join, *params)
+    return _ConvGroupBNAct.apply(x, W, list(mods), join, outs, *params)
 
 
 def _pool_out(n: int, k: int, s: int, p: int, ceil: bool) -> int:
@@ -516,9 +541,31 @@ def conv_bn_relu_maxpool(x, conv, bn, pool):
 
 
 # ============================================================================ conv + bias
+_UNIT = {}
+
+
+def _unit_affine(C: int, device):
+    """(mean 0, rstd 1, gamma 1, beta 0) of length C: the identity 'BN' through which a
+    plain ReLU's mask and bias-gradient reduction ride the fused BN-backward-reduction
+    dgrad (bn(y) = y, so the mask is y > 0 and sum g is the bias gradient)."""
+    key = (C, device)
+    t = _UNIT.get(key)
+    if t is None:
+        z, o = torch.zeros(C, device=device), torch.ones(C, device=device)
+        t = _UNIT[key] = (z, o, o, z)
+    return t
+
+
 class _ConvAct(torch.autograd.Function):
+    """act(conv(x) + b).  ``link_out`` (BNLink): this op's ReLU output feeds ONLY the next
+    conv, whose dgrad applies the ReLU mask (y > 0) and reduces the bias gradient in its
+    epilogue (the BN-backward-reduction flavour with an identity affine), so this op's
+    backward runs no act_bwd pass (VGG / AlexNet conv -> ReLU -> conv chains,
+    ``/root/reference/models.py:50,59``); ``link_in``: the BNLink of this op's input."""
+
     @staticmethod
-    def forward(ctx, x, w, b, conv, relu, join=None, stats=None, shift=None, out=None):
+    def forward(ctx, x, w, b, conv, relu, join=None, stats=None, shift=None, out=None,
+                link_in=None, link_out=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
         if out is not None:  # written straight into a channel window of a wider buffer
@@ -533,6 +580,14 @@ class _ConvAct(torch.autograd.Function):
         ctx.params = (w, b)
         ctx.in_hw = (x.shape[1], x.shape[2])
         ctx.join = join
+        ctx.link_in = link_in
+        ctx.link_out = link_out
+        if link_out is not None and relu and out is None:
+            C = y.shape[-1]
+            link_out.z = link_out.y = y
+            link_out.mean, link_out.rstd, link_out.gamma, link_out.beta = \
+                _unit_affine(C, y.device)
+            link_out.sums = None
         ctx.save_for_backward(x, y if relu else None)
         return y
 
@@ -543,7 +598,16 @@ class _ConvAct(torch.autograd.Function):
         conv = ctx.conv
         k = K(dy)
         dy = dy.contiguous()
-        g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
+        lo = ctx.link_out
+        if lo is not None and lo.sums is not None:
+            # the consumer's dgrad already applied the mask; its sum g is the bias gradient
+            g = dy
+            bs = _sink(b, dy)
+            if bs.numel():
+                k.add_f32_(bs, lo.sums[:bs.numel()])
+            lo.sums = None
+        else:
+            g = k.act_bwd(dy, _or_empty(y, dy), _sink(b, dy))
         _done(b)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
@@ -552,13 +616,23 @@ class _ConvAct(torch.autograd.Function):
             _done(w)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad_joined(k, ctx.join, g, weight_of(w), ctx.in_hw, conv, weight_t_of(w))
-        return dx, None, None, None, None, None, None, None, None
+            li = ctx.link_in
+            wt = weight_t_of(w)
+            if (li is not None and li.z is not None and ctx.join is None
+                    and (wt is not None or not g.is_cuda)
+                    and k.conv_bnred_ok(w.shape[0], w.shape[3])):
+                dx, li.sums = k.conv_dgrad_bnred(g, weight_of(w), ctx.in_hw[0], ctx.in_hw[1],
+                                                 sh, sw, ph, pw, wt, li.z, _or_empty(li.y, g),
+                                                 li.mean, li.rstd, gamma=li.gamma, beta=li.beta)
+            else:
+                dx = _dgrad_joined(k, ctx.join, g, weight_of(w), ctx.in_hw, conv, wt)
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_act(x, conv, relu: bool = False, join: Optional[GradJoin] = None,
              stats: Optional[torch.Tensor] = None, shift: Optional[torch.Tensor] = None,
-             out: Optional[torch.Tensor] = None):
+             out: Optional[torch.Tensor] = None, link_in: Optional[BNLink] = None,
+             link_out: Optional[BNLink] = None):
     """act(conv(x) + b); ``join``: x's gradient is summed with its other consumers' (see
     GradJoin); ``stats`` ([2, N] fp32, training): receives the output's per-channel
     [mean | var] from the GEMM epilogue (sums shifted by ``shift`` for precision); ``out``
@@ -566,7 +640,8 @@ def conv_act(x, conv, relu: bool = False, join: Optional[GradJoin] = None,
     result is that window; ``stats`` may then be a [2, N] window of a wider table)."""
     x = conv.fit_input(x)
     if torch.is_grad_enabled() and (conv.weight.requires_grad or x.requires_grad):
-        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu, join, stats, shift, out)
+        return _ConvAct.apply(x, conv.weight, conv.bias, conv, relu, join, stats, shift, out,
+                              link_in, link_out)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     return k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, relu,
@@ -576,13 +651,16 @@ def conv_act(x, conv, relu: bool = False, join: Optional[GradJoin] = None,
 # =========================================================================== standalone BN
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, bn, relu, stats=None):
+    def forward(ctx, x, gamma, beta, bn, relu, stats=None, out=None):
         k = K(x)
         y, mean, rstd = k.bn_fwd_train(x, _or_empty(stats, x), gamma, beta, bn.running_mean,
                                        bn.running_var, bn.momentum_value(), bn.eps, _empty(x),
-                                       relu, bn.num_batches_tracked)
+                                       relu, bn.num_batches_tracked, out=out)
         ctx.params = (gamma, beta)
-        ctx.save_for_backward(x, y if relu else None, mean, rstd)
+        # relu(bn(x)) with an affine BN recomputes its mask from x: y is not kept
+        zmask = relu and beta is not None and gamma is not None
+        ctx.zmask = zmask
+        ctx.save_for_backward(x, y if (relu and not zmask) else None, mean, rstd)
         return y
 
     @staticmethod
@@ -590,18 +668,21 @@ class _BNAct(torch.autograd.Function):
         x, y, mean, rstd = ctx.saved_tensors
         gamma, beta = ctx.params
         k = K(dy)
-        dy = dy.contiguous()
+        dy = _rows(dy)
         dx, _g = k.bn_bwd(dy, x, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
-                          _sink(beta, dy), bool(ctx.needs_input_grad[0]), False)
+                          _sink(beta, dy), bool(ctx.needs_input_grad[0]), False,
+                          beta if ctx.zmask else None)
         _done(gamma, beta)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def bn_act(x, bn, relu: bool = True, stats: Optional[torch.Tensor] = None):
+def bn_act(x, bn, relu: bool = True, stats: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None):
     """relu?(bn(x)); ``stats`` (train mode): x's [mean | var] [2, C] when already known
-    (a DenseNet block's per-feature statistics), saving the statistics pass."""
+    (a DenseNet block's per-feature statistics), saving the statistics pass; ``out`` (train
+    mode): a channel window of a wider buffer to write the result into."""
     if bn.training:
-        return _BNAct.apply(x, bn.weight, bn.bias, bn, relu, stats)
+        return _BNAct.apply(x, bn.weight, bn.bias, bn, relu, stats, out)
     return K(x).bn_fwd_eval(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
                             _empty(x), relu)
 
@@ -769,6 +850,64 @@ def adaptive_avg_pool2d(x, out_hw):
     if torch.is_grad_enabled() and x.requires_grad:
         return _AdaptiveAvgPool.apply(x, oh, ow)
     return K(x).adaptive_avgpool_fwd(x, oh, ow)
+
+
+# ============================================================ concat at channel offsets
+class _ChannelBuffer(torch.autograd.Function):
+    """The channel concat of ``parts`` that their producers already wrote into their
+    windows of ``buf`` (``out=`` of conv_bn_act / bn_act / conv1x1_group): forward returns
+    the buffer (a part NOT at its window is copied in), backward hands each part its
+    window of the gradient - a row-strided view, which the BN backward kernels read in
+    place.  SURVEY K13: torchvision's ``torch.cat`` of Inception branch outputs
+    (``/root/reference/models.py:83-95``) without the copy kernels."""
+
+    @staticmethod
+    def forward(ctx, buf, *parts):
+        k = K(buf)
+        o = 0
+        ctx.sizes = []
+        for t in parts:
+            n = t.shape[-1]
+            win = buf[..., o:o + n]
+            if t.data_ptr() != win.data_ptr() or t.stride() != win.stride():
+                k.chan_insert(buf, o, t.contiguous())
+            ctx.sizes.append(n)
+            o += n
+        return buf.view(buf.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        outs, o = [], 0
+        for n in ctx.sizes:
+            outs.append(dy[..., o:o + n])
+            o += n
+        return (None,) + tuple(outs)
+
+
+class ChannelBuffer:
+    """An NHWC block output [N, H, W, sum(widths)] whose branches write their results at
+    their channel offsets: ``window(i)`` is branch i's destination (pass it as ``out=``),
+    ``gather(parts)`` the concat (no copy for parts already in place)."""
+
+    def __init__(self, like: torch.Tensor, hw, widths):
+        self.widths = list(widths)
+        self.offs = [sum(self.widths[:i]) for i in range(len(self.widths))]
+        self.buf = torch.empty((like.shape[0], hw[0], hw[1], sum(self.widths)),
+                               device=like.device, dtype=like.dtype)
+
+    def window(self, i: int) -> torch.Tensor:
+        o = self.offs[i]
+        return self.buf[..., o:o + self.widths[i]]
+
+    def gather(self, parts):
+        if torch.is_grad_enabled() and any(t.requires_grad for t in parts):
+            return _ChannelBuffer.apply(self.buf, *parts)
+        k = K(self.buf)
+        for i, t in enumerate(parts):
+            w = self.window(i)
+            if t.data_ptr() != w.data_ptr():
+                k.chan_insert(self.buf, self.offs[i], t.contiguous())
+        return self.buf
 
 
 # ======================================================================== channel concat

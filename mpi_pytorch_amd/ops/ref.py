@@ -132,7 +132,7 @@ def bn_stats_affine(x, stats, gamma, beta, rmean, rvar, momentum, eps, counter=N
 
 
 def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, relu,
-                 counter=None, mask=None, channels=0, res_affine=None):
+                 counter=None, mask=None, channels=0, res_affine=None, out=None):
     # the oracle always uses exact two-pass statistics (``stats`` from a fused producer
     # epilogue is accepted for API parity but not needed); channels > 0: BN of the first
     # ``channels`` channels of a wider buffer
@@ -161,6 +161,11 @@ def bn_fwd_train(x, stats, gamma, beta, rmean, rvar, momentum, eps, residual, re
     y = y.reshape(x.shape).to(x.dtype)
     if _opt(mask) is not None:
         mask.copy_(relu_bitmask(y))
+    if _opt(out) is not None:  # a channel window of a wider buffer
+        # (through .data, like a native kernel's store: no autograd version bump of the
+        # buffer the other branches' outputs are views of)
+        out.data.copy_(y)
+        y = out
     return y, mean.contiguous(), rstd.contiguous()
 
 
@@ -577,12 +582,16 @@ def add_bf16_(a, b):
     a.add_(b)
 
 
+def add_f32_(dst, src):
+    dst.add_(src)
+
+
 def chan_slice(src, off, cs):
     return src[..., off:off + cs].clone()
 
 
 def chan_insert(dst, off, src):
-    dst[..., off:off + src.shape[-1]] = src
+    dst.data[..., off:off + src.shape[-1]] = src
 
 
 def chan_extract(g, off, cs):

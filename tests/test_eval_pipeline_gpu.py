@@ -150,3 +150,24 @@ def test_real_jpeg_ring_decode_error_raises(gpu, model, tmp_path):
         assert feed_error(ring) is not None
     finally:
         ring.stop()
+
+
+@pytest.mark.parametrize("name,hw,src", [("inception", 299, 340), ("densenet", 224, 256)])
+def test_zoo_ring_pipeline_equals_plain_eval(gpu, name, hw, src):
+    """The reference predicts with whichever MODEL_NAME was trained
+    (``/root/reference/evaluation_pipeline.py:138-144``): Inception-v3 at 299 (BASELINE
+    config 5 names it with the HIP-stream pipeline) and DenseNet-121 at 224, 2 predictor
+    lanes, PIL-exact bicubic from larger sources - equal to the plain evaluation."""
+    torch.manual_seed(0)
+    m, _opt, _step, _ = build_training(name, NC, gpu, World(device=gpu), 1e-3)
+    m.eval()
+    names, labels = _manifest(37, seed=7)
+    source = SyntheticImages((src, src))
+    ref = plain_eval(m, names, labels, 8, source, gpu, (hw, hw))
+    ring, nb = make_ring(names, labels, 8, source, NC, depth=3, threads=2)
+    try:
+        pipe = StreamPipeline(m, gpu, (hw, hw), lanes=2, assign="roundrobin")
+        counts = pipe.run_ring(ring, nb)
+    finally:
+        ring.stop()
+    assert sum(counts) == ref and sum(pipe.seen) == 37

@@ -444,3 +444,73 @@ def test_resnet_deferred_downsample_bn_equals_materialized(monkeypatch):
     assert torch.allclose(o1, o2, atol=1e-5)
     assert all(torch.allclose(u.float(), v.float(), atol=1e-5) for u, v in zip(r1, r2))
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
+def test_feature_stack_links_match_unlinked():
+    """FusedSequential's conv -> ReLU -> conv hand-offs (the consumer dgrad applies the
+    producer's ReLU mask / BN reduction, no act_bwd or reduce pass) give the same
+    gradients as the unlinked form, for plain ReLU (VGG-16 / AlexNet) and BN+ReLU
+    (VGG11_bn) producers."""
+    import mpi_pytorch_amd.models.layers as L
+    from mpi_pytorch_amd.models.layers import (Conv2d, BatchNorm2d, ReLU, MaxPool2d,
+                                               FusedSequential)
+    from mpi_pytorch_amd.parallel import ParamArena
+    torch.manual_seed(0)
+
+    def make():
+        torch.manual_seed(0)
+        seq = FusedSequential(Conv2d(3, 16, 3, 1, 1), ReLU(True), Conv2d(16, 16, 3, 1, 1),
+                              ReLU(True), MaxPool2d(2, 2), Conv2d(16, 24, 3, 1, 1, bias=False),
+                              BatchNorm2d(24), ReLU(True), Conv2d(24, 24, 3, 1, 1, bias=False),
+                              BatchNorm2d(24), ReLU(True), Conv2d(24, 8, 3, 2, 1))
+        ParamArena(seq, torch.device("cpu"))
+        seq.train()
+        return seq
+
+    x = torch.randn(2, 12, 12, 3)
+    grads = []
+    for on in (True, False):
+        old = L._LINK
+        L._LINK = on
+        try:
+            seq = make()
+            assert any(seq.links(seq.groups())) == on
+            y = seq(x.clone())
+            (y.float() ** 2).sum().backward()
+            grads.append([p.grad.clone() for p in seq.parameters()])
+        finally:
+            L._LINK = old
+    for a, b in zip(*grads):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("merged", [True, False])
+def test_inception_branches_written_in_place_equal_concat(monkeypatch, merged):
+    """Inception blocks whose branches write their outputs at their channel offsets of the
+    block output (Fn.ChannelBuffer; backward hands each branch a row-strided window of the
+    gradient) == branch tensors concatenated by copy (MPA_CAT_INTO=0), fp32 on the CPU:
+    same logits and running statistics, gradients to fp32 rounding."""
+    import mpi_pytorch_amd.models.inception as I
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("inception", 10, torch.device("cpu"), World(), 1e-3)
+    model.dropout.p = 0.0
+    for m in model.modules():
+        if hasattr(m, "heads"):
+            m.merge_1x1 = merged
+    a = model._mpa_arena
+    x = torch.randn(2, 299, 299, 8) * (torch.arange(8) < 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    for into in (True, False):
+        monkeypatch.setattr(I, "_CAT_INTO", into)
+        model.load_state_dict(sd)
+        a.zero_grad()
+        out = model(x)
+        loss_fn(out, y).backward()
+        res.append((out[0].detach(), a.grad.clone(),
+                    [v.clone() for k, v in model.state_dict().items() if "running" in k]))
+    (o1, g1, r1), (o2, g2, r2) = res
+    assert torch.allclose(o1, o2, atol=1e-5)
+    assert all(torch.allclose(u, v, atol=1e-5) for u, v in zip(r1, r2))
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
