@@ -1500,6 +1500,16 @@ int64_t maxpool_bn_ws_floats(int M, int C) {
   return (int64_t)grid_for(M, C, stem_grid(1)).x * 2 * C + 2 * C;
 }
 
+void maxpool_bn_sel_sums(const bf16_raw* dp, const bf16_raw* zsel, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, int C, int MP,
+                         float* ws, hipStream_t s) {
+  float* slab = ws + 2 * C;
+  const dim3 gr = grid_for(MP, C, stem_grid(1));
+  hipLaunchKernelGGL(maxpool_bn_bwd_sel_reduce_kernel, gr, dim3(256), 0, s, dp, zsel, mean, rstd,
+                     gamma, beta, C, MP, slab, ws);
+  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+}
+
 void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, float* dgamma,
                     float* dbeta, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh,

@@ -1160,6 +1160,20 @@ static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s
   if (tbm) tuned_store(key, tbm, tbn);
 }
 
+bool igemm_wgrad_stem_pb(WGradArgs a, const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z,
+                         const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, const float* sums, float* dgamma, float* dbeta,
+                         int P2, int Q2, hipStream_t s) {
+  if (igemm_engine() < 1 || !stem_wgrad_pb_ok(a, P2, Q2)) return false;
+  const int z_ = stem_wgrad_pb(a, dp, idx, z, mean, rstd, gamma, beta, sums, dgamma, dbeta, P2,
+                               Q2, s);
+  const int64_t n = (int64_t)a.Kout * a.Ncols;
+  const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z_, n, a.dw,
+                     a.overwrite);
+  return true;
+}
+
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   if (igemm_engine() >= 1 && conv3_halo_wgrad_ok(a)) {  // 3x3 / stride 1: halo-staged
     const int z = conv3_halo_wgrad(a, s);

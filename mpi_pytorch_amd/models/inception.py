@@ -31,8 +31,27 @@ class BasicConv2d(nn.Module):
         self.conv = Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False)
         self.bn = BatchNorm2d(out_channels, eps=0.001)
 
-    def forward(self, x, join=None, out=None):
-        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True, join_x=join, out=out)
+    def forward(self, x, join=None, out=None, link_in=None, link_out=None):
+        return Fn.conv_bn_act(x, self.conv, self.bn, relu=True, join_x=join, out=out,
+                              link_in=link_in, link_out=link_out)
+
+
+# MPA_INC_LINK=0: the BasicConv2d chains inside a branch run each BN's own reduce pass
+_LINK = os.environ.get("MPA_INC_LINK", "1") == "1"
+
+
+def _chain(mod, mods, x, out=None):
+    """A branch's BasicConv2d chain (e.g. 7x7dbl_2 -> _3 -> _4 -> _5): each BN+ReLU output
+    feeds ONLY the next conv, so that conv's dgrad performs its backward reduction
+    (Fn.BNLink: no reduce pass); the last conv writes into ``out`` (the block buffer)."""
+    link = None
+    use = _LINK and mod.training and torch.is_grad_enabled()
+    for k, m in enumerate(mods):
+        last = k == len(mods) - 1
+        nxt = Fn.BNLink() if (use and not last) else None
+        x = m(x, out=out if last else None, link_in=link, link_out=nxt)
+        link = nxt
+    return x
 
 
 def _avg3(x, join=None):
@@ -155,7 +174,7 @@ class InceptionA(nn.Module):
             b5, b3 = self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
             bp = self.branch_pool(x, j, out=cb.window(3))
         b5 = self.branch5x5_2(b5, out=cb.window(1))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(b3), out=cb.window(2))
+        b3 = _chain(self, [self.branch3x3dbl_2, self.branch3x3dbl_3], b3, cb.window(2))
         return cb.gather([b1, b5, b3, bp])
 
 
@@ -172,8 +191,8 @@ class InceptionB(nn.Module):
         cb = _out(_buffer(self, x, (_half(x.shape[1]), _half(x.shape[2])),
                           [384, 96, x.shape[-1]]))
         b3 = self.branch3x3(x, j, out=cb.window(0))
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, j)),
-                                 out=cb.window(1))
+        bd = _chain(self, [self.branch3x3dbl_2, self.branch3x3dbl_3],
+                    self.branch3x3dbl_1(x, j), cb.window(1))
         return cb.gather([b3, bd, _max3s2(x, j)])
 
 
@@ -205,10 +224,9 @@ class InceptionC(nn.Module):
             b1 = self.branch1x1(x, j, out=cb.window(0))
             b7, bd = self.branch7x7_1(x, j), self.branch7x7dbl_1(x, j)
             bp = self.branch_pool(x, j, out=cb.window(3))
-        b7 = self.branch7x7_3(self.branch7x7_2(b7), out=cb.window(1))
-        for m in (self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4):
-            bd = m(bd)
-        bd = self.branch7x7dbl_5(bd, out=cb.window(2))
+        b7 = _chain(self, [self.branch7x7_2, self.branch7x7_3], b7, cb.window(1))
+        bd = _chain(self, [self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
+                           self.branch7x7dbl_5], bd, cb.window(2))
         return cb.gather([b1, b7, bd, bp])
 
 
@@ -236,9 +254,8 @@ class InceptionD(nn.Module):
         cb = _out(_buffer(self, x, (_half(x.shape[1]), _half(x.shape[2])),
                           [320, 192, x.shape[-1]]))
         b3 = self.branch3x3_2(b3, out=cb.window(0))
-        for m in (self.branch7x7x3_2, self.branch7x7x3_3):
-            b7 = m(b7)
-        b7 = self.branch7x7x3_4(b7, out=cb.window(1))
+        b7 = _chain(self, [self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4], b7,
+                    cb.window(1))
         return cb.gather([b3, b7, _max3s2(x, j)])
 
 
@@ -335,7 +352,7 @@ class Inception3(nn.Module):
                 m.init_(lambda w, s=std: nn.init.trunc_normal_(w, 0.0, s, -2, 2))
 
     def forward(self, x):
-        x = self.Conv2d_2a_3x3(self.Conv2d_1a_3x3(x))
+        x = _chain(self, [self.Conv2d_1a_3x3, self.Conv2d_2a_3x3], x)
         if self.fuse_stem_pools:
             x = Fn.conv_bn_relu_maxpool(x, self.Conv2d_2b_3x3.conv, self.Conv2d_2b_3x3.bn,
                                         self.maxpool1)

@@ -35,6 +35,9 @@ _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
 _NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
 _NO_ZSEL = os.environ.get("MPA_NO_ZSEL", "0") == "1"  # A/B: stem backward reduce from full z
+# MPA_FUSE_STEM_BWD=0: the stem's max-pool + BN backward writes dz for a separate weight
+# gradient instead of being computed inside the stem weight-gradient kernel's staging
+_FUSE_STEM_BWD = os.environ.get("MPA_FUSE_STEM_BWD", "1") == "1"
 # A/B: residual blocks' backward reads y for the ReLU mask instead of a 1-bit-per-element mask
 _NO_YMASK = os.environ.get("MPA_NO_YMASK", "0") == "1"
 
@@ -513,10 +516,23 @@ class _ConvBNReLUPool(torch.autograd.Function):
         w, gamma, beta = ctx.params
         conv = ctx.conv
         k = K(dy)
-        dz = k.maxpool_bn_bwd(dy.contiguous(), idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
+        sh, sw, ph, pw = conv.kgeom
+        dy = dy.contiguous()
+        if (dy.is_cuda and _FUSE_STEM_BWD and zsel is not None and w.requires_grad
+                and not ctx.needs_input_grad[0] and gamma is not None and beta is not None):
+            # the image needs no gradient, so dz feeds only the weight gradient: build it
+            # inside that kernel's staging instead of writing and re-reading it
+            if k.stem_wgrad_poolbn(dy, idx, z, zsel, mean, rstd, gamma, beta,
+                                   _sink(gamma, dy), _sink(beta, dy), x, w.grad, sh, sw, ph,
+                                   pw, _fresh(w)):
+                _done(gamma, beta)
+                conv.fix_grad(w.grad)
+                _done(w)
+                _done(ctx.bias)
+                return None, None, None, None, None, None, None, None
+        dz = k.maxpool_bn_bwd(dy, idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
                               _sink(beta, dy), *ctx.cfg[:6], zsel=zsel)
         _done(gamma, beta)
-        sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
             k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
             conv.fix_grad(w.grad)

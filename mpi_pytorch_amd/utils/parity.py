@@ -79,17 +79,20 @@ def _tapped_groups(name: str, fs, rec: Dict):
     cls_run = type(fs).run_group
     mods = list(fs._modules.values())
 
-    def run_group(g, x):
+    def run_group(g, x, link_in=None, link_out=None):
+        # (the BN / ReLU backward hand-offs between groups are kept: a unit's recorded
+        # output gradient is then its consumer's masked dgrad, the same gradient after
+        # the unit's own ReLU)
         i0, i1, kind = g
         if not any(p.requires_grad for mm in mods[i0:i1] for p in mm.parameters()):
-            return cls_run(fs, g, x)
+            return cls_run(fs, g, x, link_in=link_in, link_out=link_out)
         key = "%s[%d:%d]" % (name, i0, i1)
         r = rec.setdefault(key, {"calls": 0, "group": g, "fs": name, "fs_mod": fs,
                                  "kind": kind})
         r["calls"] += 1
         bx, by = [], []
         r["x"], r["gx"] = x.detach().clone(), bx
-        out = cls_run(fs, g, _Tap.apply(x, bx))
+        out = cls_run(fs, g, _Tap.apply(x, bx), link_in=link_in, link_out=link_out)
         r["y"], r["gy"] = out.detach().clone(), by
         return _Tap.apply(out, by)
 

@@ -45,16 +45,21 @@ def test_model_parity(gpu, name, hw):
     assert abs(float(lc) - float(lg)) < 0.05 * max(1.0, abs(float(lc))), (float(lc), float(lg))
     gc = mc._mpa_arena.grad
     gg = mg._mpa_arena.grad.cpu()
-    cos = float(torch.nn.functional.cosine_similarity(gc, gg, dim=0))
     ratio = float(gg.norm() / gc.norm())
-    # Deep BN nets at init have gradients that are chaotic w.r.t. rounding: the native
-    # path run twice on identical inputs (fp32 atomic summation order of the BN slab
-    # reductions) agrees only to cos 0.35-0.48 for inception-v3 at batch 4
-    # (tools/diag_engines.py) and ~0.9 for densenet - tools/diag_grads.py.  Those get a
-    # loose direction bound; loss and gradient magnitude must match for all.
-    bound = {"inception": 0.03, "densenet": 0.6, "resnet34": 0.75}.get(name, 0.9)
-    assert cos > bound, (cos, bound)
     assert 0.8 < ratio < 1.25, ratio
+    # The whole-model gradient DIRECTION of a deep BN net at init is chaotic w.r.t.
+    # rounding - the fp32 CPU path alone moves to cos 0.39 (Inception) / 0.90 (DenseNet)
+    # when only the input image is rounded to bf16
+    # (test_models_cpu.py::test_whole_model_gradients_are_shattered_in_fp32) - so no tight
+    # whole-model bound exists; per-unit parity (test_layer_parity_gpu.py, cos >= 0.99 for
+    # every block / layer) is the real check.  What IS well conditioned end to end: the
+    # classifier head's gradient (features x softmax error, no deep backward behind it).
+    from mpi_pytorch_amd.models import head_parameters
+    hc = torch.cat([p.grad.reshape(-1) for p in head_parameters(mc) if p.grad is not None])
+    hg = torch.cat([p.grad.reshape(-1).cpu() for p in head_parameters(mg)
+                    if p.grad is not None])
+    hcos = float(torch.nn.functional.cosine_similarity(hc, hg, dim=0))
+    assert hcos > 0.99, hcos
 
 
 def test_resnet18_training_decreases_loss(gpu):
