@@ -171,10 +171,18 @@ void conv_fwd_into(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int6
 struct BnRed {
   Tensor z, y, mean, rstd, sums, gamma, beta;
 };
+// src2: a second conv reading the same input with the same stride (its dy2 on dy's pixel
+// grid with dy's channel count, weight w2 [K][R2][S2][C], transposed wt2 [C][R2*S2][K], pad
+// ph2 / pw2): its taps join the stride phases they belong to (IGemmArgs::A2)
+struct DgradSrc2 {
+  Tensor dy2, w2, wt2;
+  int ph2, pw2;
+};
 
 static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw,
                               int64_t ph, int64_t pw, c10::optional<Tensor> wt_opt,
-                              BnRed* bnred, c10::optional<Tensor> accum = c10::nullopt) {
+                              BnRed* bnred, c10::optional<Tensor> accum = c10::nullopt,
+                              const DgradSrc2* src2 = nullptr) {
   CHECK_ACT(dy);
   CHECK_ACT(w);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -230,6 +238,20 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
           ++T;
         }
       }
+      if (src2) {
+        const int R2 = src2->w2.size(1), S2 = src2->w2.size(2);
+        for (int r = 0; r < R2; ++r) {
+          if (((a_ + src2->ph2 - r) % sh) != 0) continue;
+          for (int s = 0; s < S2; ++s) {
+            if (((b_ + src2->pw2 - s) % sw) != 0) continue;
+            TORCH_CHECK(T < mpa::MAXT, "conv_dgrad: too many taps");
+            a.taps.dh[T] = (a_ + src2->ph2 - r) / sh;
+            a.taps.dw[T] = (b_ + src2->pw2 - s) / sw;
+            a.taps.bt[T] = (short)((r * S2 + s) | mpa::TAP_SRC2);
+            ++T;
+          }
+        }
+      }
       TORCH_CHECK(nph < mpa::MAXPH, "conv_dgrad: too many stride phases");
       a.ph[nph++] = mpa::PhaseDesc{N * Hp * Wp, Hp, Wp, (T - t0) * K, t0, T - t0, a_, b_, 0};
     }
@@ -277,11 +299,17 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
     // untouched)
     bool empty = false;
     for (int i = 0; i < nph; ++i) empty |= a.ph[i].T == 0;
-    if (empty && !acc) dx.zero_();
     int k = 0;
     for (int i = 0; i < nph; ++i)
       if (a.ph[i].T > 0) a.ph[k++] = a.ph[i];
     a.nphase = k;
+    if (src2) {
+      a.A2 = bp(src2->dy2);
+      a.B2 = bp(src2->wt2);
+      a.ldb2 = src2->w2.size(1) * src2->w2.size(2) * K;
+      if (!mpa::igemm_dgrad_src2_ok(a, vw, bkc)) return Tensor();  // caller runs them apart
+    }
+    if (empty && !acc) dx.zero_();
     mpa::igemm_rows_dgrad_phases(a, vw, cur_stream(), bkc);
   }
   return dx;
@@ -290,6 +318,32 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t sw, int64_t ph,
                   int64_t pw, c10::optional<Tensor> wt_opt, c10::optional<Tensor> accum) {
   return conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt_opt, nullptr, accum);
+}
+
+// dx of two convs that read the same input with the same stride (a residual stage's 3x3/s2
+// conv1 and its 1x1/s2 shortcut) in ONE merged stride-phase launch: the shortcut's taps
+// are extra K of the phases they hit, so dx is written once, with no accumulate pass.
+// Returns None when that launch is not available (the caller runs the two dgrads apart).
+c10::optional<Tensor> conv_dgrad_pair(Tensor dy, Tensor w, Tensor wt, int64_t H, int64_t W,
+                                      int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                                      Tensor dy2, Tensor w2, Tensor wt2, int64_t ph2,
+                                      int64_t pw2, c10::optional<Tensor> accum) {
+  CHECK_ACT(dy2);
+  CHECK_ACT(w2);
+  CHECK_ACT(wt2);
+  TORCH_CHECK(dy2.sizes() == dy.sizes(), "conv_dgrad_pair: dy2 must have dy's shape");
+  TORCH_CHECK(w2.dim() == 4 && w2.size(0) == w.size(0) && w2.size(3) == w.size(3) &&
+                  wt2.numel() == w2.numel(),
+              "conv_dgrad_pair: w2 [K][R2][S2][C] with w's K and C, and its transpose");
+  if (sh == 1 && sw == 1) return c10::nullopt;
+  if (!(wt.defined() && wt.numel() == w.numel())) return c10::nullopt;
+  // the two convs' output grids must coincide: P = (H + 2 ph - R) / sh + 1 for both
+  const int P2 = (H + 2 * ph2 - w2.size(1)) / sh + 1, Q2 = (W + 2 * pw2 - w2.size(2)) / sw + 1;
+  if (P2 != dy.size(1) || Q2 != dy.size(2)) return c10::nullopt;
+  DgradSrc2 s2{dy2, w2, wt2, (int)ph2, (int)pw2};
+  Tensor dx = conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt, nullptr, accum, &s2);
+  if (!dx.defined()) return c10::nullopt;
+  return dx;
 }
 
 // fused-reduction dgrad available: LDS-DMA engine, 16-B granular dy (K) and dx (C), and
@@ -1457,6 +1511,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred_gacc", &conv_dgrad_bnred_gacc);
+  m.def("conv_dgrad_pair", &conv_dgrad_pair, py::arg("dy"), py::arg("w"), py::arg("wt"),
+        py::arg("H"), py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dy2"), py::arg("w2"), py::arg("wt2"), py::arg("ph2"), py::arg("pw2"),
+        py::arg("accum") = py::none());
   m.def("bn_defer_step", &bn_defer_step, py::arg("sums"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("s0"), py::arg("k12"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("G"), py::arg("x"), py::arg("out") = py::none());

@@ -98,7 +98,16 @@ struct IGemmArgs {
   int beta;               // 1: accumulate, C = acc + C (bf16 read-add-write, one rounding):
                           // a second gradient contribution lands in the first one's buffer
   FastDiv fd_hw, fd_ow;   // oH * oW, oW (igemm_set_fastdiv, right before a launch)
+  // second GEMM source (merged stride-phase dgrad, uniform-tap LDS-DMA kernel only): tap
+  // entries with bt & TAP_SRC2 read A2 (same pixel grid and channel count as A) and B2
+  // (K-contiguous, row stride ldb2) - the dgrad of a second conv that reads the same input
+  // with the same stride (ResNet's 1x1/s2 shortcut) lands as extra K of the phase its
+  // taps belong to, so dx is written once
+  const bf16_raw* A2;
+  const bf16_raw* B2;
+  int ldb2;
 };
+constexpr short TAP_SRC2 = 0x2000;
 
 // fill the FastDiv fields of a rows launch (and of its stride phases)
 inline void igemm_set_fastdiv(IGemmArgs& a) {
@@ -133,6 +142,8 @@ void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc = 
 // all stride phases of a strided-conv dgrad (a.nphase, a.ph[], shared a.taps) in one launch
 // on the LDS-DMA engine when eligible, else one igemm_rows_dgrad per phase
 void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc = false);
+// whether a merged-phase dgrad with a second source (a.A2) runs on the kernel that reads it
+bool igemm_dgrad_src2_ok(const IGemmArgs& a, int vw, bool bkc);
 // dgrad with the fused BN-backward reduction (a.ep_* set): sums[2][N] receives
 // (sum g, sum g * xhat); slab holds igemm_bnred_slab_floats(a) floats
 int64_t igemm_bnred_slab_floats(int M, int N, int nphase);

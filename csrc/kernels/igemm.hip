@@ -983,10 +983,18 @@ void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* s
 // All stride phases in ONE launch on the LDS-DMA engine: a stride-2 conv's dgrad is 4
 // GEMMs of a quarter of the pixels each; launched separately each fills a fraction of the
 // 256 CUs (ResNet-18 layer4 at batch 256: 196 tiles per phase), merged they fill it.
+bool igemm_dgrad_src2_ok(const IGemmArgs& a, int vw, bool bkc) {
+  return use_dma(vw) && a.nphase > 0 && a.nphase <= MAXPH && igemm_rows_uni_src2_ok(a, bkc);
+}
+
 void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
   a.stats = nullptr;
   a.bias = nullptr;
   if (a.nphase <= 0) return;
+  if (a.A2 && !igemm_dgrad_src2_ok(a, vw, bkc)) {
+    fprintf(stderr, "igemm_rows_dgrad_phases: second source on an ineligible launch\n");
+    abort();
+  }
   if (use_dma(vw) && a.nphase <= MAXPH) {
     int tbm = 0, tbn = 0;
     if (g_tune && !deterministic() && !(g_force_bm && g_force_bn) && !stream_capturing(s)) {
@@ -1015,6 +1023,10 @@ void igemm_rows_dgrad_phases(IGemmArgs a, int vw, hipStream_t s, bool bkc) {
     int BM, BN;
     plan_phases(a, BM, BN, tbm, tbn);
     if (a.tiles_total > 0 && igemm_rows_dma(a, BM, BN, bkc, 1, s)) return;
+  }
+  if (a.A2) {  // (unreachable: every planned tile has a kernel)
+    fprintf(stderr, "igemm_rows_dgrad_phases: no merged launch for a second source\n");
+    abort();
   }
   for (int i = 0; i < a.nphase; ++i) {  // one launch per phase
     const PhaseDesc& d = a.ph[i];

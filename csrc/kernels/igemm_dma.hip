@@ -313,7 +313,9 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     tap_hw[t] = (dh << 16) | (dw & 0xffff);
     tap_b[t] = bt;
     tap_ab[t] = (dh * p.aW + dw) * aC * 2;
-    tap_ab[MAXT + t] = BKC ? (bt & 0xfff) * aC * 2 : (bt & 0xfff) * p.ldb * 2;
+    // (bit 31: a second-source tap, see IGemmArgs::A2; its B rows have stride ldb2)
+    tap_ab[MAXT + t] = (PH && (bt & TAP_SRC2)) ? (int)(0x80000000u | (uint32_t)((bt & 0xfff) * aC * 2))
+                       : BKC ? (bt & 0xfff) * aC * 2 : (bt & 0xfff) * p.ldb * 2;
   }
   __syncthreads();
 
@@ -324,6 +326,9 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   // issue-bound, MFMA busy ~25 %.)
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, 0x7fffffffu);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, 0x7fffffffu);
+  // second source (PH, BKC only): its own descriptors; null -> the first (never selected)
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(PH && p.A2 ? p.A2 : p.A, 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t rb2 = make_rsrc(PH && p.B2 ? p.B2 : p.B, 0x7fffffffu);
   const uint32_t s32 = lds_base(smem);
   const int kch = kc_lane_chunk(lane);
   // K elements per tap-table entry: aC, or 32 for super-taps (4 kernel columns x 8 ch)
@@ -366,21 +371,30 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     const int hwv = __builtin_amdgcn_readfirstlane(tap_hw[t_s]);
     const int dh = hwv >> 16, dw = (short)(hwv & 0xffff);
     const int toff = __builtin_amdgcn_readfirstlane(tap_ab[t_s]) + c_s * 2;
+    const int braw = __builtin_amdgcn_readfirstlane(tap_ab[MAXT + t_s]);
+    const bool x2 = PH && BKC && braw < 0;  // wave-uniform: a second-source tap
+    const __amdgpu_buffer_rsrc_t rA = x2 ? ra2 : ra;
+    const __amdgpu_buffer_rsrc_t rB = x2 ? rb2 : rb;
 #pragma unroll
     for (int i = 0; i < IAW; ++i) {
       const bool ok = ((unsigned)(a_bh[i] + dh) < (unsigned)p.aH) &
                       ((unsigned)(a_bw[i] + dw) < (unsigned)p.aW);
-      buf_lds16_at(ra, st + (wave * IAW + i) * 1024, ok ? a_off[i] + toff : 0x80000000u);
+      buf_lds16_at(rA, st + (wave * IAW + i) * 1024, ok ? a_off[i] + toff : 0x80000000u);
     }
     const uint32_t bst = st + A_BYTES;
-    const int boff = __builtin_amdgcn_readfirstlane(tap_ab[MAXT + t_s]) +
-                     (BKC ? c_s * 2 : c_s * p.RS * p.ldb * 2);
+    const int boff = (braw & 0x7fffffff) + (BKC ? c_s * 2 : c_s * p.RS * p.ldb * 2);
     // super-tap: chunks past the kernel's last column read zeros (ns valid columns)
     const bool bok = !p.stap || kch < (__builtin_amdgcn_readfirstlane(tap_b[t_s]) >> 12);
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
       const int jb = wave + NW * i;
-      if (jb < IB) buf_lds16_so(rb, bst + jb * 1024, bok ? b_off[i] : 0x80000000u, boff);
+      uint32_t bo = b_off[i];
+      if constexpr (PH && BKC) {
+        // second-source rows (stride ldb2): recomputed on its few K-steps, not held
+        if (x2) bo = (uint32_t)((min(n0 + 16 * min(jb, IB - 1) + (lane >> 2), p.N - 1) * p.ldb2 +
+                                 kch * 8) * 2);
+      }
+      if (jb < IB) buf_lds16_so(rB, bst + jb * 1024, bok ? bo : 0x80000000u, boff);
     }
     c_s += BK;
     if (c_s >= kpt) { c_s = 0; ++t_s; }
@@ -745,7 +759,14 @@ static bool rows_uni_fits(const IGemmArgs& a, bool bkc) {
   const int64_t nimg = hw > 0 ? (m + hw - 1) / hw : 0;
   const int64_t abytes = nimg * a.aH * a.aW * a.aC * 2;
   const int64_t bbytes = (bkc ? (int64_t)a.N : (int64_t)a.aC * a.RS) * a.ldb * 2;
-  return abytes < (1ll << 31) && bbytes < (1ll << 31);
+  const int64_t b2bytes = (int64_t)a.N * a.ldb2 * 2;
+  return abytes < (1ll << 31) && bbytes < (1ll << 31) && b2bytes < (1ll << 31);
+}
+
+// a second GEMM source is read only by the uniform-tap kernel's phase form with K-contiguous
+// B (launch_rows_dma_v picks that kernel under exactly these conditions)
+bool igemm_rows_uni_src2_ok(const IGemmArgs& a, bool bkc) {
+  return bkc && a.nphase > 0 && a.aC % BK == 0 && !a.stap && g_dma_uni && rows_uni_fits(a, bkc);
 }
 
 template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>

@@ -148,13 +148,37 @@ class GradJoin:
 
 
 class _Deferred:
-    """A parked dgrad: ``run(accum)`` launches it (fresh when accum is None)."""
+    """A parked dgrad: ``run(accum)`` launches it (fresh when accum is None); ``args`` =
+    (dz, w, wt, conv) lets the next contribution merge it into its own launch."""
 
-    __slots__ = ("run", "full")
+    __slots__ = ("run", "full", "args")
 
-    def __init__(self, run, full: bool):
+    def __init__(self, run, full: bool, args=None):
         self.run = run
         self.full = full
+        self.args = args
+
+
+# MPA_DGRAD_PAIR=0: a residual stage's conv1 (3x3/s2) and 1x1/s2 shortcut dgrads run as two
+# launches (the second accumulating into the first's dx) instead of one merged launch
+_PAIR = os.environ.get("MPA_DGRAD_PAIR", "1") == "1"
+
+
+def _dgrad_pair(k, a, b, in_hw):
+    """Both parked/current dgrads of one activation in one launch (``conv_dgrad_pair``):
+    a = (dz, w, wt, conv) of a conv whose taps cover every pixel, b = the other."""
+    dz, w, wt, conv = a
+    dz2, w2, wt2, conv2 = b
+    sh, sw, ph, pw = conv.kgeom
+    sh2, sw2, ph2, pw2 = conv2.kgeom
+    if (sh, sw) != (sh2, sw2) or (dz.is_cuda and (wt is None or wt2 is None)):
+        return None
+    if tuple(dz.shape) != tuple(dz2.shape) or w.shape[3] != w2.shape[3]:
+        return None
+    if not hasattr(k, "conv_dgrad_pair"):
+        return None
+    return k.conv_dgrad_pair(dz, w, wt, in_hw[0], in_hw[1], sh, sw, ph, pw, dz2, w2, wt2,
+                             ph2, pw2)
 
 
 def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
@@ -196,13 +220,20 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
     last = join.arrive()
     prev = join.take()
     full = _dgrad_full(conv, in_hw)
+    args = (dz, w, wt, conv)
     if prev is None:
         if last:
             return run(None)
-        join.partial = _Deferred(run, full)
+        join.partial = _Deferred(run, full, args)
         return None
     if isinstance(prev, _Deferred):
-        if full or not prev.full:
+        acc = None
+        if _PAIR and prev.args is not None and full != prev.full:
+            acc = (_dgrad_pair(k, args, prev.args, in_hw) if full
+                   else _dgrad_pair(k, prev.args, args, in_hw))
+        if acc is not None:
+            pass
+        elif full or not prev.full:
             acc = prev.run(run(None))
         else:
             acc = run(prev.run(None))

@@ -77,6 +77,31 @@ def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None, accum=None):
     return _nhwc(gi).to(dy.dtype)
 
 
+def conv_dgrad_pair(dy, w, wt, H, W, sh, sw, ph, pw, dy2, w2, wt2, ph2, pw2, accum=None):
+    """dx of two convs reading the same input with the same stride (3x3/s2 conv1 + its
+    1x1/s2 shortcut), summed in fp32 and rounded once; None if the grids differ."""
+    if sh == 1 and sw == 1:
+        return None
+    P2 = (H + 2 * ph2 - w2.shape[1]) // sh + 1
+    Q2 = (W + 2 * pw2 - w2.shape[2]) // sw + 1
+    if (P2, Q2) != tuple(dy.shape[1:3]):
+        return None
+
+    def gi(d, ww, p_h, p_w):
+        N = d.shape[0]
+        C = ww.shape[3]
+        return torch.ops.aten.convolution_backward(
+            _nchw(_f(d)).contiguous(), torch.empty(N, C, H, W, device=d.device),
+            _f(ww).permute(0, 3, 1, 2).contiguous(), None, [sh, sw], [p_h, p_w], [1, 1],
+            False, [0, 0], 1, [True, False, False])[0]
+
+    tot = _nhwc(gi(dy, w, ph, pw) + gi(dy2, w2, ph2, pw2))
+    if accum is not None:
+        accum.copy_((_f(accum) + tot).to(accum.dtype))
+        return accum
+    return tot.to(dy.dtype)
+
+
 def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False):
     K, R, S, C = dw.shape
     gw = torch.ops.aten.convolution_backward(

@@ -162,6 +162,36 @@ def test_conv_dgrad_transposed_weight(gpu, engine, case):
         assert torch.equal(dx, dxt), rel(dxt, dx)
 
 
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128), (4, 28, 28, 128, 256), (3, 15, 13, 64, 64),
+                                  (2, 56, 56, 64, 128)])
+def test_conv_dgrad_pair(gpu, case):
+    """A residual stage's 3x3/s2 conv1 dgrad and its 1x1/s2 shortcut dgrad in ONE merged
+    stride-phase launch (the shortcut's tap is extra K of the (even, even) phase) == the
+    two oracle dgrads summed; and close to the two-launch form (dgrad + accumulate)."""
+    torch.manual_seed(12)
+    N, H, W, Cc, K = case
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy = bf(N, P, Q, K, dev=gpu)
+    dy2 = bf(N, P, Q, K, dev=gpu)
+    w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * K))
+    w2 = bf(K, 1, 1, Cc, dev=gpu, scale=1.0 / math.sqrt(K))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+    wt2 = w2.permute(3, 1, 2, 0).reshape(Cc, 1, K).contiguous()
+    dx = C().conv_dgrad_pair(dy, w, wt, H, W, 2, 2, 1, 1, dy2, w2, wt2, 0, 0)
+    assert dx is not None, "merged launch unavailable on the LDS-DMA engine"
+    exp = ref.conv_dgrad_pair(dy, w, wt, H, W, 2, 2, 1, 1, dy2, w2, wt2, 0, 0)
+    two = C().conv_dgrad(dy2, w2, H, W, 2, 2, 0, 0, wt2,
+                         C().conv_dgrad(dy, w, H, W, 2, 2, 1, 1, wt))
+    torch.cuda.synchronize()
+    assert dx.shape == (N, H, W, Cc)
+    assert rel(dx, exp) < 1e-2
+    assert rel(two, exp) < 2e-2
+    # the odd phases carry no shortcut tap: bitwise the single dgrad there
+    one = C().conv_dgrad(dy, w, H, W, 2, 2, 1, 1, wt)
+    torch.cuda.synchronize()
+    assert torch.equal(dx[:, 1::2], one[:, 1::2]) and torch.equal(dx[:, :, 1::2], one[:, :, 1::2])
+
+
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 3, 1, 1), (2, 14, 14, 64, 128, 3, 3, 2, 1),
                                   (4, 28, 28, 128, 128, 3, 3, 1, 1), (3, 9, 11, 96, 48, 3, 3, 1, 1)])
 def test_conv_dgrad_fused_bn_reduction(gpu, case):

@@ -446,6 +446,37 @@ def test_resnet_deferred_downsample_bn_equals_materialized(monkeypatch):
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
 
 
+def test_resnet_dgrad_pair_equals_two_dgrads(monkeypatch):
+    """Each residual stage's conv1 (3x3/s2) and 1x1/s2 shortcut dgrads merged into one
+    launch (Fn._dgrad_pair -> conv_dgrad_pair; 3 per ResNet-18 step) == the two separate
+    dgrads summed by GradJoin (fp32, CPU)."""
+    from mpi_pytorch_amd.ops import functional as Fn
+    from mpi_pytorch_amd.ops import ref
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("resnet18", 10, torch.device("cpu"), World(), 1e-3)
+    a = model._mpa_arena
+    x = torch.randn(2, 64, 64, 3)
+    y = torch.randint(0, 10, (2,))
+    calls = []
+    real = ref.conv_dgrad_pair
+
+    def counting(*args, **kw):
+        r = real(*args, **kw)
+        calls.append(r is not None)
+        return r
+
+    monkeypatch.setattr(ref, "conv_dgrad_pair", counting)
+    grads = []
+    for pair in (True, False):
+        monkeypatch.setattr(Fn, "_PAIR", pair)
+        a.zero_grad()
+        loss_fn(model(x), y).backward()
+        grads.append(a.grad.clone())
+    assert calls == [True, True, True]
+    g1, g2 = grads
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
 def test_feature_stack_links_match_unlinked():
     """FusedSequential's conv -> ReLU -> conv hand-offs (the consumer dgrad applies the
     producer's ReLU mask / BN reduction, no act_bwd or reduce pass) give the same
