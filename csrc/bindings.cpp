@@ -813,6 +813,37 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, Tensor y, Tensor mean, Tensor rs
   return {dx, gout};
 }
 
+// backward of relu(bn(x) + bn2(x2)) with both BNs in train mode (ResNet bn2 + the deferred
+// downsample BN): returns [dx, dx2]; both BNs' dgamma/dbeta receive their sums
+std::vector<Tensor> bn_bwd_pair(Tensor dy, Tensor x, Tensor ymask, Tensor mean, Tensor rstd,
+                                Tensor gamma, Tensor dgamma, Tensor dbeta, Tensor x2, Tensor mean2,
+                                Tensor rstd2, Tensor gamma2, Tensor dgamma2, Tensor dbeta2) {
+  CHECK_CUDA(dy);
+  CHECK_BF16(dy);
+  dy = dy.contiguous();
+  CHECK_ACT(x);
+  CHECK_ACT(x2);
+  const int C = dy.size(-1);
+  const int M = dy.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_bwd_pair: channels must be a multiple of 8");
+  TORCH_CHECK(x.sizes() == dy.sizes() && x2.sizes() == dy.sizes(), "bn_bwd_pair: shape mismatch");
+  for (const Tensor* t : {&mean, &rstd, &gamma, &mean2, &rstd2, &gamma2}) {
+    CHECK_CUDA(*t);
+    CHECK_F32(*t);
+    TORCH_CHECK(t->numel() == C, "bn_bwd_pair: per-channel vector size");
+  }
+  const uint8_t* ym = ymask_ptr(ymask, dy);
+  TORCH_CHECK(ym, "bn_bwd_pair: needs the forward's ReLU bit mask");
+  const c10::OptionalDeviceGuard g(device_of(x));
+  Tensor dx = torch::empty(dy.sizes(), dy.options());
+  Tensor dx2 = torch::empty(dy.sizes(), dy.options());
+  Tensor ws = torch::empty({mpa::bn_pair_ws_floats(M, C)}, x.options().dtype(torch::kFloat32));
+  mpa::bn_bwd_pair(bp(dy), bp(x), bp(x2), ym, fopt(mean), fopt(rstd), fopt(gamma), fopt(mean2),
+                   fopt(rstd2), fopt(gamma2), fopt_mut(dgamma), fopt_mut(dbeta), fopt_mut(dgamma2),
+                   fopt_mut(dbeta2), M, C, bpm(dx), bpm(dx2), ws.data_ptr<float>(), cur_stream());
+  return {dx, dx2};
+}
+
 Tensor relu_fwd(Tensor x) {
   CHECK_ACT(x);
   TORCH_CHECK(x.numel() % 8 == 0, "relu: numel must be a multiple of 8");
@@ -1540,6 +1571,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("eps"), py::arg("res"), py::arg("relu"),
         py::arg("channels") = 0);
+  m.def("bn_bwd_pair", &bn_bwd_pair);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none(),

@@ -267,6 +267,15 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
             int lddx = 0,            // dx row stride (0: C) - a channel window of a wider buffer
             bool gacc_bf16 = false,  // gacc holds bf16 (cast the pointer) instead of fp32
             int lddy = 0);           // dy row stride (0: C) - a channel window of a wider buffer
+// backward of relu(bn(x) + bn2(x2)), both train-mode BNs (bn2: a deferred downsample BN
+// applied on read): dx and dx2 from one reduce and one apply pass, mask = the forward's bit
+// mask; ws holds bn_pair_ws_floats(M, C) floats
+int64_t bn_pair_ws_floats(int M, int C);
+void bn_bwd_pair(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* x2, const uint8_t* ymask,
+                 const float* mean, const float* rstd, const float* gamma, const float* mean2,
+                 const float* rstd2, const float* gamma2, float* dgamma, float* dbeta,
+                 float* dgamma2, float* dbeta2, int M, int C, bf16_raw* dx, bf16_raw* dx2,
+                 float* ws, hipStream_t s);
 void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const float* mean,
                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, int M,
                   int C, bf16_raw* dx, bf16_raw* g, const float* sums, hipStream_t s,

@@ -581,6 +581,143 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       });
 }
 
+// ---------------------------------------------------------------- residual BN pair
+// Backward of y = relu(bn(x) + bn2(x2)) when BOTH BNs are train-mode (ResNet's bn2 and the
+// deferred downsample BN it applies on read, Fn.BNDefer): both see the same upstream
+// g = dy * mask, so one reduce pass yields [sum g | sum g*xhat | sum g*xhat2] and one apply
+// pass writes dx AND dx2 - g is never materialised, and the second BN's own reduce and
+// apply passes (read g, x2; read g, x2, write dx2) disappear.  Mask: the forward's bit mask.
+template <int UNR>
+__global__ __launch_bounds__(256) void bn_bwd_pair_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+    const uint8_t* __restrict__ ym, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ mean2, const float* __restrict__ rstd2, int M, int C,
+    float* __restrict__ slab, float* __restrict__ sums) {
+  __shared__ float red[256 * 8];
+  const ColMap cm = colmap(C / 8);
+  float sg[8], sgx[8], sgx2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sgx[j] = 0.f; sgx2[j] = 0.f; }
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    if (blockIdx.x == 0 && cm.r0 == 0) {  // slab_reduce accumulates into these afterwards
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sums[c0 + j] = 0.f;
+        sums[C + c0 + j] = 0.f;
+        sums[2 * C + c0 + j] = 0.f;
+      }
+    }
+    float mu[8], rs[8], mu2[8], rs2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j];
+      mu2[j] = mean2[c0 + j]; rs2[j] = rstd2[c0 + j];
+    }
+    sweep_rows<UNR>(cm, M, [&](int r, int st, int n) {
+      uint4 dv[UNR], xr[UNR], x2r[UNR];
+      uint32_t mb[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (u < n) {
+          const size_t off = (size_t)(r + u * st) * C + c0;
+          dv[u] = *(const uint4*)(dy + off);
+          xr[u] = *(const uint4*)(x + off);
+          x2r[u] = *(const uint4*)(x2 + off);
+          mb[u] = ym[off / 8];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (u >= n) break;
+        float g[8], xv[8], x2v[8];
+        unpack8(dv[u], g);
+        unpack8(xr[u], xv);
+        unpack8(x2r[u], x2v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gj = (mb[u] >> j) & 1u ? g[j] : 0.f;
+          sg[j] += gj;
+          sgx[j] += gj * (xv[j] - mu[j]) * rs[j];
+          sgx2[j] += gj * (x2v[j] - mu2[j]) * rs2[j];
+        }
+      }
+    });
+  }
+  block_reduce8(sg, cm, red);
+  block_reduce8(sgx, cm, red);
+  block_reduce8(sgx2, cm, red);
+  if (cm.active && cm.r0 == 0) {
+    float* row = slab + (size_t)blockIdx.x * 3 * C + cm.cc * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      row[j] = sg[j];
+      row[C + j] = sgx[j];
+      row[2 * C + j] = sgx2[j];
+    }
+  }
+}
+
+// dx = a*g + b + c*x, dx2 = a2*g + b2 + c2*x2; block 0 folds the sums into both BNs'
+// dgamma / dbeta
+template <int UNR>
+__global__ __launch_bounds__(256) void bn_bwd_pair_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+    const uint8_t* __restrict__ ym, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ mean2,
+    const float* __restrict__ rstd2, const float* __restrict__ gamma2,
+    const float* __restrict__ ws, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dgamma2, float* __restrict__ dbeta2, int M, int C,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dx2) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float a[8], b[8], cc[8], a2[8], b2[8], cc2[8];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sg = ws[c0 + j], sgx = ws[C + c0 + j], sgx2 = ws[2 * C + c0 + j];
+    const float rs = rstd[c0 + j], sc = gamma[c0 + j] * rs;
+    a[j] = sc;
+    cc[j] = -sc * rs * sgx * invM;
+    b[j] = -sc * sg * invM - cc[j] * mean[c0 + j];
+    const float rs2_ = rstd2[c0 + j], sc2 = gamma2[c0 + j] * rs2_;
+    a2[j] = sc2;
+    cc2[j] = -sc2 * rs2_ * sgx2 * invM;
+    b2[j] = -sc2 * sg * invM - cc2[j] * mean2[c0 + j];
+    if (blockIdx.x == 0 && cm.r0 == 0) {
+      if (dgamma) dgamma[c0 + j] += sgx;
+      if (dbeta) dbeta[c0 + j] += sg;
+      if (dgamma2) dgamma2[c0 + j] += sgx2;
+      if (dbeta2) dbeta2[c0 + j] += sg;
+    }
+  }
+  sweep_rows_pl<UNR, 4>(
+      cm, M,
+      [&](int r, uint4 (&v)[4]) {
+        const size_t off = (size_t)r * C + c0;
+        v[0] = *(const uint4*)(dy + off);
+        v[3].x = ym[off / 8];
+        v[1] = *(const uint4*)(x + off);
+        v[2] = *(const uint4*)(x2 + off);
+      },
+      [&](int r, uint4 (&v)[4]) {
+        const size_t off = (size_t)r * C + c0;
+        float g[8], xv[8], x2v[8];
+        unpack8(v[0], g);
+        unpack8(v[1], xv);
+        unpack8(v[2], x2v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          g[j] = (v[3].x >> j) & 1u ? g[j] : 0.f;
+          xv[j] = a[j] * g[j] + b[j] + cc[j] * xv[j];
+          x2v[j] = a2[j] * g[j] + b2[j] + cc2[j] * x2v[j];
+        }
+        *(uint4*)(dx + off) = pack8(xv);
+        *(uint4*)(dx2 + off) = pack8(x2v);
+      });
+}
+
 // g = dy * (y > 0) ; dbias += colsum(g)
 template <int UNR>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16_t* __restrict__ dy,
@@ -1449,6 +1586,23 @@ void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, cons
   BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
               (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr, C,
               (float*)nullptr, 0, C, lddy);
+}
+
+int64_t bn_pair_ws_floats(int M, int C) { return (int64_t)3 * C * (1 + grid_for(M, C).x); }
+
+void bn_bwd_pair(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* x2, const uint8_t* ymask,
+                 const float* mean, const float* rstd, const float* gamma, const float* mean2,
+                 const float* rstd2, const float* gamma2, float* dgamma, float* dbeta,
+                 float* dgamma2, float* dbeta2, int M, int C, bf16_raw* dx, bf16_raw* dx2,
+                 float* ws, hipStream_t s) {
+  // ws layout: [3C] final sums | [gx][3C] per-block partials
+  const dim3 gr = grid_for(M, C);
+  float* slab = ws + 3 * C;
+  BN_LAUNCH(bn_bwd_pair_reduce_kernel, gr, s, dy, x, x2, ymask, mean, rstd, mean2, rstd2, M, C,
+            slab, ws);
+  slab_reduce(slab, gr.x, 3 * C, ws, false, s);
+  BN_LAUNCH(bn_bwd_pair_apply_kernel, gr, s, dy, x, x2, ymask, mean, rstd, gamma, mean2, rstd2,
+            gamma2, ws, dgamma, dbeta, dgamma2, dbeta2, M, C, dx, dx2);
 }
 
 void act_bwd(const bf16_raw* dy, const bf16_raw* y, float* dbias, int M, int C, bf16_raw* g,

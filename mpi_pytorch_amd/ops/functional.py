@@ -107,10 +107,19 @@ class BNDefer:
     reading it.  The tensor then stands for the BN output in autograd: the consumer hands
     back d/d(BN output), which the producer's backward turns into its own BN backward."""
 
-    __slots__ = ("aff",)
+    __slots__ = ("aff", "z", "mean", "rstd", "gamma", "beta", "done")
 
     def __init__(self):
         self.aff = None
+        # the producer's BN inputs, for the consumer's fused backward (bn_bwd_pair): the
+        # consumer then hands back d/dz directly and sets `done`
+        self.z = self.mean = self.rstd = self.gamma = self.beta = None
+        self.done = False
+
+
+# MPA_BN_PAIR=0: the consumer of a deferred BN (ResNet bn2) writes g = dy * mask and the
+# downsample op runs its own BN backward (reduce + apply) on it
+_BN_PAIR = os.environ.get("MPA_BN_PAIR", "1") == "1"
 
 
 class GradJoin:
@@ -248,7 +257,7 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, w, b, gamma, beta, conv, bn, relu, link_in=None, link_out=None,
-                join_x=None, join_res=None, defer=None, res_affine=None, out=None):
+                join_x=None, join_res=None, defer=None, res_defer=None, out=None):
         k = K(x)
         sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
@@ -265,13 +274,16 @@ class _ConvBNAct(torch.autograd.Function):
             mean, rstd, defer.aff = k.bn_stats_affine(z, stats, gamma, beta, bn.running_mean,
                                                       bn.running_var, bn.momentum_value(),
                                                       bn.eps, bn.num_batches_tracked)
+            defer.z, defer.mean, defer.rstd, defer.gamma, defer.beta = z, mean, rstd, gamma, beta
+            defer.done = False
             y = z
         else:
             y, mean, rstd = k.bn_fwd_train(z, stats, gamma, beta, bn.running_mean,
                                            bn.running_var, bn.momentum_value(), bn.eps,
                                            _or_empty(residual, x), relu,
                                            bn.num_batches_tracked, mask=ymask,
-                                           res_affine=res_affine, out=out)
+                                           res_affine=(res_defer.aff if res_defer is not None
+                                                       else None), out=out)
         ctx.conv = conv
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -285,6 +297,8 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.link_out = link_out
         ctx.join_x = join_x
         ctx.join_res = join_res
+        ctx.defer = defer
+        ctx.res_defer = res_defer if (ymask is not None and relu and _BN_PAIR) else None
         if link_out is not None:
             link_out.z, link_out.mean, link_out.rstd = z, mean, rstd
             # ReLU without a residual: the consumer's halo dgrad recomputes the mask from z
@@ -305,7 +319,23 @@ class _ConvBNAct(torch.autograd.Function):
         dy = _rows(dy)
         want_g = bool(ctx.has_res and ctx.needs_input_grad[1])
         lo = ctx.link_out
-        if lo is not None and lo.sums is not None:
+        rd = ctx.res_defer
+        dres_pair = None
+        if ctx.defer is not None and ctx.defer.done:
+            # the consumer's bn_bwd_pair already ran this BN's backward: dy IS d/dz, and the
+            # affine gradients are in place
+            dz = dy
+            ctx.defer.done = False
+        elif (rd is not None and rd.z is not None and ctx.needs_input_grad[1]
+                and ctx.join_res is None and hasattr(k, "bn_bwd_pair")):
+            g2, b2 = rd.gamma, rd.beta
+            dz, dres_pair = k.bn_bwd_pair(dy, z, ymask, mean, rstd, gamma, _sink(gamma, dy),
+                                          _sink(beta, dy), rd.z, rd.mean, rd.rstd, g2,
+                                          _sink(g2, dy), _sink(b2, dy))
+            _done(g2, b2)
+            rd.done = True
+            rd.z = None
+        elif lo is not None and lo.sums is not None:
             # the consumer's dgrad already masked dy and reduced (sum g, sum g*xhat)
             dz, g = k.bn_bwd_apply(dy, z, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
                                    _sink(beta, dy), lo.sums, True, want_g)
@@ -317,15 +347,19 @@ class _ConvBNAct(torch.autograd.Function):
         else:
             dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
                              _sink(beta, dy), True, want_g, ymask=ymask)
-        _done(gamma, beta)
+        if ctx.defer is None or dz is not dy:
+            _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
             k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
             conv.fix_grad(w.grad)
             _done(w)
         _done(ctx.bias)
-        dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
-        dres = _join_grad(ctx.join_res, dres)
+        if dres_pair is not None:
+            dres = dres_pair  # d/dz of the deferred BN's producer (see BNDefer.done)
+        else:
+            dres = g if (ctx.has_res and ctx.needs_input_grad[1]) else None
+            dres = _join_grad(ctx.join_res, dres)
         dx = None
         if ctx.needs_input_grad[0]:
             li = ctx.link_in
@@ -383,11 +417,11 @@ def conv_bn_act(x, conv, bn, relu: bool = True, residual: Optional[torch.Tensor]
         if defer is not None and (relu or residual is not None or bn.weight is None
                                   or bn.bias is None):
             defer = None
-        raff = res_defer.aff if res_defer is not None else None
         if out is not None and (residual is not None or defer is not None or link_out is not None):
             out = None
         return _ConvBNAct.apply(x, residual, conv.weight, conv.bias, bn.weight, bn.bias, conv,
-                                bn, relu, link_in, link_out, join_x, join_res, defer, raff, out)
+                                bn, relu, link_in, link_out, join_x, join_res, defer, res_defer,
+                                out)
     k = K(x)
     sh, sw, ph, pw = conv.kgeom
     z = k.conv_fwd(x, weight_of(conv.weight), _or_empty(conv.bias, x), sh, sw, ph, pw, False,

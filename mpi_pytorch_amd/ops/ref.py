@@ -251,6 +251,28 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, dgamma, dbeta, want_dx, want_g=True, zma
     return dx, g.reshape(dy.shape).to(dy.dtype)
 
 
+def bn_bwd_pair(dy, x, ymask, mean, rstd, gamma, dgamma, dbeta, x2, mean2, rstd2, gamma2,
+                dgamma2, dbeta2):
+    """Backward of relu(bn(x) + bn2(x2)), both BNs train-mode: [dx, dx2] from the shared
+    g = dy * mask (kept in fp32, as the fused kernel does)."""
+    C = dy.shape[-1]
+    g = _f(dy).reshape(-1, C) * bitmask_unpack(ymask, (dy.numel() // C, C))
+    M = g.shape[0]
+    sg = g.sum(0)
+    out = []
+    for xx, mu, rs, ga, dga, dbe in ((x, mean, rstd, gamma, dgamma, dbeta),
+                                     (x2, mean2, rstd2, gamma2, dgamma2, dbeta2)):
+        xhat = (_f(xx).reshape(-1, C) - mu) * rs
+        sgx = (g * xhat).sum(0)
+        if _opt(dga) is not None:
+            dga.add_(sgx)
+        if _opt(dbe) is not None:
+            dbe.add_(sg)
+        d = (ga * rs) * (g - sg / M - xhat * (sgx / M))
+        out.append(d.reshape(dy.shape).to(dy.dtype))
+    return out
+
+
 def bn_bwd_apply(dy, x, y, mean, rstd, gamma, dgamma, dbeta, sums, want_dx, want_g=True):
     """bn_bwd's apply pass with precomputed sums = [sum g | sum g*xhat]."""
     C = x.shape[-1]

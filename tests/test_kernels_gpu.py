@@ -742,6 +742,51 @@ def test_bn_relu_bitmask(gpu, M, Cc):
     assert torch.equal(dg, dg2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,Cc", [(4096, 64), (100352, 128), (1003, 24)])
+def test_bn_bwd_pair_residual_deferred_bn(gpu, M, Cc):
+    """relu(bn(x) + bn2(x2)) backward with both BNs in train mode (ResNet bn2 + the deferred
+    downsample BN): bn_bwd_pair's dx / dx2 / affine gradients == the oracle, and == the
+    two-stage form (bn_bwd writing g, then bn_bwd of the second BN on g) to bf16 rounding."""
+    torch.manual_seed(16)
+    x = (bf(M, Cc, dev=gpu, scale=2.0) + 0.3).to(torch.bfloat16)
+    x2 = (bf(M, Cc, dev=gpu, scale=1.5) - 0.2).to(torch.bfloat16)
+    e = torch.empty(0, device=gpu)
+    g, b = torch.rand(Cc, device=gpu) + 0.5, torch.randn(Cc, device=gpu)
+    g2, b2 = torch.rand(Cc, device=gpu) + 0.5, torch.randn(Cc, device=gpu)
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    st2 = C().bn_stats(x2, e)
+    mean2, rstd2, aff2 = C().bn_stats_affine(x2.reshape(M, Cc), st2, g2, b2, rm.clone(), rv.clone(),
+                                             0.1, 1e-5, e)
+    mask = torch.empty(M * Cc // 8, dtype=torch.uint8, device=gpu)
+    y, mean, rstd = C().bn_fwd_train(x, e, g, b, rm, rv, 0.1, 1e-5, x2, True, e, mask,
+                                     res_affine=aff2)
+    dy = bf(M, Cc, dev=gpu)
+    C().set_deterministic(1)  # fixed-order slab combine: the bitwise check below
+    try:
+        _bn_pair_checks(dy, x, x2, mask, mean, rstd, g, mean2, rstd2, g2, Cc, gpu)
+    finally:
+        C().set_deterministic(0)
+
+
+def _bn_pair_checks(dy, x, x2, mask, mean, rstd, g, mean2, rstd2, g2, Cc, gpu):
+    e = torch.empty(0, device=gpu)
+    sk = [torch.zeros(Cc, device=gpu) for _ in range(4)]
+    dx, dx2 = C().bn_bwd_pair(dy, x, mask, mean, rstd, g, sk[0], sk[1], x2, mean2, rstd2, g2,
+                              sk[2], sk[3])
+    rk = [torch.zeros(Cc, device=gpu) for _ in range(4)]
+    rx, rx2 = ref.bn_bwd_pair(dy, x, mask, mean, rstd, g, rk[0], rk[1], x2, mean2, rstd2, g2,
+                              rk[2], rk[3])
+    tk = [torch.zeros(Cc, device=gpu) for _ in range(4)]
+    tx, tg = C().bn_bwd(dy, x, e, mean, rstd, g, tk[0], tk[1], True, True, None, mask)
+    tx2, _ = C().bn_bwd(tg, x2, e, mean2, rstd2, g2, tk[2], tk[3], True, False)
+    torch.cuda.synchronize()
+    assert rel(dx, rx) < 1e-2 and rel(dx2, rx2) < 1e-2
+    for u, v in zip(sk, rk):
+        assert rel(u, v) < 1e-3
+    assert torch.equal(dx, tx)  # same sums, same apply arithmetic
+    assert rel(dx2, tx2) < 1e-2  # (the two-stage form rounds g to bf16 first)
+
+
 @pytest.mark.parametrize("M,Cc,Ctot", [(4096, 64, 96), (3001, 136, 256), (50000, 32, 32)])
 def test_bn_channel_prefix_and_accumulate(gpu, M, Cc, Ctot):
     """DenseNet block buffer: BN (train / eval forward, z-mask backward) of the first Cc
