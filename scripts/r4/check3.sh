@@ -4,11 +4,11 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
 R=$GRAFT_REPO_ROOT
-T="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 900 $T tests/test_kernels_gpu.py -k "halo or bnred or stem_wgrad_fused or bn or dropout or dgrad" > $O/c3_t1.log 2>&1
-rc=$?; tail -2 $O/c3_t1.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $O/c3_t1.log | head -20; exit $rc; }
+rc=$?; tail -2 $O/c3_t1.log; [ $rc -eq 0 ] || grep -E "^E |FAILED|Error" $O/c3_t1.log | head -20; [ $rc -le 1 ] || exit $rc
 timeout -k 10 900 $T tests/test_models_gpu.py tests/test_grouped_gpu.py tests/test_eval_pipeline_gpu.py tests/test_determinism_gpu.py > $O/c3_t2.log 2>&1
-rc=$?; tail -2 $O/c3_t2.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $O/c3_t2.log | head -20; exit $rc; }
+rc=$?; tail -2 $O/c3_t2.log; [ $rc -eq 0 ] || grep -E "^E |FAILED|Error" $O/c3_t2.log | head -20; [ $rc -le 1 ] || exit $rc
 b() { local name=$1; shift; timeout -k 10 300 env "$@" > $O/c3_$name.json 2> $O/c3_$name.err || { echo "bench $name failed"; tail -4 $O/c3_$name.err; exit 1; }; python -c "import json; d=json.load(open('$O/c3_$name.json')); print('$name', d['value'], d['ms_per_step'])"; }
 b head python bench.py --steps 20 --warmup 5
 b nostemfuse MPA_FUSE_STEM_BWD=0 python bench.py --steps 20 --warmup 5 --small-batch 0

@@ -54,12 +54,17 @@ def test_model_parity(gpu, name, hw):
     # whole-model bound exists; per-unit parity (test_layer_parity_gpu.py, cos >= 0.99 for
     # every block / layer) is the real check.  What IS well conditioned end to end: the
     # classifier head's gradient (features x softmax error, no deep backward behind it).
+    # (The final classifier weight - the head's largest tensor; Inception's auxiliary head
+    # has BN'd convs of its own and gets the looser bound with the rest of the head.)
     from mpi_pytorch_amd.models import head_parameters
-    hc = torch.cat([p.grad.reshape(-1) for p in head_parameters(mc) if p.grad is not None])
-    hg = torch.cat([p.grad.reshape(-1).cpu() for p in head_parameters(mg)
-                    if p.grad is not None])
-    hcos = float(torch.nn.functional.cosine_similarity(hc, hg, dim=0))
-    assert hcos > 0.99, hcos
+    pc = [p.grad for p in head_parameters(mc) if p.grad is not None]
+    pg = [p.grad.cpu() for p in head_parameters(mg) if p.grad is not None]
+    cos = torch.nn.functional.cosine_similarity
+    big = max(range(len(pc)), key=lambda i: pc[i].numel())
+    fcos = float(cos(pc[big].reshape(-1), pg[big].reshape(-1), dim=0))
+    hcos = float(cos(torch.cat([t.reshape(-1) for t in pc]),
+                     torch.cat([t.reshape(-1) for t in pg]), dim=0))
+    assert fcos > 0.99 and hcos > 0.95, (fcos, hcos)
 
 
 def test_resnet18_training_decreases_loss(gpu):
