@@ -541,13 +541,13 @@ bool stem_wgrad_poolbn(Tensor dp, Tensor idx, Tensor z, Tensor zsel, Tensor mean
   a.Ncols = a.R * a.S * C;
   a.overwrite = overwrite ? 1 : 0;
   const int P2 = dp.size(1), Q2 = dp.size(2);
+  Tensor slab;  // (the eligibility check includes the partials slab)
+  a.slab = alloc_ws(slab, z, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   if (!mpa::stem_wgrad_pb_ok(a, P2, Q2)) return false;
   Tensor ws = torch::empty({mpa::maxpool_bn_ws_floats(N * P2 * Q2, K)},
                            z.options().dtype(torch::kFloat32));
   mpa::maxpool_bn_sel_sums(bp(dp), bp(zsel), fopt(mean), fopt(rstd), fopt(gamma), fopt(beta), K,
                            N * P2 * Q2, ws.data_ptr<float>(), cur_stream());
-  Tensor slab;
-  a.slab = alloc_ws(slab, z, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
   return mpa::igemm_wgrad_stem_pb(a, bp(dp), idx.data_ptr<uint8_t>(), bp(z), fopt(mean),
                                   fopt(rstd), fopt(gamma), fopt(beta), ws.data_ptr<float>(),
                                   fopt_mut(dgamma), fopt_mut(dbeta), P2, Q2, cur_stream());

@@ -1361,6 +1361,10 @@ def test_stem_wgrad_fused_pool_bn_backward(gpu, hw, N, monkeypatch):
     model = build_training("resnet18", 10, gpu, World(device=gpu), 1e-3)[0]
     x = (torch.randn(N, hw, hw, 8) * (torch.arange(8) < 3)).to(gpu, torch.bfloat16)
     a = model._mpa_arena
+    ext = C()
+    real = ext.stem_wgrad_poolbn
+    ran = []
+    monkeypatch.setattr(ext, "stem_wgrad_poolbn", lambda *t: ran.append(real(*t)) or ran[-1])
     grads = []
     for fused in (True, False):
         monkeypatch.setattr(F_, "_FUSE_STEM_BWD", fused)
@@ -1371,6 +1375,7 @@ def test_stem_wgrad_fused_pool_bn_backward(gpu, hw, N, monkeypatch):
         torch.cuda.synchronize()
         grads.append([p.grad.clone() for p in (model.conv1.weight, model.bn1.weight,
                                                 model.bn1.bias)])
+    assert ran == [True], ran  # the fused kernel ran (no silent fallback)
     for u, v in zip(*grads):
         assert float(v.abs().max()) > 0
         assert rel(u, v) < 1e-2, rel(u, v)
