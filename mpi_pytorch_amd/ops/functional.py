@@ -35,9 +35,12 @@ _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
 _NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
 _NO_ZSEL = os.environ.get("MPA_NO_ZSEL", "0") == "1"  # A/B: stem backward reduce from full z
-# MPA_FUSE_STEM_BWD=0: the stem's max-pool + BN backward writes dz for a separate weight
-# gradient instead of being computed inside the stem weight-gradient kernel's staging
-_FUSE_STEM_BWD = os.environ.get("MPA_FUSE_STEM_BWD", "1") == "1"
+# MPA_FUSE_STEM_BWD=1: the stem's max-pool + BN backward computed inside the stem
+# weight-gradient kernel's staging (dz never written).  Off by default: measured ~1 ms
+# SLOWER per ResNet-18 b1024 step than the separate cell backward + wgrad (48.5-48.7k vs
+# 49.6k img/s, profiles/ab_r4.txt) - the fused kernel runs at one wave per SIMD (256 VGPRs
+# + 147 AGPRs) and its dz build serialises with the staging.
+_FUSE_STEM_BWD = os.environ.get("MPA_FUSE_STEM_BWD", "0") == "1"
 # A/B: residual blocks' backward reads y for the ReLU mask instead of a 1-bit-per-element mask
 _NO_YMASK = os.environ.get("MPA_NO_YMASK", "0") == "1"
 
