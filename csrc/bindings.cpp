@@ -1525,6 +1525,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_tuned_table", &mpa::igemm_tuned_table, "autotuned GEMM tiles so far");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");
+  m.def("igemm_set_halo_strip", &mpa::igemm_set_halo_strip,
+        "strip-tiled halo conv: 0 off, 1 images too wide for linear tiles, 2 also layer1");
   m.def("igemm_halo_enabled", &mpa::igemm_halo_enabled);
   m.def("igemm_set_stem", &mpa::igemm_set_stem, "direct row-staged 7x7 pixel-pair stem on/off");
   m.def("preprocess_set_copy", &mpa::preprocess_set_copy,

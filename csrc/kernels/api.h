@@ -166,6 +166,7 @@ bool conv3_halo_ok(const IGemmArgs& a);
 int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
+void igemm_set_halo_strip(int mode);  // MPA_HALO_STRIP (0 off, 1 wide images, 2 + layer1 3-stage)
 // halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z
 // halo-staged pixel-pair stem weight gradient (conv_stem.hip): partials into a.slab
 // ([Z][64][224], <= stem_wgrad_ws_floats()); returns Z

@@ -576,6 +576,319 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
 }
 
 // ======================================================================================
+//  Strip-tiled 3x3 / stride-1 convolution (same engine, 2-D tiles)
+//
+//  conv3_halo_kernel's tiles are 256 consecutive pixels of the flattened (image, row, col)
+//  sequence; its halo image must hold every input row those pixels touch plus one above and
+//  below, so an image wider than ~60 pixels (VGG's 224^2 / 112^2 layers, Inception's 147^2 /
+//  73^2) does not fit a 36 KiB stage and runs on the implicit GEMM, which gathers every input
+//  pixel nine times.  Here a tile is TR rows x TW columns of ONE image (TW = W, or W split
+//  into equal strips of <= 128 columns; TR*TW <= 256 MFMA rows, the rest masked), and the
+//  stage holds (TR + 2) slot rows of pitch P = TW + 2 (left / right halo columns, rounded up
+//  to 8): every tap is still one uniform offset dh*P + dw, the A fragment addresses are
+//  tile-independent (computed once per block), and only (TR+2)*P pixels are staged:
+//  ResNet layer1 (W 56): 4 x 56 tiles, 384 pixels per item instead of 576.
+//
+//  NS = 3 (resident weights, <= 6 halo DMAs per producer wave): two items in flight while a
+//  third is multiplied.  The layer1 halo kernel stages 37 KB per 2.9 us item per CU
+//  (~13 GB/s/CU): one item in flight per CU is HBM latency-bound, not bandwidth-bound
+//  (tools/dma_probe.hip).
+//  Producer waves only (8-wave blocks), 64-wide column tiles (N % 64 == 0).
+// ======================================================================================
+struct StripPlan {
+  int tr, tw, p;            // tile rows / columns, LDS pitch (pixels)
+  int hiw;                  // halo DMA instructions per producer wave per item (<= 9)
+  int tiles_c, tiles_img;   // column strips per row band, tiles per image
+  int tiles_total, cc;
+  uint32_t mag_tw, mag_p, mag_tc, mag_timg;  // floor(2^32 / d) + 1
+  int btoff[9];
+  uint32_t a_bytes, b_bytes;
+};
+
+// s_waitcnt vmcnt(n) for the run-time per-item DMA counts of the strip producers
+__device__ __forceinline__ void strip_wait(int n) {
+  switch (n) {
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <bool WRES, int EPI, int NS>
+__global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripPlan h) {
+  constexpr int NJ = 4;
+  __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
+  const int HBY = h.hiw * 4096;  // halo stage bytes (4 producer waves x hiw KiB)
+  char* const hal = smem;
+  char* const wst = smem + NS * HBY;
+  char* const red = smem + 2 * HB_HBYTES + 2 * HB_WBYTES;
+  float* const cst = (float*)(red + HB_RED);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = wave_all & (HB_NW - 1);
+  const int H = p.aH, W = p.aW, HW = H * W, P = h.p, aC = p.aC;
+  const int TR = h.tr, TW = h.tw;
+  const int jq = lane >> 4, l15 = lane & 15;
+
+  const int T = h.tiles_total;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, G8 = gridDim.x >> 3;
+  const int tbeg = (int)((int64_t)xcd * T / 8), tend = (int)((int64_t)(xcd + 1) * T / 8);
+  const int ntiles = tbeg + loc < tend ? (tend - tbeg - loc + G8 - 1) / G8 : 0;
+  const int CC = h.cc;
+  const int nitems = ntiles * CC;
+  const int nt = (tbeg + loc) % p.tiles_n;
+  const int n0 = nt * HB_BN;
+  // tile tk of this block -> (image, first row, first column)
+  auto origin = [&](int tk, int& img, int& r0, int& c0) {
+    const uint32_t mt = (uint32_t)((tbeg + loc + tk * G8) / p.tiles_n);
+    img = (int)udiv(mt, h.mag_timg);
+    const uint32_t rem = mt - (uint32_t)img * h.tiles_img;
+    const uint32_t tr = udiv(rem, h.mag_tc);
+    r0 = (int)tr * TR;
+    c0 = (int)(rem - tr * h.tiles_c) * TW;
+  };
+
+  if (wave_all >= HB_NW) {
+    // ---- producers: halo lanes (slot row, column, logical chunk) are tile-independent
+    const int hiw = h.hiw;
+    uint32_t hsc[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const uint32_t hp = 16 * (wave * hiw + j) + (lane >> 2);
+      const uint32_t s = udiv(hp, h.mag_p);
+      const uint32_t col = hp - s * P;
+      const uint32_t lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
+      hsc[j] = s | (col << 10) | (lc << 20);
+    }
+    uint32_t wv[HB_WIW];
+#pragma unroll
+    for (int j = 0; j < HB_WIW; ++j) {
+      const int q = wave * HB_WIW + j;
+      const int r = 16 * q + (lane >> 2);
+      const int n = r & 63;
+      const int lc = (lane & 3) ^ (((r >> 2) & 1) << 1);
+      wv[j] = (n0 + n < p.N) ? (uint32_t)(n0 + n) * p.ldb * 2 + h.btoff[q >> 2] + lc * 16
+                             : 0x80000000u;
+    }
+    uint32_t hv[9];
+    auto prep_tile = [&](int tk) {
+      int img, r0, c0;
+      origin(tk, img, r0, c0);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int s = hsc[j] & 1023, col = (hsc[j] >> 10) & 1023;
+        const int ih = r0 - 1 + s, iw = c0 - 1 + col;
+        const bool ok = s < TR + 2 && col < TW + 2 && (unsigned)ih < (unsigned)H &&
+                        (unsigned)iw < (unsigned)W;
+        hv[j] = ok ? ((((uint32_t)img * H + ih) * W + iw) * aC) * 2 + (hsc[j] >> 20) * 16
+                   : 0x80000000u;
+      }
+    };
+    auto issue = [&](int cc, int stage) {
+      const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        if (j < hiw) buf_lds16(ra, hal + stage * HBY + (wave * hiw + j) * 1024, hv[j]);
+      if constexpr (!WRES) {
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+#pragma unroll
+        for (int j = 0; j < HB_WIW; ++j)
+          buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j) * 1024, wv[j]);
+      }
+    };
+    const int dpi = hiw + (WRES ? 0 : HB_WIW);  // DMAs per item per producer wave
+    if (nitems > 0) {
+      if constexpr (WRES) {
+        for (int cc = 0; cc < CC; ++cc) {
+          const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
+          char* wdst = wst + cc * HB_WBYTES + wave * HB_WIW * 1024;
+#pragma unroll
+          for (int j = 0; j < HB_WIW; ++j) buf_lds16(rb, wdst + j * 1024, wv[j]);
+        }
+      }
+    }
+    int ki = 0;  // next item to issue (issue order == item order)
+    auto issue_next = [&]() {
+      const int tk = ki / CC, cc = ki - tk * CC;
+      if (cc == 0) prep_tile(tk);
+      issue(cc, ki % NS);
+      ++ki;
+    };
+    while (ki < NS - 1 && ki < nitems) issue_next();
+    for (int k = 0; k < nitems; ++k) {
+      strip_wait((ki - k - 1) * dpi);  // item k landed; younger items stay in flight
+      __builtin_amdgcn_s_barrier();    // publishes stage k % NS, frees stage (k - 1) % NS
+      if (ki < nitems) issue_next();
+    }
+    if constexpr (EPI & (EP_STATS | EP_BNRED)) __syncthreads();  // halo_stats_flush's
+    return;
+  }
+
+  // ---- MFMA waves
+  if (tid < 16 * NJ) {
+    const float* bsrc = (EPI & EP_BNRED) ? p.ep_mean : p.bias;
+    const float* ssrc = (EPI & EP_BNRED) ? p.ep_rstd : p.stats_shift;
+    const float b = bsrc ? bsrc[n0 + tid] : 0.f, sv = ssrc ? ssrc[n0 + tid] : 0.f;
+    cst[tid] = b;
+    cst[HB_BN + tid] = sv;
+    if constexpr (EPI & EP_BNRED) {
+      const float sc = p.ep_gamma[n0 + tid] * sv;
+      cst[2 * HB_BN + tid] = sc;
+      cst[3 * HB_BN + tid] = __builtin_fmaf(-b, sc, p.ep_beta[n0 + tid]);
+    }
+  }
+  constexpr bool TRED = (EPI & EP_BNRED) != 0;
+  if constexpr (TRED) ((float2*)red)[tid] = make_float2(0.f, 0.f);
+  float ss[4][4], sq[4][4];
+#pragma unroll
+  for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { ss[jn][r] = 0.f; sq[jn][r] = 0.f; }
+
+  const int boff = l15 * 64 + ((jq ^ ((l15 >> 1) & 2)) << 4);
+  // A row addresses (tile-independent): local pixel li -> slot (lr + 1), column (lc + 1),
+  // column tap dw = d - 1; rows past the tile read its last pixel (their outputs are masked)
+  int xbw[4][3], lrc[4];
+  const int tpx = TR * TW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int li = min(wave * 64 + i * 16 + l15, tpx - 1);
+    const int lr = (int)udiv((uint32_t)li, h.mag_tw), lc = li - lr * TW;
+    lrc[i] = (wave * 64 + i * 16 + l15 < tpx) ? (lr << 16) | lc : -1;
+    const int hp = (lr + 1) * P + lc + 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int x = ((hp + d - 1) << 6) + (jq << 4);
+      xbw[i][d] = x ^ ((x >> 3) & 32);
+    }
+  }
+  EpiIn ein;
+  f32x4 acc[4][4];
+  int mrow[4];  // output pixel of each row fragment's lane in the current tile (-1: masked)
+  auto set_rows = [&](int tk) {
+    int img, r0, c0;
+    origin(tk, img, r0, c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = lrc[i] >> 16, lc = lrc[i] & 0xffff;
+      mrow[i] = (lrc[i] >= 0 && r0 + lr < H && c0 + lc < W)
+                    ? (img * H + r0 + lr) * W + c0 + lc : -1;
+    }
+  };
+  auto preload = [&]() {
+    if constexpr (EPI & (EP_BETA | EP_BNRED)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t orow = (uint32_t)max(mrow[i], 0) * p.ldc + n0 + jq * 4;
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) {
+          if constexpr (EPI & EP_BNRED) ein.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
+          else ein.a[i][jn] = *(const uint2*)((const bf16_t*)p.C + orow + jn * 16);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn) ein.a[i][jn] = make_uint2(0u, 0u);
+    }
+  };
+  auto epi_tile = [&]() {
+    if constexpr (TRED) {
+      float* rd = (float*)red;
+#pragma unroll
+      for (int jn = 0; jn < NJ; ++jn) {
+        asm volatile("" ::: "memory");
+        const int c = jn * 16 + jq * 4;
+        const f32x4 colb = *LDS_PTR(const f32x4, cst + c);
+        const f32x4 cols = *LDS_PTR(const f32x4, cst + HB_BN + c);
+        const f32x4 mc = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
+        const f32x4 mh = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+        float ts[4][4], tq[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { ts[jn][r] = 0.f; tq[jn][r] = 0.f; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t orow = (uint32_t)max(mrow[i], 0) * p.ldc + n0 + jq * 4;
+          epi_frag<EPI, false>(p, acc[i][jn], ein.a[i][jn], mrow[i] >= 0, jn, orow, colb, cols,
+                               mc, mh, ts[jn], tq[jn]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ts[jn][r] = row16_sum(ts[jn][r]);
+          tq[jn][r] = row16_sum(tq[jn][r]);
+        }
+        if (l15 == 0) {
+          f32x4* q = (f32x4*)(rd + (wave * 64 + jn * 16 + jq * 4) * 2);
+          f32x4 q0 = q[0], q1 = q[1];
+          q0[0] += ts[jn][0]; q0[1] += tq[jn][0]; q0[2] += ts[jn][1]; q0[3] += tq[jn][1];
+          q1[0] += ts[jn][2]; q1[1] += tq[jn][2]; q1[2] += ts[jn][3]; q1[3] += tq[jn][3];
+          q[0] = q0;
+          q[1] = q1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) {
+          const int c = jn * 16 + jq * 4;
+          const f32x4 colb = *(const f32x4*)(cst + c);
+          const f32x4 cols = *(const f32x4*)(cst + HB_BN + c);
+          const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+          const uint32_t orow = (uint32_t)max(mrow[i], 0) * p.ldc + n0 + jq * 4;
+          epi_frag<EPI, false>(p, acc[i][jn], ein.a[i][jn], mrow[i] >= 0, jn, orow, colb, cols,
+                               z4, z4, ss[jn], sq[jn]);
+        }
+    }
+  };
+  // one 32-channel chunk, all 9 taps (as conv3_halo_kernel's mma_chunk)
+  auto mma_chunk = [&](int st, int cc, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
+    const int hbase = st * HBY;
+    const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
+    bf16x8 a2[2][4], b2[2][4];
+    auto ld = [&](int t, int b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * P * 64 + xbw[i][t % 3]);
+#pragma unroll
+      for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn)
+          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
+                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+    }
+  };
+  for (int tk = 0; tk < ntiles; ++tk) {
+    set_rows(tk);
+    for (int cc = 0; cc < CC; ++cc) {
+      const int k = tk * CC + cc;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      if (cc == max(CC - 2, 0)) preload();
+      if (cc == 0) mma_chunk(k % NS, 0, std::true_type{});
+      else mma_chunk(k % NS, cc, std::false_type{});
+    }
+    epi_tile();
+  }
+  if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush<TRED>(p, ss, sq, red, n0, wave, tid);
+}
+
+// ======================================================================================
 //  Halo-staged 3x3 / stride-1 weight gradient:
 //    dW[k][t = 3r+s][c] += sum_pix dy[pix][k] * x[pix + (r-1, s-1)][c]
 //  The implicit-GEMM wgrad gathers an im2col column panel per (tap, channel) tile, i.e.
@@ -858,7 +1171,9 @@ static int halo_epi(const IGemmArgs& a) {
   }
 }
 
-bool conv3_halo_ok(const IGemmArgs& a) {
+// eligibility of the halo engine (either tiling); `linear`: the 256-pixel linear tiles fit
+static bool halo_ok_impl(const IGemmArgs& a, bool& linear) {
+  linear = false;
   if (!g_halo || a.nphase > 0 || a.stap || a.T != 9 || a.Uh != 1 || a.Uw != 1) return false;
   if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.M <= 0) return false;
   // 64-wide column tiles, or one 32-wide tile (DenseNet's growth-rate convs) in the
@@ -879,15 +1194,17 @@ bool conv3_halo_ok(const IGemmArgs& a) {
   }
   if (seen != 511) return false;
   const int64_t HW = (int64_t)a.aH * a.aW;
-  if (a.M % HW != 0 || HW + HB_BM >= 65536 || a.aW + 2 > 255) return false;
+  if (a.M % HW != 0) return false;
   if ((int64_t)a.M * a.aC * 2 >= (1ll << 31)) return false;
   if ((int64_t)a.N * a.ldb * 2 >= (1ll << 31)) return false;
+  if (HW + HB_BM >= 65536 || a.aW + 2 > 255) return true;  // (strip tiles only)
   // halo slots of any 256-pixel tile: rows touched + 2 halo rows + image separators
   const int64_t rows = (HB_BM - 1 + a.aW - 1) / a.aW + 1;
   const int64_t seps = (HB_BM - 1) / HW + 1;
   // (+1: with P == W + 1 the last slot's right border is the next pixel)
   const int P = halo_pitch(a.aW);
-  return (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
+  linear = (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
+  return true;
 }
 
 // MPA_HALO_WRES=0: no resident-weight variant (A/B of the 64-channel layers)
@@ -895,6 +1212,101 @@ static const bool g_halo_wres = [] {
   const char* e = getenv("MPA_HALO_WRES");
   return !(e && atoi(e) == 0);
 }();
+
+// ------------------------------------------------------------------ strip tiles (host)
+// MPA_HALO_STRIP: 0 off; 1 (default) images too wide for the linear tiles; 2 also the
+// resident-weight layers whose strips leave room for a third stage (ResNet layer1)
+static int g_strip = [] {
+  const char* e = getenv("MPA_HALO_STRIP");
+  return e ? atoi(e) : 1;
+}();
+void igemm_set_halo_strip(int mode) { g_strip = mode; }
+
+static bool strip_plan(const IGemmArgs& a, StripPlan& h, bool& wres, int& ns) {
+  const int W = a.aW, H = a.aH;
+  if (a.N % HB_BN != 0 || W < 8) return false;
+  const int nstrip = (W + 127) / 128;
+  const int TW = (W + nstrip - 1) / nstrip;
+  int TR = std::max(1, std::min(H, HB_BM / TW));
+  const int P = (TW + 2 + 7) / 8 * 8;
+  while (TR > 1 && ((TR + 2) * P + 63) / 64 > HB_HIW) --TR;
+  const int hiw = ((TR + 2) * P + 63) / 64;
+  if (hiw > HB_HIW || 2 * TR * TW < HB_BM) return false;  // at least half the MFMA rows live
+  h.tr = TR;
+  h.tw = TW;
+  h.p = P;
+  h.hiw = hiw;
+  h.tiles_c = (W + TW - 1) / TW;
+  h.tiles_img = ((H + TR - 1) / TR) * h.tiles_c;
+  h.cc = a.aC / 32;
+  const int nimg = a.M / (H * W);
+  wres = g_halo_wres && (a.N + HB_BN - 1) / HB_BN == 1 && h.cc <= 2;
+  const int lds = 2 * HB_HBYTES + 2 * HB_WBYTES;
+  ns = 2;
+  if (wres && 3 * hiw * 4096 + h.cc * HB_WBYTES <= lds) ns = 3;
+  if (ns * hiw * 4096 + (wres ? h.cc : ns) * HB_WBYTES > lds) return false;
+  h.mag_tw = magic(TW);
+  h.mag_p = magic(P);
+  h.mag_tc = magic(h.tiles_c);
+  h.mag_timg = magic(h.tiles_img);
+  h.tiles_total = nimg * h.tiles_img * ((a.N + HB_BN - 1) / HB_BN);
+  return (int64_t)nimg * h.tiles_img < (1 << 24);
+}
+
+template <int EPI>
+static void launch_strip(bool wres, int ns, int grid, const IGemmArgs& a, const StripPlan& h,
+                         hipStream_t s) {
+  if (wres && ns == 3)
+    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 3>), dim3(grid), dim3(512), 0, s, a, h);
+  else if (wres)
+    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 2>), dim3(grid), dim3(512), 0, s, a, h);
+  else
+    hipLaunchKernelGGL((conv3_strip_kernel<false, EPI, 2>), dim3(grid), dim3(512), 0, s, a, h);
+}
+
+static int conv3_strip(IGemmArgs a, hipStream_t s) {
+  StripPlan h{};
+  bool wres;
+  int ns;
+  strip_plan(a, h, wres, ns);
+  for (int t = 0; t < 9; ++t) {
+    const int r = (a.Oh + a.taps.dh[t] + 1) * 3 + (a.Ow + a.taps.dw[t] + 1);
+    h.btoff[r] = a.taps.bt[t] * a.aC * 2;
+  }
+  h.a_bytes = (uint32_t)((int64_t)a.M * a.aC * 2);
+  h.b_bytes = (uint32_t)((int64_t)a.N * a.ldb * 2);
+  a.tiles_n = (a.N + HB_BN - 1) / HB_BN;
+  a.tiles_total = h.tiles_total;
+  int g8 = std::min(std::min(active_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
+  g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
+  const int grid = 8 * g8;
+  switch (halo_epi(a)) {
+    case 0: launch_strip<0>(wres, ns, grid, a, h, s); break;
+    case EP_BETA: launch_strip<EP_BETA>(wres, ns, grid, a, h, s); break;
+    case EP_STATS: launch_strip<EP_STATS>(wres, ns, grid, a, h, s); break;
+    case EP_BIAS | EP_RELU: launch_strip<EP_BIAS | EP_RELU>(wres, ns, grid, a, h, s); break;
+    case EP_BIAS | EP_STATS: launch_strip<EP_BIAS | EP_STATS>(wres, ns, grid, a, h, s); break;
+    default: launch_strip<EP_BNRED>(wres, ns, grid, a, h, s); break;
+  }
+  return grid;
+}
+
+// strip tiles for this launch: images the linear tiles cannot hold, or (MPA_HALO_STRIP=2)
+// resident-weight layers that get a third stage
+static bool use_strip(const IGemmArgs& a, bool linear) {
+  if (g_strip < 1) return false;
+  StripPlan h{};
+  bool wres;
+  int ns;
+  if (!strip_plan(a, h, wres, ns)) return false;
+  return !linear || (g_strip >= 2 && ns == 3);
+}
+
+bool conv3_halo_ok(const IGemmArgs& a) {
+  bool linear;
+  if (!halo_ok_impl(a, linear)) return false;
+  return linear || use_strip(a, linear);
+}
 
 // Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves; each MFMA wave then has
 // 256 registers, which every flavour fits).  MPA_HALO_PROD=0: 4-wave blocks.
@@ -949,6 +1361,11 @@ static void launch_halo32(bool wres, int grid, const IGemmArgs& a, const HaloPla
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
 // returns the number of statistics-slab rows written (one per block, <= HALO_MAX_ROWS).
 int conv3_halo(IGemmArgs a, hipStream_t s) {
+  {
+    bool linear;
+    halo_ok_impl(a, linear);
+    if (use_strip(a, linear)) return conv3_strip(a, s);
+  }
   HaloPlan h{};
   h.dbg = g_halo_dbg & 1;
   const int W2 = halo_pitch(a.aW);

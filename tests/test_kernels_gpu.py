@@ -331,6 +331,77 @@ def test_conv_halo_dgrad(gpu, case):
         assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
 
 
+STRIP_CASES = [
+    # N, H, W, C, K, MPA_HALO_STRIP mode
+    (2, 112, 112, 64, 64, 1),   # VGG 112^2 (resident weights, one 112-wide strip)
+    (1, 224, 224, 64, 64, 1),   # VGG 224^2 (two 112-wide strips)
+    (2, 33, 150, 64, 128, 1),   # partial row bands and strips, two column tiles
+    (3, 20, 131, 96, 64, 1),    # three channel chunks: streamed weights
+    (1, 147, 147, 32, 64, 1),   # Inception Conv2d_2b
+    (4, 56, 56, 64, 64, 2),     # ResNet layer1: 4 x 56 tiles, 3-stage ring
+    (2, 56, 56, 64, 64, 0),     # (linear tiles, for comparison)
+]
+
+
+@pytest.mark.parametrize("case", STRIP_CASES)
+def test_conv_halo_strip(gpu, case):
+    """Strip-tiled halo kernel (2-D tiles, images wider than the linear tiles hold; 3-stage
+    ring for resident-weight layer1 shapes): forward with BN statistics, bias + ReLU,
+    dgrad plain / accumulating / fused BN reduction == implicit GEMM and the oracle."""
+    torch.manual_seed(25)
+    N, H, W, Cc, K, mode = case
+    C().igemm_set_halo_strip(mode)
+    try:
+        x = bf(N, H, W, Cc, dev=gpu)
+        w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * Cc))
+        b = torch.randn(K, device=gpu)
+        e = torch.empty(0, device=gpu)
+        shift = torch.randn(K, device=gpu) * 0.1
+        for bias, relu, stats in ((e, False, True), (b, True, False)):
+
+            def run():
+                st = torch.zeros(2, K, device=gpu) if stats else e
+                return C().conv_fwd(x, w, bias, 1, 1, 1, 1, relu, st, shift if stats else e), st
+
+            (y, st), (y0, st0) = _halo_pair(run)
+            str_ = torch.zeros(2, K, device=gpu) if stats else e
+            yr = ref.conv_fwd(x, w, bias, 1, 1, 1, 1, relu, str_, shift if stats else e)
+            assert rel(y, y0) < 1e-2 and rel(y, yr) < 2e-2
+            if stats:
+                assert rel(st, st0) < 1e-3 and rel(st, str_) < 2e-2
+        dy = bf(N, H, W, K, dev=gpu)
+        wd = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * K))
+        wt = wd.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+        dx, dx0 = _halo_pair(lambda: C().conv_dgrad(dy, wd, H, W, 1, 1, 1, 1, wt))
+        dxr = ref.conv_dgrad(dy, wd, H, W, 1, 1, 1, 1)
+        assert rel(dx, dx0) < 1e-2 and rel(dx, dxr) < 2e-2
+        acc0 = bf(N, H, W, Cc, dev=gpu)
+        acc, _ = _halo_pair(lambda: C().conv_dgrad(dy, wd, H, W, 1, 1, 1, 1, wt, acc0.clone()))
+        assert rel(acc, acc0.float() + dxr.float()) < 2e-2
+        z = bf(N, H, W, Cc, dev=gpu, scale=2.0)
+        mean = torch.randn(Cc, device=gpu) * 0.3
+        rstd = torch.rand(Cc, device=gpu) + 0.5
+        gamma = torch.rand(Cc, device=gpu) + 0.5
+        beta = torch.randn(Cc, device=gpu) * 0.2
+        sc = gamma * rstd
+        yz = torch.relu(z.float() * sc + (beta - mean * sc)).to(torch.bfloat16)
+        (g, sums), (g0, sums0) = _halo_pair(
+            lambda: C().conv_dgrad_bnred(dy, wd, H, W, 1, 1, 1, 1, wt, z, yz, mean, rstd,
+                                         gamma=gamma, beta=beta))
+        gr, sr = ref.conv_dgrad_bnred(dy, wd, H, W, 1, 1, 1, 1, None, z, None, mean, rstd,
+                                      gamma, beta)
+        assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
+        assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+        # persistent ring: repeated launches bitwise identical (race screen)
+        C().igemm_set_halo(1)
+        outs = [C().conv_dgrad(dy, wd, H, W, 1, 1, 1, 1, wt) for _ in range(3)]
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, outs[0]) for o in outs[1:])
+    finally:
+        C().igemm_set_halo_strip(1)
+        C().igemm_set_halo(0)
+
+
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_wgrad(gpu, case):
     """Halo-staged 3x3/s1 weight gradient (slab partials + reduce, accumulating into dw)
