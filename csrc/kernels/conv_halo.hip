@@ -600,10 +600,15 @@ struct StripPlan {
   int hiw;                  // halo DMA instructions per producer wave per item (<= 9)
   int tiles_c, tiles_img;   // column strips per row band, tiles per image
   int tiles_total, cc;
-  uint32_t mag_tw, mag_p, mag_tc, mag_timg;  // floor(2^32 / d) + 1
+  uint32_t mag_tw, mag_p, mag_tc, mag_timg;  // floor(2^32 / d) + 1 (0: d == 1)
   int btoff[9];
   uint32_t a_bytes, b_bytes;
 };
+
+// n / d from udiv's magic, with magic 0 standing for d == 1 (floor(2^32 / 1) + 1 wraps)
+__device__ __forceinline__ uint32_t udiv1(uint32_t n, uint32_t mag) {
+  return mag ? udiv(n, mag) : n;
+}
 
 // s_waitcnt vmcnt(n) for the run-time per-item DMA counts of the strip producers
 __device__ __forceinline__ void strip_wait(int n) {
@@ -648,9 +653,9 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
   // tile tk of this block -> (image, first row, first column)
   auto origin = [&](int tk, int& img, int& r0, int& c0) {
     const uint32_t mt = (uint32_t)((tbeg + loc + tk * G8) / p.tiles_n);
-    img = (int)udiv(mt, h.mag_timg);
+    img = (int)udiv1(mt, h.mag_timg);
     const uint32_t rem = mt - (uint32_t)img * h.tiles_img;
-    const uint32_t tr = udiv(rem, h.mag_tc);
+    const uint32_t tr = udiv1(rem, h.mag_tc);
     r0 = (int)tr * TR;
     c0 = (int)(rem - tr * h.tiles_c) * TW;
   };
@@ -1247,8 +1252,8 @@ static bool strip_plan(const IGemmArgs& a, StripPlan& h, bool& wres, int& ns) {
   if (ns * hiw * 4096 + (wres ? h.cc : ns) * HB_WBYTES > lds) return false;
   h.mag_tw = magic(TW);
   h.mag_p = magic(P);
-  h.mag_tc = magic(h.tiles_c);
-  h.mag_timg = magic(h.tiles_img);
+  h.mag_tc = h.tiles_c > 1 ? magic(h.tiles_c) : 0u;
+  h.mag_timg = h.tiles_img > 1 ? magic(h.tiles_img) : 0u;
   h.tiles_total = nimg * h.tiles_img * ((a.N + HB_BN - 1) / HB_BN);
   return (int64_t)nimg * h.tiles_img < (1 << 24);
 }
