@@ -922,6 +922,10 @@ struct HaloWPlan {
   int tiles_m, parts, kparts, Z;
   uint32_t dy_bytes, x_bytes;
   int dbg;  // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
+  // STRIP: tiles of tr rows x tw columns of one image (w2 = tw + 2 rounded up to 16), for
+  // images too wide for the 128-pixel linear tiles' halo (VGG 224^2 / 112^2)
+  int tr, tw, tiles_c, tiles_img;
+  uint32_t mag_tw, mag_tc, mag_timg;  // (0: divisor 1)
 };
 
 // W2T: the halo pitch as a compile-time constant (16 / 32 / 48 / 64: every ResNet and
@@ -931,7 +935,7 @@ struct HaloWPlan {
 // of a stage hold ONE 896-pixel halo image of the first chunk (14 DMA instructions per
 // wave instead of 2 x 7).  Waves 2 and 3 then read chunk 0 as well; their partials are
 // duplicates of waves 0 / 1 and are not stored.
-template <int W2T, bool ONECH = false>
+template <int W2T, bool ONECH = false, bool STRIP = false>
 __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
   constexpr int HIW = ONECH ? 2 * HW_HIW : HW_HIW;  // halo DMA instructions per wave (chunk)
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
@@ -954,7 +958,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   for (int j = 0; j < 4; ++j) {
     const int row = 8 * (4 * wave + j) + (lane >> 3);
     const int chunk = (lane & 7) ^ mn_swz<64>(row & 31);
-    drow[j] = ((uint32_t)row * K + k0 + chunk * 8) * 2;  // + pixel0 * K * 2 per tile
+    // linear: + pixel0 * K * 2 per tile; STRIP: + (the row's pixel) * K * 2
+    drow[j] = ((uint32_t)(STRIP ? 0 : row) * K + k0 + chunk * 8) * 2;
     kok[j] = k0 + chunk * 8 < K;
   }
   // halo: instruction j = pixels 16 (7 wave + j) + lane/4 of the image; chunk 1 of the
@@ -981,7 +986,49 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   // and the row pitch W2 is a multiple of 16, so a tap's row offset dh * W2 never changes
   // it - the swizzled address of pixel (hp + dh*W2 + dw) is hbw[dw] + dh*W2*64
   int hbw[4][2][3];
+  const int tpx = STRIP ? h.tr * h.tw : HW_BM;
+  if constexpr (STRIP) {
+    // B-row addresses are tile-independent: local pixel n -> slot (lr + 1), column (lc + 1);
+    // rows past the tile (dy rows zero) read its last pixel
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const uint32_t n = (uint32_t)min(ks * 32 + 8 * g + 4 * e + q, tpx - 1);
+        const uint32_t lr = udiv1(n, h.mag_tw), lc = n - lr * h.tw;
+        const int hp = (int)(lr + 1) * W2 + (int)lc + 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const int x = (hp + d - 1) * 64 + cbyte;
+          hbw[ks][e][d] = x ^ ((x >> 4) & 32);
+        }
+      }
+  }
   auto prep = [&](int mt) {
+    if constexpr (STRIP) {
+      const int img = (int)udiv1((uint32_t)mt, h.mag_timg);
+      const uint32_t rem = (uint32_t)(mt - img * h.tiles_img);
+      const uint32_t band = udiv1(rem, h.mag_tc);
+      const int r0 = (int)band * h.tr, cs0 = (int)(rem - band * h.tiles_c) * h.tw;
+#pragma unroll
+      for (int j = 0; j < HIW; ++j) {
+        const int sl = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255);
+        const int ih = r0 - 1 + sl, iw = cs0 - 1 + col;
+        const bool ok = sl < h.tr + 2 && col < h.tw + 2 && (unsigned)ih < (unsigned)H &&
+                        (unsigned)iw < (unsigned)W;
+        hv[j] = ok ? ((((uint32_t)img * H + ih) * W + iw) * C + c0) * 2 + (hsc[j] >> 18) * 16
+                   : 0x80000000u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t row = 8 * (4 * wave + j) + (lane >> 3);
+        const uint32_t lr = udiv1(row, h.mag_tw), lc = row - lr * h.tw;
+        const bool ok = (int)row < tpx && r0 + (int)lr < H && cs0 + (int)lc < W && kok[j];
+        dv[j] = ok ? drow[j] + (((uint32_t)img * H + r0 + lr) * W + cs0 + lc) * (uint32_t)K * 2
+                   : 0x80000000u;
+      }
+      return;
+    }
     const int m0 = mt * HW_BM;
     const int img0 = m0 / HW;
     const int r0 = m0 - img0 * HW;
@@ -1414,15 +1461,54 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
 // ------------------------------------------------------------------ halo wgrad host
 static int halo_wgrad_pitch(int W) { return (W + 2 + 15) / 16 * 16; }
 
-static bool halo_wgrad_geom(const WGradArgs& a) {
+// shape checks shared by the linear and strip tilings
+static bool halo_wgrad_base(const WGradArgs& a) {
   if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1)
     return false;
   // 64 x 64 partitions; a 32-wide remainder in either dimension is zero-filled
   if (a.P != a.H || a.Q != a.W || a.C % 32 != 0 || a.Kout % 32 != 0) return false;
   const int64_t HW = (int64_t)a.H * a.W;
-  if (a.Mpix % HW != 0 || HW + HW_BM >= 65536 || a.W + 2 > 255) return false;
-  if ((int64_t)a.Mpix * a.C * 2 >= (1ll << 31) || (int64_t)a.Mpix * a.Kout * 2 >= (1ll << 31))
-    return false;
+  if (a.Mpix % HW != 0) return false;
+  return (int64_t)a.Mpix * a.C * 2 < (1ll << 31) && (int64_t)a.Mpix * a.Kout * 2 < (1ll << 31);
+}
+
+// strip tiling of the weight gradient (images too wide for the linear tiles): the TR x TW
+// tile (TR * TW <= 128 pixels) minimising tiles x (128 MFMA rows + staged halo pixels)
+static bool halo_wgrad_strip_plan(const WGradArgs& a, HaloWPlan& h) {
+  if (g_strip < 1 || !halo_wgrad_base(a)) return false;
+  const int64_t nimg = a.Mpix / ((int64_t)a.H * a.W);
+  int64_t best = -1;
+  for (int n = 1; n <= a.W; ++n) {
+    const int tw = (a.W + n - 1) / n;
+    if (tw > 126 || (n > 1 && (a.W + tw - 1) / tw != n)) continue;
+    if (tw < 8) break;
+    const int pitch = (tw + 2 + 15) / 16 * 16;
+    int tr = std::max(1, std::min(a.H, HW_BM / tw));
+    while (tr > 1 && (tr + 2) * pitch > HW_HPX) --tr;
+    if ((tr + 2) * pitch > HW_HPX) continue;
+    const int64_t tiles = nimg * ((a.H + tr - 1) / tr) * n;
+    const int64_t cost = tiles * (HW_BM + (tr + 2) * pitch);
+    if (best < 0 || cost < best) {
+      best = cost;
+      h.tr = tr;
+      h.tw = tw;
+      h.w2 = pitch;
+      h.tiles_c = n;
+      h.tiles_img = ((a.H + tr - 1) / tr) * n;
+      h.tiles_m = (int)tiles;
+    }
+  }
+  if (best < 0 || h.tiles_m <= 0) return false;
+  h.mag_tw = magic(h.tw);
+  h.mag_tc = h.tiles_c > 1 ? magic(h.tiles_c) : 0u;
+  h.mag_timg = h.tiles_img > 1 ? magic(h.tiles_img) : 0u;
+  return true;
+}
+
+static bool halo_wgrad_geom(const WGradArgs& a) {
+  if (!halo_wgrad_base(a)) return false;
+  const int64_t HW = (int64_t)a.H * a.W;
+  if (HW + HW_BM >= 65536 || a.W + 2 > 255) return false;
   const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
   const int64_t seps = (HW_BM - 1) / HW + 1;
   // 32-channel partitions may use both chunk areas for one wider halo image (ONECH)
@@ -1443,13 +1529,30 @@ int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols) {
 }
 
 bool conv3_halo_wgrad_ok(const WGradArgs& a) {
-  return halo_wgrad_geom(a) && a.slab != nullptr;
+  if (a.slab == nullptr) return false;
+  if (halo_wgrad_geom(a)) return true;
+  HaloWPlan h{};
+  return halo_wgrad_strip_plan(a, h);
 }
 
 // slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   HaloWPlan h{};
   h.dbg = g_halo_dbg & 1;
+  if (!halo_wgrad_geom(a) && halo_wgrad_strip_plan(a, h)) {
+    const int W2 = h.w2;
+    for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);
+    h.mag_w2 = magic(W2);
+    h.kparts = (a.Kout + 63) / 64;
+    h.parts = h.kparts * ((a.C + 63) / 64);
+    const int G = std::min(active_cus(), HALO_MAX_ROWS);
+    h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
+    h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
+    h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
+    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, false, true>), dim3(h.parts * h.Z), dim3(256),
+                       0, s, a, h);
+    return h.Z;
+  }
   const int W2 = halo_wgrad_pitch(a.W);
   h.w2 = W2;
   for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);

@@ -392,6 +392,18 @@ def test_conv_halo_strip(gpu, case):
                                       gamma, beta)
         assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
         assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+        # weight gradient (strip tiles where the linear 128-pixel tiles do not fit)
+        dw0 = torch.randn(K, 3, 3, Cc, device=gpu)
+
+        def wg():
+            dw = dw0.clone()
+            C().conv_wgrad(dy, x, dw, 1, 1, 1, 1)
+            return dw
+
+        dw, dwi = _halo_pair(wg)
+        dwr = dw0.clone()
+        ref.conv_wgrad(dy, x, dwr, 1, 1, 1, 1)
+        assert rel(dw - dw0, dwi - dw0) < 1e-2 and rel(dw - dw0, dwr - dw0) < 2e-2
         # persistent ring: repeated launches bitwise identical (race screen)
         C().igemm_set_halo(1)
         outs = [C().conv_dgrad(dy, wd, H, W, 1, 1, 1, 1, wt) for _ in range(3)]
