@@ -874,8 +874,11 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t kh, int64_t kw, int64_t sh, in
   const c10::OptionalDeviceGuard g(device_of(x));
   Tensor y = empty_like_shape(x, {N, P, Q, C}, torch::kBFloat16);
   Tensor idx = empty_like_shape(x, {N, P, Q, C}, torch::kUInt8);
-  mpa::maxpool_fwd(bp(x), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, bpm(y), idx.data_ptr<uint8_t>(),
-                   cur_stream());
+  if (mpa::maxpool2_ok(N, H, W, C, kh, kw, sh, sw, ph, pw))
+    mpa::maxpool2_fwd(bp(x), N, H, W, C, bpm(y), idx.data_ptr<uint8_t>(), cur_stream());
+  else
+    mpa::maxpool_fwd(bp(x), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw, bpm(y),
+                     idx.data_ptr<uint8_t>(), cur_stream());
   return {y, idx};
 }
 
@@ -886,9 +889,37 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t kh, int6
   (void)ceil;
   const c10::OptionalDeviceGuard g(device_of(dy));
   Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
-  mpa::maxpool_bwd(bp(dy), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw,
-                   bpm(dx), cur_stream());
+  if (mpa::maxpool2_ok(N, H, W, C, kh, kw, sh, sw, ph, pw))
+    mpa::maxpool2_bwd(bp(dy), idx.data_ptr<uint8_t>(), nullptr, N, H, W, C, bpm(dx), nullptr,
+                      nullptr, cur_stream());
+  else
+    mpa::maxpool_bwd(bp(dy), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw,
+                     bpm(dx), cur_stream());
   return dx;
+}
+
+// max-pool backward whose input is a ReLU output handed over by its producer (Fn.BNLink):
+// the gradient routes only where the pooled value is > 0, and the per-channel sum of what
+// is routed (the producer's bias gradient) comes back with it.  None: not a 2x2/s2 pool.
+c10::optional<std::vector<Tensor>> maxpool_bwd_relu(Tensor dy, Tensor idx, Tensor y, int64_t H,
+                                                    int64_t W, int64_t kh, int64_t kw,
+                                                    int64_t sh, int64_t sw, int64_t ph,
+                                                    int64_t pw) {
+  CHECK_ACT(dy);
+  CHECK_ACT(y);
+  const int N = dy.size(0), C = dy.size(3);
+  if (!mpa::maxpool2_ok(N, H, W, C, kh, kw, sh, sw, ph, pw)) return c10::nullopt;
+  TORCH_CHECK(y.sizes() == dy.sizes() && idx.sizes() == dy.sizes() &&
+                  idx.scalar_type() == torch::kUInt8 && idx.is_contiguous(),
+              "maxpool_bwd_relu: pooled tensors");
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  Tensor sums = torch::empty({C}, dy.options().dtype(torch::kFloat32));
+  Tensor ws = torch::empty({mpa::maxpool2_ws_floats(N, H, W, C)},
+                           dy.options().dtype(torch::kFloat32));
+  mpa::maxpool2_bwd(bp(dy), idx.data_ptr<uint8_t>(), bp(y), N, H, W, C, bpm(dx),
+                    sums.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+  return std::vector<Tensor>{dx, sums};
 }
 
 // conv -> BN -> ReLU -> max-pool stem: z is the raw conv output, stats its (shifted)
@@ -1574,6 +1605,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rmean"), py::arg("rvar"), py::arg("eps"), py::arg("res"), py::arg("relu"),
         py::arg("channels") = 0);
   m.def("bn_bwd_pair", &bn_bwd_pair);
+  m.def("maxpool_bwd_relu", &maxpool_bwd_relu);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("want_dx"), py::arg("want_g"), py::arg("zmask_beta") = py::none(),

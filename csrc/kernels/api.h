@@ -271,6 +271,15 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
 // backward of relu(bn(x) + bn2(x2)), both train-mode BNs (bn2: a deferred downsample BN
 // applied on read): dx and dx2 from one reduce and one apply pass, mask = the forward's bit
 // mask; ws holds bn_pair_ws_floats(M, C) floats
+// 2x2 / stride-2 / pad-0 max pool over an even image (VGG): one pooled pixel x 8 channels
+// per thread; backward with yp + sums: the pooled tensor is a ReLU output whose producer's
+// mask and bias-gradient sum are applied / reduced here (sums [C]; ws maxpool2_ws_floats)
+bool maxpool2_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw);
+void maxpool2_fwd(const bf16_raw* x, int N, int H, int W, int C, bf16_raw* y, uint8_t* idx,
+                  hipStream_t s);
+int64_t maxpool2_ws_floats(int N, int H, int W, int C);
+void maxpool2_bwd(const bf16_raw* dy, const uint8_t* idx, const bf16_raw* yp, int N, int H, int W,
+                  int C, bf16_raw* dx, float* sums, float* ws, hipStream_t s);
 int64_t bn_pair_ws_floats(int M, int C);
 void bn_bwd_pair(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* x2, const uint8_t* ymask,
                  const float* mean, const float* rstd, const float* gamma, const float* mean2,

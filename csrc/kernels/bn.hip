@@ -581,6 +581,114 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       });
 }
 
+// ------------------------------------------------------- 2x2 / stride-2 max pool (VGG)
+// The generic kernels above split every flat index with 64-bit divisions, loop over
+// window bounds and move the argmax byte by byte.  A 2x2/s2/p0 pool over an even image
+// tiles the input exactly: one thread = one pooled pixel x 8 channels, four 16-B loads in,
+// one 16-B value + one 8-B argmax out (forward), or one 2x2 block of 16-B stores (backward:
+// every input pixel is written exactly once, no gather, no atomics).
+__global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const bf16_t* __restrict__ x, int NP,
+                                                           int Q, int C, bf16_t* __restrict__ y,
+                                                           uint8_t* __restrict__ idx) {
+  const int cv = C / 8;
+  const int total = NP * Q * cv;  // (n, p) rows x Q x chunks (host: < 2^31)
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const int cc = t % cv, r = t / cv;  // r = (n * P + p) * Q + q
+    const int q = r % Q, np_ = r / Q;
+    // input pixel (n, 2p + a, 2q + b) = row 2 * np_ + a of the [N * H] rows, width 2Q
+    const size_t row0 = (size_t)(2 * np_) * (2 * Q) + 2 * q;
+    const size_t W2C = (size_t)2 * Q * C;
+    uint4 v[4];
+    v[0] = *(const uint4*)(x + row0 * C + cc * 8);
+    v[1] = *(const uint4*)(x + (row0 + 1) * C + cc * 8);
+    v[2] = *(const uint4*)(x + row0 * C + W2C + cc * 8);
+    v[3] = *(const uint4*)(x + (row0 + 1) * C + W2C + cc * 8);
+    float best[8], f[8];
+    uint32_t bi[8];
+    unpack8(v[0], best);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bi[j] = 0;
+#pragma unroll
+    for (int u = 1; u < 4; ++u) {
+      unpack8(v[u], f);
+      // window tap of input (a, b) in a 2x2 window: a * 2 + b (first max wins, NaN wins)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (f[j] > best[j] || (f[j] != f[j] && best[j] == best[j])) {
+          best[j] = f[j];
+          bi[j] = u;
+        }
+    }
+    const size_t o = (size_t)r * C + cc * 8;
+    *(uint4*)(y + o) = pack8(best);
+    uint2 ib;
+    ib.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    ib.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *(uint2*)(idx + o) = ib;
+  }
+}
+
+// RELU: the pooled tensor is a ReLU output whose producer's backward is handed over
+// (Fn.BNLink): the gradient routes only where the pooled value is > 0 (the argmax element
+// IS the pooled value, so that is the producer's own y > 0 mask), and the per-channel sum
+// of the routed gradient - the producer's bias gradient - is slab-reduced here.
+template <bool RELU>
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ yp,
+    int NP, int Q, int C, bf16_t* __restrict__ dx, float* __restrict__ slab,
+    float* __restrict__ sums) {
+  const ColMap cm = colmap(C / 8);
+  float sg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = 0.f;
+  if (cm.active) {
+    const int c0 = cm.cc * 8;
+    if (RELU && blockIdx.x == 0 && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sums[c0 + j] = 0.f;
+    }
+    const int M = NP * Q;
+    const size_t W2C = (size_t)2 * Q * C;
+    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
+      const size_t o = (size_t)r * C + c0;
+      const uint4 gv = *(const uint4*)(dy + o);
+      const uint2 iv = *(const uint2*)(idx + o);
+      float g[8];
+      unpack8(gv, g);
+      if constexpr (RELU) {
+        float yv[8];
+        unpack8(*(const uint4*)(yp + o), yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          g[j] = yv[j] > 0.f ? g[j] : 0.f;
+          sg[j] += g[j];
+        }
+      }
+      const int q = r % Q, np_ = r / Q;
+      const size_t row0 = (size_t)(2 * np_) * (2 * Q) + 2 * q;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float d[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t w = j < 4 ? iv.x : iv.y;
+          d[j] = ((w >> (8 * (j & 3))) & 0xff) == (uint32_t)u ? g[j] : 0.f;
+        }
+        bf16_t* p = dx + (row0 + (u & 1)) * C + (u >> 1) * W2C + c0;
+        *(uint4*)p = pack8(d);
+      }
+    }
+  }
+  if constexpr (RELU) {
+    __shared__ float red[256 * 8];
+    block_reduce8(sg, cm, red);
+    if (cm.active && cm.r0 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) slab[(size_t)blockIdx.x * C + cm.cc * 8 + j] = sg[j];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- residual BN pair
 // Backward of y = relu(bn(x) + bn2(x2)) when BOTH BNs are train-mode (ResNet's bn2 and the
 // deferred downsample BN it applies on read, Fn.BNDefer): both see the same upstream
@@ -1586,6 +1694,41 @@ void bn_bwd_apply(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, cons
   BN_LAUNCH_T(bn_bwd_apply_kernel, false, grid_for(M, C), s, dy, x, y, mean, rstd, gamma,
               (const float*)nullptr, sums, dgamma, dbeta, M, C, dx, g, (const uint8_t*)nullptr, C,
               (float*)nullptr, 0, C, lddy);
+}
+
+
+bool maxpool2_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
+  return kh == 2 && kw == 2 && sh == 2 && sw == 2 && ph == 0 && pw == 0 && H % 2 == 0 &&
+         W % 2 == 0 && C % 8 == 0 && (int64_t)N * H * W * C < (1ll << 31);
+}
+
+void maxpool2_fwd(const bf16_raw* x, int N, int H, int W, int C, bf16_raw* y, uint8_t* idx,
+                  hipStream_t s) {
+  const int NP = N * (H / 2), Q = W / 2;
+  const int64_t total = (int64_t)NP * Q * (C / 8);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, NP, Q, C,
+                     (bf16_t*)y, idx);
+}
+
+int64_t maxpool2_ws_floats(int N, int H, int W, int C) {
+  return (int64_t)(grid_for(N * (H / 2) * (W / 2), C).x + 1) * C;
+}
+
+void maxpool2_bwd(const bf16_raw* dy, const uint8_t* idx, const bf16_raw* yp, int N, int H, int W,
+                  int C, bf16_raw* dx, float* sums, float* ws, hipStream_t s) {
+  const int NP = N * (H / 2), Q = W / 2;
+  const dim3 gr = grid_for(NP * Q, C);
+  if (yp && sums) {
+    float* slab = ws;
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<true>, gr, dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (const bf16_t*)yp, NP, Q, C, (bf16_t*)dx, slab, sums);
+    slab_reduce(slab, gr.x, C, sums, false, s);
+  } else {
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<false>, gr, dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (const bf16_t*)nullptr, NP, Q, C, (bf16_t*)dx, (float*)nullptr,
+                       (float*)nullptr);
+  }
 }
 
 int64_t bn_pair_ws_floats(int M, int C) { return (int64_t)3 * C * (1 + grid_for(M, C).x); }

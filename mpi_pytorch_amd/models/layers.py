@@ -475,6 +475,10 @@ class FusedSequential(nn.Sequential):
             if isinstance(mods[i], Conv2d):
                 return Fn.conv_act(x, mods[i], relu=True, link_in=link_in, link_out=link_out)
             return mods[i](x, relu=True)
+        if link_in is not None and isinstance(mods[i], MaxPool2d):
+            m = mods[i]
+            return Fn.max_pool2d(x, m.kernel_size, m.stride, m.padding, m.ceil_mode,
+                                 link_in=link_in)
         return mods[i](x)
 
     def links(self, gs):
@@ -491,6 +495,13 @@ class FusedSequential(nn.Sequential):
             if (kind in ("relu", "conv_bn_relu") and isinstance(mods[i], Conv2d)
                     and kind2 in ("relu", "conv_bn_relu", "conv_bn")
                     and isinstance(mods[j], Conv2d) and not mods[j].pair):
+                out[k] = True
+            # conv -> ReLU -> 2x2/s2 max pool (VGG block ends): the pool's backward applies
+            # the ReLU mask and reduces the conv's bias gradient (no act_bwd pass)
+            m = mods[j]
+            if (kind == "relu" and isinstance(mods[i], Conv2d) and kind2 == "plain"
+                    and isinstance(m, MaxPool2d) and m.kernel_size == (2, 2)
+                    and m.stride == (2, 2) and m.padding == (0, 0)):
                 out[k] = True
         return out
 

@@ -871,27 +871,40 @@ def linear_act(x, lin, relu: bool = False):
 # ================================================================================= pools
 class _MaxPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, cfg, join=None):
+    def forward(ctx, x, cfg, join=None, link_in=None):
         y, idx = K(x).maxpool_fwd(x, *cfg)
         ctx.cfg = cfg
         ctx.join = join
+        ctx.link_in = link_in
         ctx.hw = (x.shape[1], x.shape[2])
-        ctx.save_for_backward(idx)
+        ctx.save_for_backward(idx, y if link_in is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (idx,) = ctx.saved_tensors
-        dx = K(dy).maxpool_bwd(dy.contiguous(), idx, ctx.hw[0], ctx.hw[1], *ctx.cfg)
-        return _join_grad(ctx.join, dx), None, None
+        idx, y = ctx.saved_tensors
+        k = K(dy)
+        dy = dy.contiguous()
+        li = ctx.link_in
+        if li is not None and ctx.join is None and hasattr(k, "maxpool_bwd_relu"):
+            # the input is a ReLU output whose producer handed its backward over (BNLink):
+            # route only where the pooled value is > 0 and return the producer's bias sums
+            r = k.maxpool_bwd_relu(dy, idx, y, ctx.hw[0], ctx.hw[1], *ctx.cfg[:6])
+            if r is not None:
+                li.sums = r[1]
+                return r[0], None, None, None
+        dx = k.maxpool_bwd(dy, idx, ctx.hw[0], ctx.hw[1], *ctx.cfg)
+        return _join_grad(ctx.join, dx), None, None, None
 
 
 def max_pool2d(x, kernel, stride, padding=(0, 0), ceil_mode=False,
-               join: Optional[GradJoin] = None):
-    """``join``: the input's other consumers share it (see GradJoin)."""
+               join: Optional[GradJoin] = None, link_in: Optional[BNLink] = None):
+    """``join``: the input's other consumers share it (see GradJoin); ``link_in``: the input
+    is a conv -> ReLU output that feeds only this pool, and the pool's backward applies the
+    ReLU mask and reduces the conv's bias gradient (Fn.BNLink; 2x2/s2 pools)."""
     cfg = (kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], bool(ceil_mode))
     if torch.is_grad_enabled() and x.requires_grad:
-        return _MaxPool.apply(x, cfg, join)
+        return _MaxPool.apply(x, cfg, join, link_in)
     return K(x).maxpool_fwd(x, *cfg)[0]
 
 

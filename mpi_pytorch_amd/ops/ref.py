@@ -397,6 +397,17 @@ def maxpool_bwd(dy, idx, H, W, kh, kw, sh, sw, ph, pw, ceil):
     return _nhwc(out.reshape(N, C, H, W)).to(dy.dtype)
 
 
+def maxpool_bwd_relu(dy, idx, y, H, W, kh, kw, sh, sw, ph, pw):
+    """Max-pool backward of a ReLU output handed over by its producer: the gradient routes
+    only where the pooled value is > 0; returns (dx, per-channel sum of the routed
+    gradient), or None when the fused kernel would not apply (not a 2x2/s2/p0 pool)."""
+    if not (kh == kw == sh == sw == 2 and ph == pw == 0 and H % 2 == 0 and W % 2 == 0):
+        return None
+    g = _f(dy) * (_f(y) > 0)
+    dx = maxpool_bwd(g, idx, H, W, kh, kw, sh, sw, ph, pw, False).to(dy.dtype)
+    return dx, g.reshape(-1, g.shape[-1]).sum(0)
+
+
 def bn_relu_maxpool_fwd(z, stats, gamma, beta, rmean, rvar, momentum, eps, kh, kw, sh, sw, ph,
                         pw, ceil, counter=None, zsel_out=None):
     y, mean, rstd = bn_fwd_train(z, stats, gamma, beta, rmean, rvar, momentum, eps, None, True,

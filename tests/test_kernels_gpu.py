@@ -870,6 +870,37 @@ def _bn_pair_checks(dy, x, x2, mask, mean, rstd, g, mean2, rstd2, g2, Cc, gpu):
     assert rel(dx2, tx2) < 1e-2  # (the two-stage form rounds g to bf16 first)
 
 
+@pytest.mark.parametrize("N,H,W,Cc", [(2, 8, 10, 64), (4, 56, 56, 128), (1, 224, 224, 64)])
+def test_maxpool2_fast_path_and_relu_handoff(gpu, N, H, W, Cc):
+    """2x2/s2 max pool fast kernels == the generic window kernels' argmax encoding and the
+    oracle (forward values, backward routing), and the ReLU-linked backward (mask from the
+    pooled value, bias-gradient sums) == generic backward of the masked gradient."""
+    torch.manual_seed(31)
+    x = torch.relu(bf(N, H, W, Cc, dev=gpu)).to(torch.bfloat16)  # a ReLU output (ties at 0)
+    y, idx = C().maxpool_fwd(x, 2, 2, 2, 2, 0, 0, False)
+    yr, _ = ref.maxpool_fwd(x, 2, 2, 2, 2, 0, 0, False)
+    assert torch.equal(y, yr.to(y.dtype))
+    # generic kernels (3-wide window trick: kernel 2 via a non-fast shape is not reachable,
+    # so check the encoding directly: tap a*2+b holds the max and is the first max)
+    xv = x.float().reshape(N, H // 2, 2, W // 2, 2, Cc).permute(0, 1, 3, 2, 4, 5)
+    xv = xv.reshape(N, H // 2, W // 2, 4, Cc)
+    first = (xv == y.float().unsqueeze(3)).float().argmax(3)
+    assert torch.equal(idx.long(), first)
+    dy = bf(N, H // 2, W // 2, Cc, dev=gpu)
+    dx = C().maxpool_bwd(dy, idx, H, W, 2, 2, 2, 2, 0, 0, False)
+    exp = torch.zeros(N, H // 2, W // 2, 4, Cc, device=gpu)
+    exp.scatter_(3, idx.long().unsqueeze(3), dy.float().unsqueeze(3))
+    exp = exp.reshape(N, H // 2, W // 2, 2, 2, Cc).permute(0, 1, 3, 2, 4, 5).reshape(N, H, W, Cc)
+    assert torch.equal(dx.float(), exp)
+    dxr, sums = C().maxpool_bwd_relu(dy, idx, y, H, W, 2, 2, 2, 2, 0, 0)
+    g = dy.float() * (y.float() > 0)
+    dxm = C().maxpool_bwd(g.to(torch.bfloat16), idx, H, W, 2, 2, 2, 2, 0, 0, False)
+    torch.cuda.synchronize()
+    assert torch.equal(dxr, dxm)
+    assert rel(sums, g.reshape(-1, Cc).sum(0)) < 1e-4
+    assert C().maxpool_bwd_relu(dy, idx, y, H, W, 3, 3, 2, 2, 1, 1) is None
+
+
 @pytest.mark.parametrize("M,Cc,Ctot", [(4096, 64, 96), (3001, 136, 256), (50000, 32, 32)])
 def test_bn_channel_prefix_and_accumulate(gpu, M, Cc, Ctot):
     """DenseNet block buffer: BN (train / eval forward, z-mask backward) of the first Cc

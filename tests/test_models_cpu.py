@@ -503,8 +503,9 @@ def test_resnet_bn_pair_backward_equals_separate(monkeypatch):
 
 
 def test_feature_stack_links_match_unlinked():
-    """FusedSequential's conv -> ReLU -> conv hand-offs (the consumer dgrad applies the
-    producer's ReLU mask / BN reduction, no act_bwd or reduce pass) give the same
+    """FusedSequential's conv -> ReLU -> conv / 2x2 max-pool hand-offs (the consumer's
+    backward applies the producer's ReLU mask / BN reduction, no act_bwd or reduce pass)
+    give the same
     gradients as the unlinked form, for plain ReLU (VGG-16 / AlexNet) and BN+ReLU
     (VGG11_bn) producers."""
     import mpi_pytorch_amd.models.layers as L
@@ -523,8 +524,12 @@ def test_feature_stack_links_match_unlinked():
         seq.train()
         return seq
 
+    from mpi_pytorch_amd.ops import ref
     x = torch.randn(2, 12, 12, 3)
     grads = []
+    pooled = []
+    real = ref.maxpool_bwd_relu
+    ref.maxpool_bwd_relu = lambda *t: pooled.append(1) or real(*t)
     for on in (True, False):
         old = L._LINK
         L._LINK = on
@@ -536,6 +541,9 @@ def test_feature_stack_links_match_unlinked():
             grads.append([p.grad.clone() for p in seq.parameters()])
         finally:
             L._LINK = old
+            ref.maxpool_bwd_relu = real if not on else ref.maxpool_bwd_relu
+    ref.maxpool_bwd_relu = real
+    assert pooled == [1]  # conv -> ReLU -> 2x2 pool: the pool's backward took the ReLU
     for a, b in zip(*grads):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (a - b).abs().max()
 
