@@ -592,17 +592,27 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const bf16_t* __restr
                                                            uint8_t* __restrict__ idx) {
   const int cv = C / 8;
   const int total = NP * Q * cv;  // (n, p) rows x Q x chunks (host: < 2^31)
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+  const size_t W2C = (size_t)2 * Q * C;
+  // thread item t -> the four 16-B input vectors of its window; the next item's loads are
+  // issued before this item's stores (loads and stores share the in-order vmcnt)
+  auto load = [&](int t, uint4 (&v)[4]) {
     const int cc = t % cv, r = t / cv;  // r = (n * P + p) * Q + q
     const int q = r % Q, np_ = r / Q;
     // input pixel (n, 2p + a, 2q + b) = row 2 * np_ + a of the [N * H] rows, width 2Q
-    const size_t row0 = (size_t)(2 * np_) * (2 * Q) + 2 * q;
-    const size_t W2C = (size_t)2 * Q * C;
-    uint4 v[4];
-    v[0] = *(const uint4*)(x + row0 * C + cc * 8);
-    v[1] = *(const uint4*)(x + (row0 + 1) * C + cc * 8);
-    v[2] = *(const uint4*)(x + row0 * C + W2C + cc * 8);
-    v[3] = *(const uint4*)(x + (row0 + 1) * C + W2C + cc * 8);
+    const size_t o = ((size_t)(2 * np_) * (2 * Q) + 2 * q) * C + cc * 8;
+    v[0] = *(const uint4*)(x + o);
+    v[1] = *(const uint4*)(x + o + C);
+    v[2] = *(const uint4*)(x + o + W2C);
+    v[3] = *(const uint4*)(x + o + W2C + C);
+  };
+  const int stride = gridDim.x * 256;
+  int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  uint4 v[4], vn[4];
+  load(t, v);
+  for (;;) {
+    const int tn = t + stride;
+    if (tn < total) load(tn, vn);
     float best[8], f[8];
     uint32_t bi[8];
     unpack8(v[0], best);
@@ -619,12 +629,16 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const bf16_t* __restr
           bi[j] = u;
         }
     }
-    const size_t o = (size_t)r * C + cc * 8;
+    const size_t o = (size_t)t * 8;  // == ((n * P + p) * Q + q) * C + cc * 8
     *(uint4*)(y + o) = pack8(best);
     uint2 ib;
     ib.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
     ib.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
     *(uint2*)(idx + o) = ib;
+    if (tn >= total) break;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = vn[u];
+    t = tn;
   }
 }
 
@@ -649,35 +663,42 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(
     }
     const int M = NP * Q;
     const size_t W2C = (size_t)2 * Q * C;
-    for (int r = blockIdx.x * cm.rpi + cm.r0; r < M; r += gridDim.x * cm.rpi) {
-      const size_t o = (size_t)r * C + c0;
-      const uint4 gv = *(const uint4*)(dy + o);
-      const uint2 iv = *(const uint2*)(idx + o);
-      float g[8];
-      unpack8(gv, g);
-      if constexpr (RELU) {
-        float yv[8];
-        unpack8(*(const uint4*)(yp + o), yv);
+    // v[0] dy, v[1] = (idx pair, -), v[2] pooled y; next row's loads before this row's stores
+    sweep_rows_pl<1, 3>(
+        cm, M,
+        [&](int r, uint4 (&v)[3]) {
+          const size_t o = (size_t)r * C + c0;
+          v[0] = *(const uint4*)(dy + o);
+          const uint2 iv = *(const uint2*)(idx + o);
+          v[1] = make_uint4(iv.x, iv.y, 0u, 0u);
+          if constexpr (RELU) v[2] = *(const uint4*)(yp + o);
+        },
+        [&](int r, uint4 (&v)[3]) {
+          float g[8];
+          unpack8(v[0], g);
+          if constexpr (RELU) {
+            float yv[8];
+            unpack8(v[2], yv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          g[j] = yv[j] > 0.f ? g[j] : 0.f;
-          sg[j] += g[j];
-        }
-      }
-      const int q = r % Q, np_ = r / Q;
-      const size_t row0 = (size_t)(2 * np_) * (2 * Q) + 2 * q;
+            for (int j = 0; j < 8; ++j) {
+              g[j] = yv[j] > 0.f ? g[j] : 0.f;
+              sg[j] += g[j];
+            }
+          }
+          const int q = r % Q, np_ = r / Q;
+          const size_t row0 = (size_t)(2 * np_) * (2 * Q) + 2 * q;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float d[8];
+          for (int u = 0; u < 4; ++u) {
+            float d[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t w = j < 4 ? iv.x : iv.y;
-          d[j] = ((w >> (8 * (j & 3))) & 0xff) == (uint32_t)u ? g[j] : 0.f;
-        }
-        bf16_t* p = dx + (row0 + (u & 1)) * C + (u >> 1) * W2C + c0;
-        *(uint4*)p = pack8(d);
-      }
-    }
+            for (int j = 0; j < 8; ++j) {
+              const uint32_t w = j < 4 ? v[1].x : v[1].y;
+              d[j] = ((w >> (8 * (j & 3))) & 0xff) == (uint32_t)u ? g[j] : 0.f;
+            }
+            bf16_t* p = dx + (row0 + (u & 1)) * C + (u >> 1) * W2C + c0;
+            *(uint4*)p = pack8(d);
+          }
+        });
   }
   if constexpr (RELU) {
     __shared__ float red[256 * 8];

@@ -603,6 +603,8 @@ struct StripPlan {
   uint32_t mag_tw, mag_p, mag_tc, mag_timg;  // floor(2^32 / d) + 1 (0: d == 1)
   int btoff[9];
   uint32_t a_bytes, b_bytes;
+  int ch, cw;               // tap-set centre shift: output (i, j) reads input rows / cols
+                            // i + ch - 1 .. i + ch + 1 (same conv 0, valid 1, its dgrad -1)
 };
 
 // n / d from udiv's magic, with magic 0 standing for d == 1 (floor(2^32 / 1) + 1 wraps)
@@ -625,9 +627,8 @@ __device__ __forceinline__ void strip_wait(int n) {
   }
 }
 
-template <bool WRES, int EPI, int NS>
+template <bool WRES, int EPI, int NS, int NJ>
 __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripPlan h) {
-  constexpr int NJ = 4;
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
   const int HBY = h.hiw * 4096;  // halo stage bytes (4 producer waves x hiw KiB)
   char* const hal = smem;
@@ -638,7 +639,8 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wave = wave_all & (HB_NW - 1);
-  const int H = p.aH, W = p.aW, HW = H * W, P = h.p, aC = p.aC;
+  const int H = p.aH, W = p.aW, P = h.p, aC = p.aC;  // input image
+  const int OH = p.oH, OW = p.oW;                      // output image (tiles)
   const int TR = h.tr, TW = h.tw;
   const int jq = lane >> 4, l15 = lane & 15;
 
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
         const int s = hsc[j] & 1023, col = (hsc[j] >> 10) & 1023;
-        const int ih = r0 - 1 + s, iw = c0 - 1 + col;
+        const int ih = r0 + h.ch - 1 + s, iw = c0 + h.cw - 1 + col;
         const bool ok = s < TR + 2 && col < TW + 2 && (unsigned)ih < (unsigned)H &&
                         (unsigned)iw < (unsigned)W;
         hv[j] = ok ? ((((uint32_t)img * H + ih) * W + iw) * aC) * 2 + (hsc[j] >> 20) * 16
@@ -783,8 +785,8 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int lr = lrc[i] >> 16, lc = lrc[i] & 0xffff;
-      mrow[i] = (lrc[i] >= 0 && r0 + lr < H && c0 + lc < W)
-                    ? (img * H + r0 + lr) * W + c0 + lc : -1;
+      mrow[i] = (lrc[i] >= 0 && r0 + lr < OH && c0 + lc < OW)
+                    ? (img * OH + r0 + lr) * OW + c0 + lc : -1;
     }
   };
   auto preload = [&]() {
@@ -1013,7 +1015,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 #pragma unroll
       for (int j = 0; j < HIW; ++j) {
         const int sl = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255);
-        const int ih = r0 - 1 + sl, iw = cs0 - 1 + col;
+        // (valid conv, pad 0: output (i, j) reads input rows i .. i + 2)
+        const int ih = r0 - p.ph + sl, iw = cs0 - p.pw + col;
         const bool ok = sl < h.tr + 2 && col < h.tw + 2 && (unsigned)ih < (unsigned)H &&
                         (unsigned)iw < (unsigned)W;
         hv[j] = ok ? ((((uint32_t)img * H + ih) * W + iw) * C + c0) * 2 + (hsc[j] >> 18) * 16
@@ -1023,8 +1026,8 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       for (int j = 0; j < 4; ++j) {
         const uint32_t row = 8 * (4 * wave + j) + (lane >> 3);
         const uint32_t lr = udiv1(row, h.mag_tw), lc = row - lr * h.tw;
-        const bool ok = (int)row < tpx && r0 + (int)lr < H && cs0 + (int)lc < W && kok[j];
-        dv[j] = ok ? drow[j] + (((uint32_t)img * H + r0 + lr) * W + cs0 + lc) * (uint32_t)K * 2
+        const bool ok = (int)row < tpx && r0 + (int)lr < p.P && cs0 + (int)lc < p.Q && kok[j];
+        dv[j] = ok ? drow[j] + (((uint32_t)img * p.P + r0 + lr) * p.Q + cs0 + lc) * (uint32_t)K * 2
                    : 0x80000000u;
       }
       return;
@@ -1224,13 +1227,36 @@ static int halo_epi(const IGemmArgs& a) {
 }
 
 // eligibility of the halo engine (either tiling); `linear`: the 256-pixel linear tiles fit
+// centre shift (ch, cw) of a 3x3 stride-1 tap set: the taps Oh + dh cover ch-1 .. ch+1 (same
+// conv 0; valid conv 1; the valid conv's dgrad, padding 2, -1) and the output is the input
+// less 2*ch rows / 2*cw columns
+static bool tap_shift(const IGemmArgs& a, int& ch, int& cw) {
+  int mh = 1 << 20, mw = 1 << 20;
+  for (int t = 0; t < 9; ++t) {
+    mh = std::min(mh, a.Oh + a.taps.dh[t]);
+    mw = std::min(mw, a.Ow + a.taps.dw[t]);
+  }
+  ch = mh + 1;
+  cw = mw + 1;
+  if (ch < -1 || ch > 1 || cw < -1 || cw > 1) return false;
+  int seen = 0;  // every relative (dh, dw) in {-1,0,1}^2 exactly once
+  for (int t = 0; t < 9; ++t) {
+    const int dh = a.Oh + a.taps.dh[t] - ch, dw = a.Ow + a.taps.dw[t] - cw;
+    if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return false;
+    seen |= 1 << ((dh + 1) * 3 + dw + 1);
+  }
+  return seen == 511 && a.oH == a.aH - 2 * ch && a.oW == a.aW - 2 * cw;
+}
+
 static bool halo_ok_impl(const IGemmArgs& a, bool& linear) {
   linear = false;
   if (!g_halo || a.nphase > 0 || a.stap || a.T != 9 || a.Uh != 1 || a.Uw != 1) return false;
-  if (a.oH != a.aH || a.oW != a.aW || a.aC % 32 != 0 || a.M <= 0) return false;
-  // 64-wide column tiles, or one 32-wide tile (DenseNet's growth-rate convs) in the
-  // flavours instantiated for it
-  if (a.N % HB_BN != 0 && !(a.N == 32 && (halo_epi(a) == 0 || halo_epi(a) == EP_STATS)))
+  if (a.aC % 32 != 0 || a.M <= 0 || a.oH <= 0 || a.oW <= 0) return false;
+  // 64-wide column tiles, or one 32-wide tile (DenseNet's growth-rate convs, Inception's
+  // Conv2d_2a) in the flavours instantiated for it (strip tiles: also accumulate / BN link)
+  const int e32 = halo_epi(a);
+  const bool n32_lin = a.N == 32 && (e32 == 0 || e32 == EP_STATS);
+  if (a.N % HB_BN != 0 && !(a.N == 32 && (n32_lin || e32 == EP_BETA || e32 == EP_BNRED)))
     return false;
   // dense [M][ldc] output (stride-1 geometry), 32-bit element offsets in the epilogue
   if (a.dH != a.oH || a.dW != a.oW || a.Uoh != 1 || a.Uow != 1 || a.Poh != 0 || a.Pow != 0)
@@ -1238,24 +1264,21 @@ static bool halo_ok_impl(const IGemmArgs& a, bool& linear) {
   if ((int64_t)a.M * a.ldc >= (1ll << 31) || a.ldc < a.N) return false;
   if (halo_epi(a) < 0) return false;  // an epilogue flavour without an instantiation
   if (a.Ktot != 9 * a.aC) return false;
-  int seen = 0;  // every (dh, dw) in {-1,0,1}^2 exactly once
-  for (int t = 0; t < 9; ++t) {
-    const int dh = a.Oh + a.taps.dh[t], dw = a.Ow + a.taps.dw[t];
-    if (dh < -1 || dh > 1 || dw < -1 || dw > 1) return false;
-    seen |= 1 << ((dh + 1) * 3 + dw + 1);
-  }
-  if (seen != 511) return false;
-  const int64_t HW = (int64_t)a.aH * a.aW;
-  if (a.M % HW != 0) return false;
-  if ((int64_t)a.M * a.aC * 2 >= (1ll << 31)) return false;
+  int ch, cw;
+  if (!tap_shift(a, ch, cw)) return false;
+  const int64_t HW = (int64_t)a.aH * a.aW, OHW = (int64_t)a.oH * a.oW;
+  if (a.M % OHW != 0) return false;
+  if ((int64_t)(a.M / OHW) * HW * a.aC * 2 >= (1ll << 31)) return false;
   if ((int64_t)a.N * a.ldb * 2 >= (1ll << 31)) return false;
-  if (HW + HB_BM >= 65536 || a.aW + 2 > 255) return true;  // (strip tiles only)
+  // (strip tiles only: shifted tap sets - valid convs and their dgrads - and wide images)
+  if (ch != 0 || cw != 0 || HW + HB_BM >= 65536 || a.aW + 2 > 255) return true;
   // halo slots of any 256-pixel tile: rows touched + 2 halo rows + image separators
   const int64_t rows = (HB_BM - 1 + a.aW - 1) / a.aW + 1;
   const int64_t seps = (HB_BM - 1) / HW + 1;
   // (+1: with P == W + 1 the last slot's right border is the next pixel)
   const int P = halo_pitch(a.aW);
-  linear = (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX;
+  linear = (rows + 2 + seps) * P + (P == a.aW + 1 ? 1 : 0) <= HB_HPX &&
+           (a.N % HB_BN == 0 || n32_lin);
   return true;
 }
 
@@ -1275,8 +1298,9 @@ static int g_strip = [] {
 void igemm_set_halo_strip(int mode) { g_strip = mode; }
 
 static bool strip_plan(const IGemmArgs& a, StripPlan& h, bool& wres, int& ns) {
-  const int W = a.aW, H = a.aH;
-  if (a.N % HB_BN != 0 || W < 8) return false;
+  const int W = a.oW, H = a.oH;  // tiles cover the output image
+  if ((a.N % HB_BN != 0 && a.N != 32) || W < 8) return false;
+  if (!tap_shift(a, h.ch, h.cw)) return false;
   const int nstrip = (W + 127) / 128;
   const int TW = (W + nstrip - 1) / nstrip;
   int TR = std::max(1, std::min(H, HB_BM / TW));
@@ -1291,7 +1315,7 @@ static bool strip_plan(const IGemmArgs& a, StripPlan& h, bool& wres, int& ns) {
   h.tiles_c = (W + TW - 1) / TW;
   h.tiles_img = ((H + TR - 1) / TR) * h.tiles_c;
   h.cc = a.aC / 32;
-  const int nimg = a.M / (H * W);
+  const int nimg = a.M / (H * W);  // (output pixels per image)
   wres = g_halo_wres && (a.N + HB_BN - 1) / HB_BN == 1 && h.cc <= 2;
   const int lds = 2 * HB_HBYTES + 2 * HB_WBYTES;
   ns = 2;
@@ -1305,15 +1329,15 @@ static bool strip_plan(const IGemmArgs& a, StripPlan& h, bool& wres, int& ns) {
   return (int64_t)nimg * h.tiles_img < (1 << 24);
 }
 
-template <int EPI>
+template <int EPI, int NJ = 4>
 static void launch_strip(bool wres, int ns, int grid, const IGemmArgs& a, const StripPlan& h,
                          hipStream_t s) {
   if (wres && ns == 3)
-    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 3>), dim3(grid), dim3(512), 0, s, a, h);
+    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 3, NJ>), dim3(grid), dim3(512), 0, s, a, h);
   else if (wres)
-    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 2>), dim3(grid), dim3(512), 0, s, a, h);
+    hipLaunchKernelGGL((conv3_strip_kernel<true, EPI, 2, NJ>), dim3(grid), dim3(512), 0, s, a, h);
   else
-    hipLaunchKernelGGL((conv3_strip_kernel<false, EPI, 2>), dim3(grid), dim3(512), 0, s, a, h);
+    hipLaunchKernelGGL((conv3_strip_kernel<false, EPI, 2, NJ>), dim3(grid), dim3(512), 0, s, a, h);
 }
 
 static int conv3_strip(IGemmArgs a, hipStream_t s) {
@@ -1322,16 +1346,25 @@ static int conv3_strip(IGemmArgs a, hipStream_t s) {
   int ns;
   strip_plan(a, h, wres, ns);
   for (int t = 0; t < 9; ++t) {
-    const int r = (a.Oh + a.taps.dh[t] + 1) * 3 + (a.Ow + a.taps.dw[t] + 1);
+    const int r = (a.Oh + a.taps.dh[t] - h.ch + 1) * 3 + (a.Ow + a.taps.dw[t] - h.cw + 1);
     h.btoff[r] = a.taps.bt[t] * a.aC * 2;
   }
-  h.a_bytes = (uint32_t)((int64_t)a.M * a.aC * 2);
+  h.a_bytes = (uint32_t)((int64_t)(a.M / ((int64_t)a.oH * a.oW)) * a.aH * a.aW * a.aC * 2);
   h.b_bytes = (uint32_t)((int64_t)a.N * a.ldb * 2);
   a.tiles_n = (a.N + HB_BN - 1) / HB_BN;
   a.tiles_total = h.tiles_total;
   int g8 = std::min(std::min(active_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
+  if (a.N == 32) {  // one 32-wide column tile (NJ = 2)
+    switch (halo_epi(a)) {
+      case 0: launch_strip<0, 2>(wres, ns, grid, a, h, s); break;
+      case EP_STATS: launch_strip<EP_STATS, 2>(wres, ns, grid, a, h, s); break;
+      case EP_BETA: launch_strip<EP_BETA, 2>(wres, ns, grid, a, h, s); break;
+      default: launch_strip<EP_BNRED, 2>(wres, ns, grid, a, h, s); break;
+    }
+    return grid;
+  }
   switch (halo_epi(a)) {
     case 0: launch_strip<0>(wres, ns, grid, a, h, s); break;
     case EP_BETA: launch_strip<EP_BETA>(wres, ns, grid, a, h, s); break;
@@ -1462,31 +1495,35 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
 static int halo_wgrad_pitch(int W) { return (W + 2 + 15) / 16 * 16; }
 
 // shape checks shared by the linear and strip tilings
+// (pad 1: same conv; pad 0: valid conv, strip tiles only - its dy is the smaller image)
 static bool halo_wgrad_base(const WGradArgs& a) {
-  if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1)
-    return false;
+  if (!g_halo || a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1) return false;
+  if (a.ph < 0 || a.ph > 1 || a.pw < 0 || a.pw > 1) return false;
+  if (a.P != a.H + 2 * a.ph - 2 || a.Q != a.W + 2 * a.pw - 2 || a.P <= 0 || a.Q <= 0) return false;
   // 64 x 64 partitions; a 32-wide remainder in either dimension is zero-filled
-  if (a.P != a.H || a.Q != a.W || a.C % 32 != 0 || a.Kout % 32 != 0) return false;
-  const int64_t HW = (int64_t)a.H * a.W;
-  if (a.Mpix % HW != 0) return false;
-  return (int64_t)a.Mpix * a.C * 2 < (1ll << 31) && (int64_t)a.Mpix * a.Kout * 2 < (1ll << 31);
+  if (a.C % 32 != 0 || a.Kout % 32 != 0) return false;
+  const int64_t PQ = (int64_t)a.P * a.Q;
+  if (a.Mpix % PQ != 0) return false;
+  const int64_t nimg = a.Mpix / PQ;
+  return nimg * a.H * a.W * a.C * 2 < (1ll << 31) && (int64_t)a.Mpix * a.Kout * 2 < (1ll << 31);
 }
 
 // strip tiling of the weight gradient (images too wide for the linear tiles): the TR x TW
 // tile (TR * TW <= 128 pixels) minimising tiles x (128 MFMA rows + staged halo pixels)
 static bool halo_wgrad_strip_plan(const WGradArgs& a, HaloWPlan& h) {
   if (g_strip < 1 || !halo_wgrad_base(a)) return false;
-  const int64_t nimg = a.Mpix / ((int64_t)a.H * a.W);
+  const int OH = a.P, OW = a.Q;  // tiles cover dy (the conv output)
+  const int64_t nimg = a.Mpix / ((int64_t)OH * OW);
   int64_t best = -1;
-  for (int n = 1; n <= a.W; ++n) {
-    const int tw = (a.W + n - 1) / n;
-    if (tw > 126 || (n > 1 && (a.W + tw - 1) / tw != n)) continue;
+  for (int n = 1; n <= OW; ++n) {
+    const int tw = (OW + n - 1) / n;
+    if (tw > 126 || (n > 1 && (OW + tw - 1) / tw != n)) continue;
     if (tw < 8) break;
     const int pitch = (tw + 2 + 15) / 16 * 16;
-    int tr = std::max(1, std::min(a.H, HW_BM / tw));
+    int tr = std::max(1, std::min(OH, HW_BM / tw));
     while (tr > 1 && (tr + 2) * pitch > HW_HPX) --tr;
     if ((tr + 2) * pitch > HW_HPX) continue;
-    const int64_t tiles = nimg * ((a.H + tr - 1) / tr) * n;
+    const int64_t tiles = nimg * ((OH + tr - 1) / tr) * n;
     const int64_t cost = tiles * (HW_BM + (tr + 2) * pitch);
     if (best < 0 || cost < best) {
       best = cost;
@@ -1494,7 +1531,7 @@ static bool halo_wgrad_strip_plan(const WGradArgs& a, HaloWPlan& h) {
       h.tw = tw;
       h.w2 = pitch;
       h.tiles_c = n;
-      h.tiles_img = ((a.H + tr - 1) / tr) * n;
+      h.tiles_img = ((OH + tr - 1) / tr) * n;
       h.tiles_m = (int)tiles;
     }
   }
@@ -1506,7 +1543,7 @@ static bool halo_wgrad_strip_plan(const WGradArgs& a, HaloWPlan& h) {
 }
 
 static bool halo_wgrad_geom(const WGradArgs& a) {
-  if (!halo_wgrad_base(a)) return false;
+  if (!halo_wgrad_base(a) || a.ph != 1 || a.pw != 1) return false;
   const int64_t HW = (int64_t)a.H * a.W;
   if (HW + HW_BM >= 65536 || a.W + 2 > 255) return false;
   const int64_t rows = (HW_BM - 1 + a.W - 1) / a.W + 1;
@@ -1548,7 +1585,7 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
     const int G = std::min(active_cus(), HALO_MAX_ROWS);
     h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
     h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
-    h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
+    h.x_bytes = (uint32_t)((int64_t)(a.Mpix / ((int64_t)a.P * a.Q)) * a.H * a.W * a.C * 2);
     hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, false, true>), dim3(h.parts * h.Z), dim3(256),
                        0, s, a, h);
     return h.Z;

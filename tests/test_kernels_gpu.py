@@ -414,6 +414,70 @@ def test_conv_halo_strip(gpu, case):
         C().igemm_set_halo(0)
 
 
+@pytest.mark.parametrize("case", [(2, 37, 41, 32, 32), (1, 149, 149, 32, 32),
+                                  (2, 20, 70, 64, 64), (2, 30, 30, 64, 32)])
+def test_conv_halo_strip_valid(gpu, case):
+    """Unpadded ("valid") 3x3 convs on the strip-tiled halo kernels (Inception's
+    Conv2d_2a): the shifted tap set in the forward (output 2 smaller), its dgrad (padding
+    2, output 2 larger: plain, accumulating, fused BN reduction) and the weight gradient ==
+    implicit GEMM and the oracle; 32-wide outputs run the NJ = 2 form."""
+    torch.manual_seed(26)
+    N, H, W, Cc, K = case
+    P, Q = H - 2, W - 2
+    C().igemm_set_halo_strip(1)
+    try:
+        x = bf(N, H, W, Cc, dev=gpu)
+        w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * Cc))
+        e = torch.empty(0, device=gpu)
+        shift = torch.randn(K, device=gpu) * 0.1
+
+        def run():
+            st = torch.zeros(2, K, device=gpu)
+            return C().conv_fwd(x, w, e, 1, 1, 0, 0, False, st, shift), st
+
+        (y, st), (y0, st0) = _halo_pair(run)
+        str_ = torch.zeros(2, K, device=gpu)
+        yr = ref.conv_fwd(x, w, e, 1, 1, 0, 0, False, str_, shift)
+        assert y.shape == (N, P, Q, K)
+        assert rel(y, y0) < 1e-2 and rel(y, yr) < 2e-2
+        assert rel(st, st0) < 1e-3 and rel(st, str_) < 2e-2
+        dy = bf(N, P, Q, K, dev=gpu)
+        wt = w.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+        dx, dx0 = _halo_pair(lambda: C().conv_dgrad(dy, w, H, W, 1, 1, 0, 0, wt))
+        dxr = ref.conv_dgrad(dy, w, H, W, 1, 1, 0, 0)
+        assert rel(dx, dx0) < 1e-2 and rel(dx, dxr) < 2e-2
+        acc0 = bf(N, H, W, Cc, dev=gpu)
+        acc, _ = _halo_pair(lambda: C().conv_dgrad(dy, w, H, W, 1, 1, 0, 0, wt, acc0.clone()))
+        assert rel(acc, acc0.float() + dxr.float()) < 2e-2
+        z = bf(N, H, W, Cc, dev=gpu, scale=2.0)
+        mean = torch.randn(Cc, device=gpu) * 0.3
+        rstd = torch.rand(Cc, device=gpu) + 0.5
+        gamma = torch.rand(Cc, device=gpu) + 0.5
+        beta = torch.randn(Cc, device=gpu) * 0.2
+        sc = gamma * rstd
+        yz = torch.relu(z.float() * sc + (beta - mean * sc)).to(torch.bfloat16)
+        (g, sums), (g0, sums0) = _halo_pair(
+            lambda: C().conv_dgrad_bnred(dy, w, H, W, 1, 1, 0, 0, wt, z, yz, mean, rstd,
+                                         gamma=gamma, beta=beta))
+        gr, sr = ref.conv_dgrad_bnred(dy, w, H, W, 1, 1, 0, 0, None, z, None, mean, rstd,
+                                      gamma, beta)
+        assert rel(g, g0) < 1e-2 and rel(sums, sums0) < 1e-2
+        assert rel(g, gr) < 2e-2 and rel(sums, sr) < 2e-2
+        dw0 = torch.randn(K, 3, 3, Cc, device=gpu)
+
+        def wg():
+            dw = dw0.clone()
+            C().conv_wgrad(dy, x, dw, 1, 1, 0, 0)
+            return dw
+
+        dw, dwi = _halo_pair(wg)
+        dwr = dw0.clone()
+        ref.conv_wgrad(dy, x, dwr, 1, 1, 0, 0)
+        assert rel(dw - dw0, dwi - dw0) < 1e-2 and rel(dw - dw0, dwr - dw0) < 2e-2
+    finally:
+        C().igemm_set_halo(0)
+
+
 @pytest.mark.parametrize("case", HALO_CASES)
 def test_conv_halo_wgrad(gpu, case):
     """Halo-staged 3x3/s1 weight gradient (slab partials + reduce, accumulating into dw)
