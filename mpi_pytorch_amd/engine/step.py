@@ -276,7 +276,12 @@ class TrainStep:
         if m is not None:
             m.range_pop()
             m.range_push("bwd")
-        loss.backward(self._one)
+        # (single GPU: conv weight gradients may run on a side stream, joined right after)
+        Fn.wgrad_stream_begin(self.bucketer is None or not self.bucketer.active)
+        try:
+            loss.backward(self._one)
+        finally:
+            Fn.join_wgrad_stream()
         if t is not None:
             t.mark(2)
         if m is not None:

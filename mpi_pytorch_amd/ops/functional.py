@@ -84,6 +84,50 @@ def _done(*ps) -> None:
             grad_done(p)
 
 
+# ================================================================ weight-gradient stream
+# MPA_WGRAD_STREAM=1: inside TrainStep's eager backward (single GPU), the conv weight
+# gradients run on a second HIP stream.  A weight gradient reads only its op's dz and x and
+# writes only the gradient arena, so it need not sit between the dgrad / BN-backward
+# launches of the main chain: the memory-bound BN passes (no LDS, or 8 KiB) can run on the
+# CUs beside a persistent MFMA-bound wgrad grid.  The step joins the stream before the
+# optimizer (join_wgrad_stream); x / dz are record_stream'ed so the caching allocator does
+# not hand their memory out while the side stream still reads it.
+_WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "0") == "1"
+_SIDE = {"stream": None, "on": False, "used": False}
+
+
+def wgrad_stream_begin(enabled: bool = True) -> None:
+    """Route the following conv weight gradients to the side stream (TrainStep backward)."""
+    _SIDE["on"] = bool(enabled and _WGRAD_STREAM)
+
+
+def join_wgrad_stream() -> None:
+    """Make the current stream wait for every side-stream weight gradient; route off."""
+    _SIDE["on"] = False
+    if _SIDE["used"]:
+        torch.cuda.current_stream().wait_stream(_SIDE["stream"])
+        _SIDE["used"] = False
+
+
+def _run_wgrad(fn, *tensors) -> None:
+    """Run ``fn`` (a weight-gradient launch and its arena notifications) on the side stream
+    when routing is on, else in place."""
+    t0 = tensors[0]
+    if not (_SIDE["on"] and t0.is_cuda) or torch.cuda.is_current_stream_capturing():
+        fn()
+        return
+    main = torch.cuda.current_stream(t0.device)
+    side = _SIDE["stream"]
+    if side is None or side.device != t0.device:
+        side = _SIDE["stream"] = torch.cuda.Stream(t0.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    for t in tensors:
+        t.record_stream(side)
+    _SIDE["used"] = True
+
+
 # =============================================================================== conv+BN
 class BNLink:
     """Backward hand-off between two fused conv+BN ops when the first op's output feeds ONLY
@@ -354,9 +398,11 @@ class _ConvBNAct(torch.autograd.Function):
             _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
-            conv.fix_grad(w.grad)
-            _done(w)
+            def wgrad():
+                k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
+                conv.fix_grad(w.grad)
+                _done(w)
+            _run_wgrad(wgrad, dz, x)
         _done(ctx.bias)
         if dres_pair is not None:
             dres = dres_pair  # d/dz of the deferred BN's producer (see BNDefer.done)
@@ -695,9 +741,11 @@ class _ConvAct(torch.autograd.Function):
         _done(b)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
-            conv.fix_grad(w.grad)
-            _done(w)
+            def wgrad():
+                k.conv_wgrad(g, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
+                conv.fix_grad(w.grad)
+                _done(w)
+            _run_wgrad(wgrad, g, x)
         dx = None
         if ctx.needs_input_grad[0]:
             li = ctx.link_in

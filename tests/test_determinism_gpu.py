@@ -79,6 +79,33 @@ def test_graph_replays_bitwise_equal_eager(det):
     assert torch.equal(model._mpa_arena.master, ref_master)
 
 
+@pytest.mark.parametrize("name,hw", [("resnet18", 64), ("vgg16", 64)])
+def test_wgrad_side_stream_bitwise(det, name, hw):
+    """Conv weight gradients on the side stream (MPA_WGRAD_STREAM, joined before the
+    optimizer) == all on one stream, bitwise, over 3 steps (losses, weights, Adam state)."""
+    gpu = det
+    import mpi_pytorch_amd.ops.functional as Fn
+    x, y = _batch(gpu, hw=hw)
+    outs = []
+    old = Fn._WGRAD_STREAM
+    try:
+        for on in (True, False):
+            Fn._WGRAD_STREAM = on
+            model, opt, step = _train(gpu, name=name)
+            losses = [step(x, y).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            if on:
+                assert Fn._SIDE["stream"] is not None
+            a = model._mpa_arena
+            outs.append((torch.stack(losses).cpu(), a.master.cpu().clone(),
+                         opt.exp_avg_sq.cpu().clone()))
+            del model, opt, step
+    finally:
+        Fn._WGRAD_STREAM = old
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+
+
 def test_early_head_update_bitwise(det):
     """The classifier's optimizer update issued on a side stream as soon as its gradients
     are final (TrainStep._early_head) == the whole update after backward, bitwise; also
