@@ -106,6 +106,10 @@ struct IGemmArgs {
   const bf16_raw* A2;
   const bf16_raw* B2;
   int ldb2;
+  // kpad (uniform-tap LDS-DMA kernel, K-contiguous B): aC is 16-B but not 32-granular
+  // (Inception's 48 / 80 channels): every tap's K is padded to a multiple of 32, Ktot =
+  // T * round32(aC), and the chunks past aC read zeros
+  int kpad;
 };
 constexpr short TAP_SRC2 = 0x2000;
 

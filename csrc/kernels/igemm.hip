@@ -833,6 +833,11 @@ static void tuned_rows_tile(const IGemmArgs& a, bool bkc, int vw, bool allow_spl
   tbn = bbn;
 }
 
+static const bool g_kpad = [] {
+  const char* e = getenv("MPA_KPAD");
+  return !(e && e[0] == '0');
+}();
+
 static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipStream_t s) {
   const bool dma = use_dma(vw);
   if (dma && bkc && conv_stem_ok(a)) {  // 7x7 pixel-pair stem: row-staged direct conv
@@ -851,6 +856,14 @@ static void run_rows(IGemmArgs a, bool bkc, int vw, float* ws, float* slab, hipS
     const int rows = conv3_halo(a, s);
     if (stats) slab_stats(slab, rows, a.N, a.stats_shift, a.M, sums, stats, s, a.stats_ld);
     return;
+  }
+  // 16-B but not 32-granular channel counts (Inception 48 / 80): the uniform-tap kernel
+  // with each tap's K padded to 32 (MPA_KPAD=0: the generic gather kernel); no split-K (the
+  // caller's workspace was sized for the unpadded K)
+  if (dma && g_kpad && igemm_rows_kpad_ok(a, bkc)) {
+    a.Ktot = a.T * ((a.aC + BK - 1) / BK) * BK;
+    a.kpad = 1;
+    ws = nullptr;
   }
   int tbm = 0, tbn = 0;
   if (dma) tuned_rows_tile(a, bkc, vw, ws != nullptr, s, tbm, tbn);
@@ -875,6 +888,9 @@ static void rows_run_plan(IGemmArgs a, bool bkc, int vw, float* ws, float* slab,
   }
   if (dma && igemm_rows_dma(a, BM, BN, bkc, splits, s)) {
     // LDS-DMA engine (igemm_dma.hip)
+  } else if (a.kpad) {  // (unreachable: every planned tile has a kernel)
+    fprintf(stderr, "rows_run_plan: padded-K launch without an LDS-DMA kernel\n");
+    abort();
   } else if (bkc) {
     if (BN == 128) dispatch_split<128, 128, 2, 2, true>(a, vw, splits, s);
     else if (BN == 64) dispatch_split<256, 64, 4, 1, true>(a, vw, splits, s);

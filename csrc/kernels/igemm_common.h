@@ -438,6 +438,7 @@ __device__ __forceinline__ void wgrad_epilogue(const WGradArgs& p,
 // required).  Return false when no instantiation covers the tile shape.
 bool igemm_rows_dma(const IGemmArgs& a, int BM, int BN, bool bkc, int splits, hipStream_t s);
 bool igemm_rows_uni_src2_ok(const IGemmArgs& a, bool bkc);
+bool igemm_rows_kpad_ok(const IGemmArgs& a, bool bkc);
 bool igemm_wgrad_dma(const WGradArgs& a, int BM, int BN, int splits, hipStream_t s);
 bool igemm_wgrad_inc_ok(const WGradArgs& a);  // incremental-pixel wgrad kernel applies
 

@@ -331,8 +331,9 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
   const __amdgpu_buffer_rsrc_t rb2 = make_rsrc(PH && p.B2 ? p.B2 : p.B, 0x7fffffffu);
   const uint32_t s32 = lds_base(smem);
   const int kch = kc_lane_chunk(lane);
-  // K elements per tap-table entry: aC, or 32 for super-taps (4 kernel columns x 8 ch)
-  const int kpt = p.stap ? BK : aC;
+  // K elements per tap-table entry: aC, or 32 for super-taps (4 kernel columns x 8 ch), or
+  // aC rounded up to 32 (kpad: the chunks past aC read zeros on both operands)
+  const int kpt = p.stap ? BK : (p.kpad ? (aC + BK - 1) / BK * BK : aC);
   // ---- A rows (rows past M clamp to M-1: their outputs are discarded)
   uint32_t a_off[IAW];
   int a_bh[IAW], a_bw[IAW];
@@ -375,16 +376,17 @@ void igemm_rows_dma_uni_kernel(IGemmArgs p) {
     const bool x2 = PH && BKC && braw < 0;  // wave-uniform: a second-source tap
     const __amdgpu_buffer_rsrc_t rA = x2 ? ra2 : ra;
     const __amdgpu_buffer_rsrc_t rB = x2 ? rb2 : rb;
+    const bool cok = !p.kpad || c_s + kch * 8 < aC;  // (kpad: this lane's chunk exists)
 #pragma unroll
     for (int i = 0; i < IAW; ++i) {
       const bool ok = ((unsigned)(a_bh[i] + dh) < (unsigned)p.aH) &
-                      ((unsigned)(a_bw[i] + dw) < (unsigned)p.aW);
+                      ((unsigned)(a_bw[i] + dw) < (unsigned)p.aW) & cok;
       buf_lds16_at(rA, st + (wave * IAW + i) * 1024, ok ? a_off[i] + toff : 0x80000000u);
     }
     const uint32_t bst = st + A_BYTES;
     const int boff = (braw & 0x7fffffff) + (BKC ? c_s * 2 : c_s * p.RS * p.ldb * 2);
     // super-tap: chunks past the kernel's last column read zeros (ns valid columns)
-    const bool bok = !p.stap || kch < (__builtin_amdgcn_readfirstlane(tap_b[t_s]) >> 12);
+    const bool bok = (!p.stap || kch < (__builtin_amdgcn_readfirstlane(tap_b[t_s]) >> 12)) & cok;
 #pragma unroll
     for (int i = 0; i < IBW; ++i) {
       const int jb = wave + NW * i;
@@ -765,6 +767,12 @@ static bool rows_uni_fits(const IGemmArgs& a, bool bkc) {
 
 // a second GEMM source is read only by the uniform-tap kernel's phase form with K-contiguous
 // B (launch_rows_dma_v picks that kernel under exactly these conditions)
+// kpad form available: the uniform-tap kernel with K-contiguous B takes the launch
+bool igemm_rows_kpad_ok(const IGemmArgs& a, bool bkc) {
+  return bkc && g_dma_uni && !a.stap && a.nphase == 0 && a.aC % BK != 0 && a.aC % 8 == 0 &&
+         rows_uni_fits(a, bkc);
+}
+
 bool igemm_rows_uni_src2_ok(const IGemmArgs& a, bool bkc) {
   return bkc && a.nphase > 0 && a.aC % BK == 0 && !a.stap && g_dma_uni && rows_uni_fits(a, bkc);
 }
@@ -773,7 +781,7 @@ template <int BM, int BN, int WM, int WN, bool BKC, bool SPLIT, bool PH>
 static void launch_rows_dma_v(const IGemmArgs& a0, dim3 grid, hipStream_t s) {
   IGemmArgs a = a0;
   igemm_set_fastdiv(a);
-  if ((a.aC % BK == 0 || a.stap) && g_dma_uni && rows_uni_fits(a, BKC))
+  if ((a.aC % BK == 0 || a.stap || (a.kpad && BKC)) && g_dma_uni && rows_uni_fits(a, BKC))
     hipLaunchKernelGGL((igemm_rows_dma_uni_kernel<BM, BN, WM, WN, BKC, SPLIT, PH>), grid,
                        dim3(WM * WN * 64), 0, s, a);
   else

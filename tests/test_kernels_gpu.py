@@ -43,6 +43,8 @@ CONV_CASES = [
     (2, 32, 32, 8, 64, 7, 7, 2, 3),        # padded stem (C=8: 16-B granular, DMA path)
     (4, 28, 28, 128, 128, 3, 3, 1, 1),     # 128x128 tile, several K-tiles
     (8, 40, 40, 3, 5, 3, 3, 1, 1),         # split wgrad, Kout*R*S*C % 4 != 0 (scalar reduce)
+    (2, 17, 17, 48, 64, 5, 5, 1, 2),       # Inception 5x5_2: C = 48, padded-K uniform taps
+    (2, 15, 13, 80, 192, 3, 3, 1, 0),      # Inception Conv2d_4a: C = 80, valid 3x3
 ]
 
 
