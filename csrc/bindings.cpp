@@ -320,6 +320,53 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t sh, int64_t
   return conv_dgrad_impl(dy, w, H, W, sh, sw, ph, pw, wt_opt, nullptr, accum);
 }
 
+// stride-1 dgrad plus a residual block's shortcut gradient dy_res * (y > 0) (y's ReLU bit
+// mask from bn_fwd_train) added in the halo kernel's epilogue: the masked shortcut gradient
+// is never written.  None when the launch would not run on the halo kernel.
+c10::optional<Tensor> conv_dgrad_res(Tensor dy, Tensor w, Tensor wt, int64_t H, int64_t W,
+                                     int64_t ph, int64_t pw, Tensor res, Tensor rmask) {
+  CHECK_ACT(dy);
+  CHECK_ACT(w);
+  CHECK_ACT(res);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  const int R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(w.size(0) == K, "conv_dgrad_res: channel mismatch");
+  TORCH_CHECK(res.dim() == 4 && res.size(0) == N && res.size(1) == H && res.size(2) == W &&
+                  res.size(3) == C,
+              "conv_dgrad_res: the residual gradient must have dx's shape");
+  TORCH_CHECK(rmask.scalar_type() == torch::kUInt8 && rmask.is_contiguous() &&
+                  rmask.numel() == res.numel() / 8 && rmask.device() == res.device(),
+              "conv_dgrad_res: ReLU mask must be contiguous uint8 [numel / 8]");
+  if (!(wt.defined() && wt.numel() == w.numel()) || vec_width(K) != 8 || vec_width(C) != 8 ||
+      mpa::igemm_engine() < 1)
+    return c10::nullopt;
+  if (P != H + 2 * ph - R + 1 || Q != W + 2 * pw - S + 1) return c10::nullopt;
+  const c10::OptionalDeviceGuard g(device_of(dy));
+  Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
+  mpa::IGemmArgs a{};
+  a.A = bp(dy); a.aH = P; a.aW = Q; a.aC = K;
+  a.Uh = 1; a.Uw = 1; a.Oh = 0; a.Ow = 0;
+  a.B = bp(wt); a.N = C; a.RS = R * S; a.ldb = R * S * K; a.b_tapmap = 1;
+  a.C = dx.data_ptr(); a.ldc = C;
+  a.dH = H; a.dW = W; a.Uoh = 1; a.Uow = 1;
+  a.beta = 1;
+  a.ep_res = bp(res);
+  a.ep_rmask = rmask.data_ptr<uint8_t>();
+  int T = 0;
+  for (int r = 0; r < R; ++r)
+    for (int s = 0; s < S; ++s) {
+      a.taps.dh[T] = ph - r;
+      a.taps.dw[T] = pw - s;
+      a.taps.bt[T] = r * S + s;
+      ++T;
+    }
+  a.T = T;
+  a.M = N * H * W; a.oH = H; a.oW = W; a.Ktot = T * K; a.Poh = 0; a.Pow = 0;
+  if (!mpa::conv3_halo_ok(a)) return c10::nullopt;
+  mpa::igemm_rows_dgrad(a, 8, nullptr, cur_stream(), true);
+  return dx;
+}
+
 // dx of two convs that read the same input with the same stride (a residual stage's 3x3/s2
 // conv1 and its 1x1/s2 shortcut) in ONE merged stride-phase launch: the shortcut's taps
 // are extra K of the phases they hit, so dx is written once, with no accumulate pass.
@@ -1575,6 +1622,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred_gacc", &conv_dgrad_bnred_gacc);
+  m.def("conv_dgrad_res", &conv_dgrad_res);
   m.def("conv_dgrad_pair", &conv_dgrad_pair, py::arg("dy"), py::arg("w"), py::arg("wt"),
         py::arg("H"), py::arg("W"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dy2"), py::arg("w2"), py::arg("wt2"), py::arg("ph2"), py::arg("pw2"),

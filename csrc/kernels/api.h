@@ -110,6 +110,12 @@ struct IGemmArgs {
   // (Inception's 48 / 80 channels): every tap's K is padded to a multiple of 32, Ktot =
   // T * round32(aC), and the chunks past aC read zeros
   int kpad;
+  // accumulate (beta = 1) from ep_res instead of the old C, masked by the ReLU bit mask
+  // ep_rmask (bit e % 8 of byte e / 8 for element e): a residual block's shortcut gradient
+  // dy * (y > 0) added in the conv1 dgrad epilogue without being written first (halo
+  // kernels only; dense [M][N] rows)
+  const bf16_raw* ep_res;
+  const uint8_t* ep_rmask;
 };
 constexpr short TAP_SRC2 = 0x2000;
 

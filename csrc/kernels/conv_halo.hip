@@ -80,6 +80,19 @@ struct EpiIn {
   uint2 a[4][4];
 };
 
+// the accumulate operand of element e: the old output, or the masked residual gradient
+// (IGemmArgs::ep_res / ep_rmask; 4 consecutive channels = 4 bits of one mask byte)
+__device__ __forceinline__ uint2 acc_operand(const IGemmArgs& p, uint32_t e) {
+  if (!p.ep_res) return *(const uint2*)((const bf16_t*)p.C + e);
+  uint2 v = *(const uint2*)((const bf16_t*)p.ep_res + e);
+  if (p.ep_rmask) {
+    const uint32_t nib = ((uint32_t)p.ep_rmask[e >> 3] >> (e & 7)) & 15u;
+    v.x &= ((nib & 1u) ? 0xffffu : 0u) | ((nib & 2u) ? 0xffff0000u : 0u);
+    v.y &= ((nib & 4u) ? 0xffffu : 0u) | ((nib & 8u) ? 0xffff0000u : 0u);
+  }
+  return v;
+}
+
 template <int EPI, int NJ>
 __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m0, int n0,
                                             int wave, int lane) {
@@ -99,7 +112,7 @@ __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m
         if constexpr (EPI & EP_BNRED) {
           in.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
         } else {
-          in.a[i][jn] = *(const uint2*)((const bf16_t*)p.C + orow + jn * 16);
+          in.a[i][jn] = acc_operand(p, orow + jn * 16);
         }
       }
     }
@@ -797,7 +810,7 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
 #pragma unroll
         for (int jn = 0; jn < NJ; ++jn) {
           if constexpr (EPI & EP_BNRED) ein.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
-          else ein.a[i][jn] = *(const uint2*)((const bf16_t*)p.C + orow + jn * 16);
+          else ein.a[i][jn] = acc_operand(p, orow + jn * 16);
         }
       }
     } else {

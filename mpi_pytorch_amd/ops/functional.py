@@ -237,13 +237,42 @@ def _dgrad_pair(k, a, b, in_hw):
                              ph2, pw2)
 
 
-def _join_grad(join: Optional[GradJoin], t: Optional[torch.Tensor]):
-    """Offer a computed contribution ``t`` to ``join``; returns what the op hands back to
-    autograd (the sum if it is the last contribution, else None)."""
+class _MaskedRes:
+    """A residual block's shortcut gradient dy * (y > 0) not yet written: the block input's
+    other consumer (conv1's stride-1 dgrad) adds it in its epilogue (``conv_dgrad_res``), or
+    it is materialised when that is not available."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy, mask):
+        self.dy = dy
+        self.mask = mask
+
+    def materialize(self, k):
+        if not self.dy.is_cuda:
+            return (self.dy.float() * ref.bitmask_unpack(self.mask, self.dy.shape)).to(
+                self.dy.dtype)
+        bits = (self.mask.unsqueeze(-1) >> torch.arange(8, device=self.mask.device,
+                                                         dtype=torch.uint8)) & 1
+        return self.dy * bits.reshape(self.dy.shape).to(self.dy.dtype)
+
+
+# MPA_RES_MASK=0: a residual block writes its shortcut gradient dy * mask for conv1's dgrad to
+# accumulate, instead of conv1's dgrad epilogue reading dy and the bit mask itself
+_RES_MASK = os.environ.get("MPA_RES_MASK", "1") == "1"
+
+
+def _join_grad(join: Optional[GradJoin], t):
+    """Offer a computed contribution ``t`` (a tensor or a _MaskedRes) to ``join``; returns
+    what the op hands back to autograd (the sum if it is the last contribution, else None)."""
     if join is None or t is None:
         return t
     last = join.arrive()
     prev = join.take()
+    if isinstance(t, _MaskedRes) and (last or prev is not None):
+        t = t.materialize(None)
+    if isinstance(prev, _MaskedRes):
+        prev = prev.materialize(None)
     if prev is None:
         acc = t
     elif isinstance(prev, _Deferred):
@@ -277,6 +306,18 @@ def _dgrad_joined(k, join: Optional[GradJoin], dz, w, in_hw, conv, wt):
     prev = join.take()
     full = _dgrad_full(conv, in_hw)
     args = (dz, w, wt, conv)
+    if isinstance(prev, _MaskedRes):
+        acc = None
+        sh, sw, ph, pw = conv.kgeom
+        if sh == 1 and sw == 1 and hasattr(k, "conv_dgrad_res") and (wt is not None
+                                                                    or not dz.is_cuda):
+            acc = k.conv_dgrad_res(dz, w, wt, in_hw[0], in_hw[1], ph, pw, prev.dy, prev.mask)
+        if acc is None:
+            acc = run(prev.materialize(k))
+        if last:
+            return acc
+        join.partial = acc
+        return None
     if prev is None:
         if last:
             return run(None)
@@ -392,8 +433,14 @@ class _ConvBNAct(torch.autograd.Function):
             dz, g = k.bn_bwd(dy, z, _empty(dy), mean, rstd, gamma, _sink(gamma, dy),
                              _sink(beta, dy), True, want_g, beta)
         else:
+            # identity shortcut: conv1's dgrad adds dy * mask in its epilogue (_MaskedRes), so
+            # g is not written here
+            mres = (want_g and _RES_MASK and ymask is not None and ctx.join_res is not None
+                    and ctx.join_res.arrived == 0 and ctx.join_res.partial is None)
             dz, g = k.bn_bwd(dy, z, _or_empty(y, dy), mean, rstd, gamma, _sink(gamma, dy),
-                             _sink(beta, dy), True, want_g, ymask=ymask)
+                             _sink(beta, dy), True, want_g and not mres, ymask=ymask)
+            if mres:
+                g = _MaskedRes(dy, ymask)
         if ctx.defer is None or dz is not dy:
             _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom

@@ -77,6 +77,14 @@ def conv_dgrad(dy, w, H, W, sh, sw, ph, pw, wt=None, accum=None):
     return _nhwc(gi).to(dy.dtype)
 
 
+def conv_dgrad_res(dy, w, wt, H, W, ph, pw, res, rmask):
+    """Stride-1 dgrad + the residual gradient res * (y > 0) (y's ReLU bit mask), summed in
+    fp32 and rounded once."""
+    d = _f(conv_dgrad(dy, w, H, W, 1, 1, ph, pw))
+    g = _f(res) * bitmask_unpack(rmask, res.shape)
+    return (d + g).to(dy.dtype)
+
+
 def conv_dgrad_pair(dy, w, wt, H, W, sh, sw, ph, pw, dy2, w2, wt2, ph2, pw2, accum=None):
     """dx of two convs reading the same input with the same stride (3x3/s2 conv1 + its
     1x1/s2 shortcut), summed in fp32 and rounded once; None if the grids differ."""

@@ -17,6 +17,7 @@ b inc_nostrip MPA_HALO_STRIP=0 python bench.py --model inception --image-size 29
 b vgg16 python bench.py --model vgg16 --batch 256 --steps 10 --warmup 3 --small-batch 0
 b head python bench.py --steps 20 --warmup 5 --small-batch 0
 b wgs MPA_WGRAD_STREAM=1 python bench.py --steps 20 --warmup 5 --small-batch 0
+b nores MPA_RES_MASK=0 python bench.py --steps 20 --warmup 5 --small-batch 0
 b head2 python bench.py --steps 20 --warmup 5 --small-batch 0
 b wgs2 MPA_WGRAD_STREAM=1 python bench.py --steps 20 --warmup 5 --small-batch 0
 b vgg16_wgs MPA_WGRAD_STREAM=1 python bench.py --model vgg16 --batch 256 --steps 10 --warmup 3 --small-batch 0

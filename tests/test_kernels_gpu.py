@@ -194,6 +194,34 @@ def test_conv_dgrad_pair(gpu, case):
     assert torch.equal(dx[:, 1::2], one[:, 1::2]) and torch.equal(dx[:, :, 1::2], one[:, :, 1::2])
 
 
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 64), (4, 56, 56, 64, 64), (2, 28, 28, 128, 128),
+                                  (1, 112, 112, 64, 64)])
+def test_conv_dgrad_masked_residual(gpu, case):
+    """conv1's stride-1 halo dgrad + the identity shortcut's gradient dy_res * (y > 0) read
+    in the epilogue (conv_dgrad_res: the masked residual is never written) == the oracle,
+    and == the written-then-accumulated form bit for bit (same single rounding)."""
+    torch.manual_seed(13)
+    N, H, W, Cc, K = case
+    dy = bf(N, H, W, K, dev=gpu)
+    w = bf(K, 3, 3, Cc, dev=gpu, scale=1.0 / math.sqrt(9 * K))
+    wt = w.permute(3, 1, 2, 0).reshape(Cc, 9, K).contiguous()
+    res = bf(N, H, W, Cc, dev=gpu)
+    yv = bf(N, H, W, Cc, dev=gpu)
+    mask = ref.relu_bitmask(yv)
+    C().igemm_set_halo(1)
+    try:
+        dx = C().conv_dgrad_res(dy, w, wt, H, W, 1, 1, res, mask)
+        assert dx is not None
+        g = (res.float() * (yv.float() > 0)).to(torch.bfloat16)
+        two = C().conv_dgrad(dy, w, H, W, 1, 1, 1, 1, wt, g.clone())
+        torch.cuda.synchronize()
+    finally:
+        C().igemm_set_halo(0)
+    exp = ref.conv_dgrad_res(dy, w, wt, H, W, 1, 1, res, mask)
+    assert rel(dx, exp) < 2e-2
+    assert torch.equal(dx, two)
+
+
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 3, 1, 1), (2, 14, 14, 64, 128, 3, 3, 2, 1),
                                   (4, 28, 28, 128, 128, 3, 3, 1, 1), (3, 9, 11, 96, 48, 3, 3, 1, 1)])
 def test_conv_dgrad_fused_bn_reduction(gpu, case):

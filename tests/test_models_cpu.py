@@ -477,6 +477,31 @@ def test_resnet_dgrad_pair_equals_two_dgrads(monkeypatch):
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
 
 
+def test_resnet_masked_shortcut_gradient_equals_written(monkeypatch):
+    """Identity blocks hand their shortcut gradient to conv1's dgrad unwritten (_MaskedRes:
+    conv_dgrad_res adds dy * mask in its epilogue; 5 per ResNet-18 step) == bn2's backward
+    writing g and conv1's dgrad accumulating into it (fp32, CPU)."""
+    from mpi_pytorch_amd.ops import functional as Fn
+    from mpi_pytorch_amd.ops import ref
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("resnet18", 10, torch.device("cpu"), World(), 1e-3)
+    a = model._mpa_arena
+    x = torch.randn(2, 64, 64, 3)
+    y = torch.randint(0, 10, (2,))
+    calls = []
+    real = ref.conv_dgrad_res
+    monkeypatch.setattr(ref, "conv_dgrad_res", lambda *t: calls.append(1) or real(*t))
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(Fn, "_RES_MASK", on)
+        a.zero_grad()
+        loss_fn(model(x), y).backward()
+        grads.append(a.grad.clone())
+    assert len(calls) == 5
+    g1, g2 = grads
+    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
+
+
 def test_resnet_bn_pair_backward_equals_separate(monkeypatch):
     """bn2 + the deferred downsample BN backwarded together (bn_bwd_pair: one reduce and
     one apply pass, g never written; 3 per ResNet-18 step) == bn2's backward handing g to
