@@ -82,6 +82,11 @@ def parse_args(argv=None):
     p.add_argument("--optimizer", default="adam")
     p.add_argument("--lr", type=float, default=4e-4)
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"])
+    # A/B switches usable under rocprofv3 (which must exec bench.py directly, no env wrapper)
+    p.add_argument("--res-mask", type=int, default=None, choices=[0, 1],
+                   help="identity shortcut gradient read by conv1's dgrad (MPA_RES_MASK)")
+    p.add_argument("--wgrad-stream", type=int, default=None, choices=[0, 1],
+                   help="conv weight gradients on a side stream (MPA_WGRAD_STREAM)")
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--comm-dtype", default="fp32")
     p.add_argument("--comm-ctas", type=int, default=None,
@@ -441,6 +446,11 @@ def main(argv=None):
     args = parse_args(argv)
     if args.gpus > 1 and not _launcher_env():
         sys.exit(spawn(argv, args.gpus))
+    from mpi_pytorch_amd.ops import functional as Fn
+    if args.res_mask is not None:
+        Fn._RES_MASK = bool(args.res_mask)
+    if args.wgrad_stream is not None:
+        Fn._WGRAD_STREAM = bool(args.wgrad_stream)
     run(args)
 
 

@@ -80,9 +80,7 @@ def _tapped_groups(name: str, fs, rec: Dict):
     mods = list(fs._modules.values())
 
     def run_group(g, x, link_in=None, link_out=None):
-        # (the BN / ReLU backward hand-offs between groups are kept: a unit's recorded
-        # output gradient is then its consumer's masked dgrad, the same gradient after
-        # the unit's own ReLU)
+        # (unit_parity runs the stacks unlinked: no hand-offs between groups)
         i0, i1, kind = g
         if not any(p.requires_grad for mm in mods[i0:i1] for p in mm.parameters()):
             return cls_run(fs, g, x, link_in=link_in, link_out=link_out)
@@ -174,6 +172,14 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
     grouped = [m for m in model_gpu.modules() if hasattr(m, "heads")]
     for m in grouped:
         m.merge_1x1 = False
+    # backward hand-offs BETWEEN units (conv -> ReLU -> conv / pool links of the VGG / AlexNet
+    # stacks, Inception's chained BasicConv2d links): the consumer's dgrad would apply the
+    # producer's ReLU mask, so its recorded input gradient is not the unit's own dx.  Units
+    # run unlinked here; the links have tests of their own (test_models_cpu.py
+    # test_feature_stack_links_match_unlinked, the model parity / learning tests).
+    from ..models import layers as _L, inception as _I
+    links = (_L._LINK, _I._LINK)
+    _L._LINK = _I._LINK = False
     try:
         arena = model_gpu._mpa_arena
         arena.zero_grad()
@@ -194,6 +200,7 @@ def unit_parity(model_gpu: nn.Module, model_cpu: nn.Module, x: torch.Tensor, y: 
             model_gpu.fuse_stem_pools = pools
         for m in grouped:
             m.__dict__.pop("merge_1x1", None)
+        _L._LINK, _I._LINK = links
     g_gpu = arena.grad.detach().cpu()
     out = []
     plain = {name: m for name, m in units}
