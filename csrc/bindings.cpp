@@ -341,6 +341,7 @@ c10::optional<Tensor> conv_dgrad_res(Tensor dy, Tensor w, Tensor wt, int64_t H, 
       mpa::igemm_engine() < 1)
     return c10::nullopt;
   if (P != H + 2 * ph - R + 1 || Q != W + 2 * pw - S + 1) return c10::nullopt;
+  if (C % 64 != 0) return c10::nullopt;  // (a column tile's 64 mask bits: one aligned 8-B load)
   const c10::OptionalDeviceGuard g(device_of(dy));
   Tensor dx = empty_like_shape(dy, {N, H, W, C}, torch::kBFloat16);
   mpa::IGemmArgs a{};

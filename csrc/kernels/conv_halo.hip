@@ -78,18 +78,27 @@ enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16 
 // registers long before the epilogue runs.
 struct EpiIn {
   uint2 a[4][4];
+  uint2 mk[4];  // (accumulate from ep_res) row i's 64 ReLU mask bits of the column tile
 };
 
-// the accumulate operand of element e: the old output, or the masked residual gradient
-// (IGemmArgs::ep_res / ep_rmask; 4 consecutive channels = 4 bits of one mask byte)
+// the accumulate operand of element e: the old output, or the residual gradient ep_res
+// (its ReLU mask is applied at the epilogue, see masked_acc: applying it here would make the
+// MFMA waves wait for the mask load at preload time)
 __device__ __forceinline__ uint2 acc_operand(const IGemmArgs& p, uint32_t e) {
-  if (!p.ep_res) return *(const uint2*)((const bf16_t*)p.C + e);
-  uint2 v = *(const uint2*)((const bf16_t*)p.ep_res + e);
-  if (p.ep_rmask) {
-    const uint32_t nib = ((uint32_t)p.ep_rmask[e >> 3] >> (e & 7)) & 15u;
-    v.x &= ((nib & 1u) ? 0xffffu : 0u) | ((nib & 2u) ? 0xffff0000u : 0u);
-    v.y &= ((nib & 4u) ? 0xffffu : 0u) | ((nib & 8u) ? 0xffff0000u : 0u);
-  }
+  return *(const uint2*)((const bf16_t*)(p.ep_res ? p.ep_res : p.C) + e);
+}
+
+// row i's 64 mask bits of the block's column tile (row element e0 = m * ldc + n0, n0 % 64 == 0)
+__device__ __forceinline__ uint2 acc_mask(const IGemmArgs& p, uint32_t e0) {
+  return p.ep_rmask ? *(const uint2*)(p.ep_rmask + (e0 >> 3)) : make_uint2(~0u, ~0u);
+}
+
+// fragment (jn, jq)'s 4 channels 16 jn + 4 jq .. +3 of the preloaded operand, masked
+__device__ __forceinline__ uint2 masked_acc(uint2 v, uint2 mk, int jn, int jq) {
+  const uint32_t word = jn < 2 ? mk.x : mk.y;
+  const uint32_t nib = (word >> ((16 * jn + 4 * jq) & 31)) & 15u;
+  v.x &= ((nib & 1u) ? 0xffffu : 0u) | ((nib & 2u) ? 0xffff0000u : 0u);
+  v.y &= ((nib & 4u) ? 0xffffu : 0u) | ((nib & 8u) ? 0xffff0000u : 0u);
   return v;
 }
 
@@ -107,6 +116,7 @@ __device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m
     for (int i = 0; i < 4; ++i) {
       const int m = min(m0 + wave * 64 + i * 16 + (lane & 15), p.M - 1);  // rows >= M: unused
       const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
+      if constexpr (!(EPI & EP_BNRED)) in.mk[i] = acc_mask(p, (uint32_t)m * p.ldc + n0);
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) {
         if constexpr (EPI & EP_BNRED) {
@@ -430,7 +440,11 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       colb = *(const f32x4*)(cst + c);
       cols = *(const f32x4*)(cst + HB_BN + c);
     }
-    epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh, es[jn],
+    uint2 av = ein.a[i][jn];
+    if constexpr ((EPI & EP_BETA) != 0) {
+      if (p.ep_rmask) av = masked_acc(av, ein.mk[i], jn, jq);
+    }
+    epi_frag<EPI, F>(p, acc[i][jn], av, m < p.M, jn, orow, colb, cols, mc, mh, es[jn],
                      eq[jn]);
   };
   // Epilogue of a whole tile (see TRED)
@@ -807,6 +821,8 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t orow = (uint32_t)max(mrow[i], 0) * p.ldc + n0 + jq * 4;
+        if constexpr (!(EPI & EP_BNRED))
+          ein.mk[i] = acc_mask(p, (uint32_t)max(mrow[i], 0) * p.ldc + n0);
 #pragma unroll
         for (int jn = 0; jn < NJ; ++jn) {
           if constexpr (EPI & EP_BNRED) ein.a[i][jn] = *(const uint2*)(p.ep_z + orow + jn * 16);
@@ -864,7 +880,11 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
           const f32x4 cols = *(const f32x4*)(cst + HB_BN + c);
           const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
           const uint32_t orow = (uint32_t)max(mrow[i], 0) * p.ldc + n0 + jq * 4;
-          epi_frag<EPI, false>(p, acc[i][jn], ein.a[i][jn], mrow[i] >= 0, jn, orow, colb, cols,
+          uint2 av = ein.a[i][jn];
+          if constexpr ((EPI & EP_BETA) != 0) {
+            if (p.ep_rmask) av = masked_acc(av, ein.mk[i], jn, jq);
+          }
+          epi_frag<EPI, false>(p, acc[i][jn], av, mrow[i] >= 0, jn, orow, colb, cols,
                                z4, z4, ss[jn], sq[jn]);
         }
     }
