@@ -79,13 +79,14 @@ def test_graph_replays_bitwise_equal_eager(det):
     assert torch.equal(model._mpa_arena.master, ref_master)
 
 
-@pytest.mark.parametrize("name,hw", [("resnet18", 64), ("vgg16", 64)])
+@pytest.mark.parametrize("name,hw", [("resnet18", 64), ("vgg16", 64), ("densenet", 64),
+                                     ("inception", 299)])
 def test_wgrad_side_stream_bitwise(det, name, hw):
     """Conv weight gradients on the side stream (MPA_WGRAD_STREAM, joined before the
     optimizer) == all on one stream, bitwise, over 3 steps (losses, weights, Adam state)."""
     gpu = det
     import mpi_pytorch_amd.ops.functional as Fn
-    x, y = _batch(gpu, hw=hw)
+    x, y = _batch(gpu, B=8 if hw > 200 else 32, hw=hw)
     outs = []
     old = Fn._WGRAD_STREAM
     try:
