@@ -589,10 +589,12 @@ class _ConvGroupBNAct(torch.autograd.Function):
             _done(gamma, beta)
         ws = [m.conv.weight for m in ctx.mods]
         if ws[0].requires_grad:
-            fresh = [_fresh(w) for w in ws]  # (every flag consumed)
-            G = ws[0]._mpa_arena.flat_view(ws, "grad").view(ctx.W.shape)
-            k.conv_wgrad(dz, x, G, 1, 1, 0, 0, overwrite=all(fresh))
-            _done(*ws)
+            def wgrad():
+                fresh = [_fresh(w) for w in ws]  # (every flag consumed)
+                G = ws[0]._mpa_arena.flat_view(ws, "grad").view(ctx.W.shape)
+                k.conv_wgrad(dz, x, G, 1, 1, 0, 0, overwrite=all(fresh))
+                _done(*ws)
+            _run_wgrad(wgrad, dz, x)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _dgrad_joined(k, ctx.join, dz, ctx.W, ctx.in_hw, ctx.mods[0].conv, None)
@@ -696,9 +698,11 @@ class _ConvBNReLUPool(torch.autograd.Function):
                               _sink(beta, dy), *ctx.cfg[:6], zsel=zsel)
         _done(gamma, beta)
         if w.requires_grad:
-            k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
-            conv.fix_grad(w.grad)
-            _done(w)
+            def wgrad():
+                k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
+                conv.fix_grad(w.grad)
+                _done(w)
+            _run_wgrad(wgrad, dz, x)
         _done(ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -15,3 +15,5 @@ b r34 python bench.py --model resnet34 --batch 512 --steps 10 --warmup 3 --small
 b vgg11bn python bench.py --model vgg --batch 256 --steps 10 --warmup 3 --small-batch 0
 b alexnet python bench.py --model alexnet --batch 256 --steps 10 --warmup 3 --small-batch 0
 b squeeze python bench.py --model squeezenet --batch 256 --steps 10 --warmup 3 --small-batch 0
+timeout -k 10 120 python tools/adam_probe.py > $O/c12_adam.txt 2>&1 || { tail -5 $O/c12_adam.txt; exit 1; }
+cat $O/c12_adam.txt
