@@ -197,7 +197,10 @@ def run_training(cfg: Config) -> dict:
         log.info("_Checkpoint loaded")
     from ..parallel import sync_params
     sync_params(model)
-    log.info("_Model loaded to {}".format("GPU" if dev.type == "cuda" else "CPU"))
+    # the reference's exact string (main.py:133 logs "CPU" whatever the device); the
+    # actual compute device goes on a line of its own
+    log.info("_Model loaded to CPU")
+    log.info("_Compute device: %s", dev)
     log.info("_Entering training Loop")
 
     if cfg.step_timers:
