@@ -269,19 +269,30 @@ class TrainStep:
         self.arena.zero_grad()
         if self._head is not None:
             self._head_left = len(self._head[1])
-        out = self.model(x)
-        loss = loss_fn(out, y, acc=self.loss_sum)
+        # (single GPU: an Inception block's longest branch chain may run on a second
+        # stream, forward and backward; joined after the backward)
+        single = self.bucketer is None or not self.bucketer.active
+        Fn.branch_streams(single)
+        try:
+            out = self.model(x)
+            loss = loss_fn(out, y, acc=self.loss_sum)
+        except BaseException:
+            Fn.branch_streams(False)
+            raise
         if t is not None:
             t.mark(1)
         if m is not None:
             m.range_pop()
             m.range_push("bwd")
         # (single GPU: conv weight gradients may run on a side stream, joined right after)
-        Fn.wgrad_stream_begin(self.bucketer is None or not self.bucketer.active)
+        Fn.wgrad_stream_begin(single)
         try:
             loss.backward(self._one)
         finally:
             Fn.join_wgrad_stream()
+            if Fn._BR["on"]:
+                Fn.branch_streams(False)
+                Fn.join_branch_stream()
         if t is not None:
             t.mark(2)
         if m is not None:

@@ -123,6 +123,32 @@ def _out(cb):
     return cb if cb is not None else _NoBuffer
 
 
+class _SideBranch:
+    """One branch chain of a block enqueued on the branch stream (Fn.branch_stream) while
+    the block's other branches go to the compute stream; ``join`` before the block output
+    is used.  Only with a ChannelBuffer (the chain writes its window) and for chains whose
+    input is a grouped-head output, so the chain's input gradient goes to
+    _ConvGroupBNAct.backward (which marks it used on the compute stream)."""
+
+    def __init__(self, x, cb):
+        self.s = Fn.branch_stream(x) if isinstance(cb, Fn.ChannelBuffer) else None
+        if self.s is not None:
+            self.main = torch.cuda.current_stream(x.device)
+            self.s.wait_stream(self.main)
+            x.record_stream(self.s)
+            cb.buf.record_stream(self.s)
+
+    def run(self, fn):
+        if self.s is None:
+            return fn()
+        with torch.cuda.stream(self.s):
+            return fn()
+
+    def join(self):
+        if self.s is not None:
+            self.main.wait_stream(self.s)
+
+
 def _half(n: int) -> int:
     return (n - 3) // 2 + 1  # 3x3 / stride 2 / no padding
 
@@ -165,16 +191,24 @@ class InceptionA(nn.Module):
     def forward(self, x, join=None):
         cb = _out(_buffer(self, x, x.shape[1:3],
                           [64, 64, 96, self.branch_pool.conv.out_channels]))
+        side = None
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
             b1, b5, b3, bp = Fn.conv1x1_group(x, self.heads(), join,
                                               [cb.window(0), None, None, cb.window(3)])
+            side = _SideBranch(b3, cb)
         else:
             j = _join(self, x, 4, join)
             b1 = self.branch1x1(x, j, out=cb.window(0))
             b5, b3 = self.branch5x5_1(x, j), self.branch3x3dbl_1(x, j)
             bp = self.branch_pool(x, j, out=cb.window(3))
+        chain = [self.branch3x3dbl_2, self.branch3x3dbl_3]
+        if side is not None:
+            b3 = side.run(lambda: _chain(self, chain, b3, cb.window(2)))
         b5 = self.branch5x5_2(b5, out=cb.window(1))
-        b3 = _chain(self, [self.branch3x3dbl_2, self.branch3x3dbl_3], b3, cb.window(2))
+        if side is not None:
+            side.join()
+        else:
+            b3 = _chain(self, chain, b3, cb.window(2))
         return cb.gather([b1, b5, b3, bp])
 
 
@@ -216,17 +250,25 @@ class InceptionC(nn.Module):
 
     def forward(self, x, join=None):
         cb = _out(_buffer(self, x, x.shape[1:3], [192, 192, 192, 192]))
+        side = None
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
             b1, b7, bd, bp = Fn.conv1x1_group(x, self.heads(), join,
                                               [cb.window(0), None, None, cb.window(3)])
+            side = _SideBranch(bd, cb)
         else:
             j = _join(self, x, 4, join)
             b1 = self.branch1x1(x, j, out=cb.window(0))
             b7, bd = self.branch7x7_1(x, j), self.branch7x7dbl_1(x, j)
             bp = self.branch_pool(x, j, out=cb.window(3))
+        dbl = [self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
+               self.branch7x7dbl_5]
+        if side is not None:  # the 4-conv chain beside the 2-conv one
+            bd = side.run(lambda: _chain(self, dbl, bd, cb.window(2)))
         b7 = _chain(self, [self.branch7x7_2, self.branch7x7_3], b7, cb.window(1))
-        bd = _chain(self, [self.branch7x7dbl_2, self.branch7x7dbl_3, self.branch7x7dbl_4,
-                           self.branch7x7dbl_5], bd, cb.window(2))
+        if side is not None:
+            side.join()
+        else:
+            bd = _chain(self, dbl, bd, cb.window(2))
         return cb.gather([b1, b7, bd, bp])
 
 
@@ -245,7 +287,8 @@ class InceptionD(nn.Module):
 
     def forward(self, x, join=None):
         # (a join handed in by the parent counts this block's consumers: see Inception3)
-        if _heads(self, x, self.heads()):
+        grouped = _heads(self, x, self.heads())
+        if grouped:
             j = _join(self, x, 2, join)
             b3, b7 = Fn.conv1x1_group(x, self.heads(), j)
         else:
@@ -253,10 +296,17 @@ class InceptionD(nn.Module):
             b3, b7 = self.branch3x3_1(x, j), self.branch7x7x3_1(x, j)
         cb = _out(_buffer(self, x, (_half(x.shape[1]), _half(x.shape[2])),
                           [320, 192, x.shape[-1]]))
+        side = _SideBranch(b7, cb) if grouped else None
+        chain = [self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4]
+        if side is not None:  # the 3-conv chain beside the 3x3/s2 conv and the pool
+            b7 = side.run(lambda: _chain(self, chain, b7, cb.window(1)))
         b3 = self.branch3x3_2(b3, out=cb.window(0))
-        b7 = _chain(self, [self.branch7x7x3_2, self.branch7x7x3_3, self.branch7x7x3_4], b7,
-                    cb.window(1))
-        return cb.gather([b3, b7, _max3s2(x, j)])
+        if side is None:
+            b7 = _chain(self, chain, b7, cb.window(1))
+        mp = _max3s2(x, j)
+        if side is not None:
+            side.join()
+        return cb.gather([b3, b7, mp])
 
 
 class InceptionE(nn.Module):
@@ -279,21 +329,32 @@ class InceptionE(nn.Module):
         # torchvision: cat([b1, cat([2a, 2b]), cat([3a, 3b]), bp]) - the same channel order
         # as one flat buffer of six windows
         cb = _out(_buffer(self, x, x.shape[1:3], [320, 384, 384, 384, 384, 192]))
+        side = None
         if _heads(self, x, self.heads()):  # every consumer of x in one grouped GEMM
             b1, b3, bd, bp = Fn.conv1x1_group(x, self.heads(), join,
                                               [cb.window(0), None, None, cb.window(5)])
+            side = _SideBranch(bd, cb)
         else:
             j = _join(self, x, 4, join)
             b1 = self.branch1x1(x, j, out=cb.window(0))
             b3, bd = self.branch3x3_1(x, j), self.branch3x3dbl_1(x, j)
             bp = self.branch_pool(x, j, out=cb.window(5))
+
+        def dbl(bd):  # 3x3 conv, then its (1x3) and (3x1) heads (all on one stream)
+            bd = self.branch3x3dbl_2(bd)
+            jd = _join(self, bd, 2)
+            return (self.branch3x3dbl_3a(bd, jd, out=cb.window(3)),
+                    self.branch3x3dbl_3b(bd, jd, out=cb.window(4)))
+
+        if side is not None:
+            bda, bdb = side.run(lambda: dbl(bd))
         j3 = _join(self, b3, 2)  # b3 and bd each feed a (1x3) and a (3x1) conv
         b3a = self.branch3x3_2a(b3, j3, out=cb.window(1))
         b3b = self.branch3x3_2b(b3, j3, out=cb.window(2))
-        bd = self.branch3x3dbl_2(bd)
-        jd = _join(self, bd, 2)
-        bda = self.branch3x3dbl_3a(bd, jd, out=cb.window(3))
-        bdb = self.branch3x3dbl_3b(bd, jd, out=cb.window(4))
+        if side is not None:
+            side.join()
+        else:
+            bda, bdb = dbl(bd)
         return cb.gather([b1, b3a, b3b, bda, bdb, bp])
 
 

@@ -129,6 +129,53 @@ def _run_wgrad(fn, *tensors) -> None:
     _SIDE["used"] = True
 
 
+# ================================================================== branch stream (Inception)
+# Inside TrainStep's step (single GPU, eager), an Inception block's longest branch chain is
+# enqueued on a second stream and the block's other branches on the compute stream, joined
+# before the block output is used (models/inception.py SideBranch).  Autograd runs each
+# node's backward on the stream of its forward, so the chains' backwards overlap too.
+# Every tensor that crosses between the streams is record_stream'ed on its consumer (the
+# chain input and block buffer at the fork, the block-output gradient in
+# _ChannelBuffer.backward, the chain-input gradient in _ConvGroupBNAct.backward), so the
+# caching allocator never hands out memory the other stream still reads.
+_BRANCH_STREAM = os.environ.get("MPA_BRANCH_STREAM", "1") == "1"
+_BR = {"stream": None, "on": False}
+
+
+def branch_streams(enabled: bool) -> None:
+    """Allow (TrainStep forward + backward) or stop side-branch streams."""
+    _BR["on"] = bool(enabled and _BRANCH_STREAM)
+
+
+def branch_stream(x: torch.Tensor):
+    """The stream a side branch reading ``x`` runs on, or None (off, CPU, no grad, or a
+    HIP-graph capture)."""
+    if not (_BR["on"] and x.is_cuda and torch.is_grad_enabled()):
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    s = _BR["stream"]
+    if s is None or s.device != x.device:
+        s = _BR["stream"] = torch.cuda.Stream(x.device)
+    return s
+
+
+def join_branch_stream() -> None:
+    """The compute stream waits for everything enqueued on the branch stream."""
+    s = _BR["stream"]
+    if s is not None and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
+def _branch_use(*ts) -> None:
+    """Mark tensors that may come from the other stream as used by the current one."""
+    if _BR["on"] and _BR["stream"] is not None:
+        cur = torch.cuda.current_stream(_BR["stream"].device)
+        for t in ts:
+            if t is not None and t.is_cuda:
+                t.record_stream(cur)
+
+
 # =============================================================================== conv+BN
 class BNLink:
     """Backward hand-off between two fused conv+BN ops when the first op's output feeds ONLY
@@ -574,6 +621,7 @@ class _ConvGroupBNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *dys):
         x, z = ctx.saved_tensors
+        _branch_use(*dys)  # (a member's gradient may come from a side-branch chain)
         k = K(z)
         dz = torch.empty_like(z)
         for m, (mean, rstd, o, n, zp, pool), dy in zip(ctx.mods, ctx.saved, dys):
@@ -1074,6 +1122,9 @@ class _ChannelBuffer(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        s = _BR["stream"] if _BR["on"] else None
+        if s is not None and dy.is_cuda:
+            dy.record_stream(s)  # (a window may be read by a side-branch chain)
         outs, o = [], 0
         for n in ctx.sizes:
             outs.append(dy[..., o:o + n])

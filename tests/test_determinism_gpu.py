@@ -110,6 +110,36 @@ def test_wgrad_side_stream_bitwise(det, name, hw):
         assert torch.equal(u, v)
 
 
+def test_branch_stream_bitwise(det):
+    """Inception side-branch chains on the branch stream (MPA_BRANCH_STREAM: forward and,
+    through autograd, backward) == every branch on one stream, bitwise, over 3 steps."""
+    gpu = det
+    import mpi_pytorch_amd.ops.functional as Fn
+    x, y = _batch(gpu, B=8, hw=299)
+    outs = []
+    old = Fn._BRANCH_STREAM
+    try:
+        for on in (True, False):
+            Fn._BRANCH_STREAM = on
+            Fn._BR["stream"] = None
+            model, opt, step = _train(gpu, name="inception")
+            for mod in model.modules():
+                if type(mod).__name__ == "Dropout":
+                    mod.p = 0.0
+            losses = [step(x, y).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            assert (Fn._BR["stream"] is not None) == on
+            a = model._mpa_arena
+            outs.append((torch.stack(losses).cpu(), a.master.cpu().clone(),
+                         opt.exp_avg_sq.cpu().clone(),
+                         torch.cat([b.float().flatten().cpu() for b in model.buffers()])))
+            del model, opt, step
+    finally:
+        Fn._BRANCH_STREAM = old
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+
+
 def test_early_head_update_bitwise(det):
     """The classifier's optimizer update issued on a side stream as soon as its gradients
     are final (TrainStep._early_head) == the whole update after backward, bitwise; also

@@ -15,7 +15,7 @@ CATS = [
     ("optimizer", r"adam_kernel|sgd_kernel|transpose_krsc|zero_f32|step_inc"),
     ("conv wgrad", r"wgrad|splitk_finalize"),
     ("conv (stem)", r"conv_stem"),
-    ("conv fwd/dgrad (halo)", r"conv3_halo_kernel"),
+    ("conv fwd/dgrad (halo)", r"conv3_halo_kernel|conv3_strip_kernel"),
     ("conv/GEMM fwd/dgrad (igemm)", r"igemm_rows|igemm_kernel|igemm_dma|gemm"),
     ("conv1 dgrad + norm1 bwd (dense_gacc)", r"dense_gacc"),
     ("BN backward", r"bn_bwd|maxpool_bn_bwd|slab_reduce|act_bwd|bn_defer"),
