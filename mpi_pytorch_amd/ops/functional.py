@@ -95,6 +95,15 @@ def _done(*ps) -> None:
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
 _SIDE = {"stream": None, "on": False, "used": False}
+# MPA_GRAPH_STREAMS=0: a HIP-graph capture keeps every launch on the capture stream.  With
+# it on (default) the side / branch streams fork from and join the captured stream, and the
+# graph keeps that concurrency (the allocator defers reuse of record_stream'ed blocks
+# until the capture ends).
+_GRAPH_STREAMS = os.environ.get("MPA_GRAPH_STREAMS", "1") == "1"
+
+
+def _capture_blocks_streams() -> bool:
+    return not _GRAPH_STREAMS and torch.cuda.is_current_stream_capturing()
 
 
 def wgrad_stream_begin(enabled: bool = True) -> None:
@@ -114,7 +123,7 @@ def _run_wgrad(fn, *tensors) -> None:
     """Run ``fn`` (a weight-gradient launch and its arena notifications) on the side stream
     when routing is on, else in place."""
     t0 = tensors[0]
-    if not (_SIDE["on"] and t0.is_cuda) or torch.cuda.is_current_stream_capturing():
+    if not (_SIDE["on"] and t0.is_cuda) or _capture_blocks_streams():
         fn()
         return
     main = torch.cuda.current_stream(t0.device)
@@ -139,7 +148,7 @@ def _run_wgrad(fn, *tensors) -> None:
 # _ChannelBuffer.backward, the chain-input gradient in _ConvGroupBNAct.backward), so the
 # caching allocator never hands out memory the other stream still reads.
 _BRANCH_STREAM = os.environ.get("MPA_BRANCH_STREAM", "1") == "1"
-_BR = {"stream": None, "on": False}
+_BR = {"stream": None, "on": False, "used": False}
 
 
 def branch_streams(enabled: bool) -> None:
@@ -149,22 +158,24 @@ def branch_streams(enabled: bool) -> None:
 
 def branch_stream(x: torch.Tensor):
     """The stream a side branch reading ``x`` runs on, or None (off, CPU, no grad, or a
-    HIP-graph capture)."""
+    HIP-graph capture with MPA_GRAPH_STREAMS=0)."""
     if not (_BR["on"] and x.is_cuda and torch.is_grad_enabled()):
         return None
-    if torch.cuda.is_current_stream_capturing():
+    if _capture_blocks_streams():
         return None
     s = _BR["stream"]
     if s is None or s.device != x.device:
         s = _BR["stream"] = torch.cuda.Stream(x.device)
+    _BR["used"] = True
     return s
 
 
 def join_branch_stream() -> None:
     """The compute stream waits for everything enqueued on the branch stream."""
     s = _BR["stream"]
-    if s is not None and not torch.cuda.is_current_stream_capturing():
+    if s is not None and _BR["used"]:
         torch.cuda.current_stream(s.device).wait_stream(s)
+    _BR["used"] = False
 
 
 def _branch_use(*ts) -> None:

@@ -207,7 +207,8 @@ def test_dropout_graph_replays_draw_fresh_masks(gpu):
     assert not torch.equal(a, b)
 
 
-@pytest.mark.parametrize("name,hw,B", [("alexnet", 64, 16), ("inception", 299, 4)])
+@pytest.mark.parametrize("name,hw,B", [("alexnet", 64, 16), ("inception", 299, 4),
+                                       ("densenet", 64, 8)])
 def test_dropout_models_graph_replays_bitwise_equal_eager(det, name, hw, B):
     """Models with dropout (torchvision classifiers of AlexNet / Inception,
     ``/root/reference/models.py:50,87``): replays of a captured step equal eager steps
