@@ -95,11 +95,13 @@ def _done(*ps) -> None:
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
 _SIDE = {"stream": None, "on": False, "used": False}
-# MPA_GRAPH_STREAMS=0: a HIP-graph capture keeps every launch on the capture stream.  With
-# it on (default) the side / branch streams fork from and join the captured stream, and the
-# graph keeps that concurrency (the allocator defers reuse of record_stream'ed blocks
-# until the capture ends).
-_GRAPH_STREAMS = os.environ.get("MPA_GRAPH_STREAMS", "1") == "1"
+# MPA_GRAPH_STREAMS=1: the side / branch streams fork from and join a HIP-graph capture
+# stream, and the graph keeps that concurrency (the allocator defers reuse of
+# record_stream'ed blocks until the capture ends; replay == eager bitwise,
+# tests/test_determinism_gpu.py).  Off by default: replaying the multi-stream graph measured
+# slower than the one-stream graph (DenseNet-121 8.93k vs 9.07k img/s), and both slower
+# than eager with streams (9.53k; profiles/ab_r4.txt call 15).
+_GRAPH_STREAMS = os.environ.get("MPA_GRAPH_STREAMS", "0") == "1"
 
 
 def _capture_blocks_streams() -> bool:
