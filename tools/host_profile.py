@@ -44,12 +44,16 @@ def main():
     wall = (time.perf_counter() - t0) / n
     print(f"{name} {hw}px b{B}: synchronized step {wall * 1e3:.2f} ms, host enqueue "
           f"{sum(host) / n * 1e3:.2f} ms/step (min {min(host) * 1e3:.2f})", flush=True)
+    # backward nodes normally run on autograd's device thread, which cProfile does not
+    # see: run them on this thread for the profile
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(n):
         step(x, y)
     torch.cuda.synchronize()
     pr.disable()
+    torch.autograd.set_multithreading_enabled(True)
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(top)
 
