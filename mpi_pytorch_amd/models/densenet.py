@@ -66,6 +66,37 @@ _POOL_FIRST = os.environ.get("MPA_DENSE_POOL_FIRST", "1") == "1"
 _FUSE_POOL = os.environ.get("MPA_DENSE_FUSE_POOL", "1") == "1"
 
 
+# MPA_DENSE_WALK=0: each layer's backward as a nested torch.autograd.backward call
+_WALK = os.environ.get("MPA_DENSE_WALK", "1") == "1"
+
+
+def _chain_nodes(out: torch.Tensor, leaf: torch.Tensor):
+    """The backward nodes from ``out`` to ``leaf`` when the layer's graph is a chain of
+    custom Functions along their first input (conv2 <- conv1+norm2 <- leaf; the parameter
+    inputs take no autograd gradient, the kernels write the arena); None otherwise."""
+    nodes, node = [], out.grad_fn
+    for _ in range(4):
+        if node is None:
+            return None
+        if type(node).__name__ == "AccumulateGrad":
+            return nodes if node.variable is leaf else None
+        if not hasattr(node, "_forward_cls") or not node.next_functions:
+            return None
+        nodes.append(node)
+        node = node.next_functions[0][0]
+    return None
+
+
+def _walk_backward(nodes, g):
+    """Run a layer's backward by calling its nodes directly (see _chain_nodes): the nested
+    engine pass per layer (graph task, dependency scan, reentrant dispatch) is host time
+    a 58-layer DenseNet pays 58 times per step.  Returns the leaf's gradient."""
+    for node in nodes:
+        r = node.apply(g)
+        g = r[0] if isinstance(r, tuple) else r
+    return g
+
+
 def _window(buf: torch.Tensor, c0: int, n: int) -> torch.Tensor:
     """buf[..., c0:c0 + n] as a plain alias of buf's storage, not an autograd view: conv2's
     custom Function returns it as its output, and the other layers' writes into buf must
@@ -92,7 +123,12 @@ class _DenseBlock(nn.ModuleDict):
         """Returns (block output, its per-channel [mean | var] or None)."""
         if fused and _BLOCK_GRAD:
             if self.training and torch.is_grad_enabled() and x.requires_grad:
-                params = [p for p in self.parameters() if p.requires_grad]
+                # (the module walk of parameters() costs ~1 ms of host time per step over
+                # the four blocks: the list is taken once, requires_grad read each step)
+                ps = self.__dict__.get("_mpa_params")
+                if ps is None:
+                    ps = self.__dict__["_mpa_params"] = tuple(self.parameters())
+                params = [p for p in ps if p.requires_grad]
                 out = _DenseBlockGrad.apply(x, self, *params)
                 return out, self.__dict__.pop("_stats", None)
             if not self.training and not (torch.is_grad_enabled() and x.requires_grad):
@@ -232,10 +268,14 @@ class _DenseBlockGrad(torch.autograd.Function):
                          k.chan_extract(G, ci, g).to(out.dtype))
             if link is not None:
                 link.gacc = G
-            torch.autograd.backward(out, g_out)
+            nodes = _chain_nodes(out, leaf) if _WALK else None
+            if nodes is not None:
+                dy = _walk_backward(nodes, g_out)
+            else:
+                torch.autograd.backward(out, g_out)
+                dy = leaf.grad
             n1 = layers[i].norm1
             gamma, beta = n1.weight, n1.bias
-            dy = leaf.grad
             if link is not None and link.sums is not None:
                 # conv1's dgrad added gamma*rstd * g into G[..., :ci]; fold this layer's
                 # corrections and finish the channels no earlier layer reads: layer i-1's

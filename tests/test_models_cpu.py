@@ -371,6 +371,30 @@ def test_densenet_feature_buffer_blocks_equal_plain_autograd(monkeypatch, defer)
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
 
 
+def test_densenet_direct_layer_walk_equals_nested_backward(monkeypatch):
+    """Each dense layer's backward by calling its chain of backward nodes directly
+    (densenet._walk_backward) == a nested torch.autograd.backward per layer, bitwise."""
+    from mpi_pytorch_amd.models import densenet as dn
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("densenet", 10, torch.device("cpu"), World(), 1e-3)
+    a = model._mpa_arena
+    x = torch.randn(2, 64, 64, 8) * (torch.arange(8) < 3)
+    y = torch.randint(0, 10, (2,))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    res = []
+    walked = []
+    real = dn._walk_backward
+    monkeypatch.setattr(dn, "_walk_backward", lambda n, g: walked.append(1) or real(n, g))
+    for walk in (True, False):
+        monkeypatch.setattr(dn, "_WALK", walk)
+        model.load_state_dict(sd)
+        a.zero_grad()
+        loss_fn(model(x), y).backward()
+        res.append(a.grad.clone())
+    assert len(walked) == 58  # every layer took the direct walk
+    assert torch.equal(res[0], res[1])
+
+
 def test_inception_fused_stem_pools_equal_modules():
     """Conv2d_2b -> maxpool1 and Conv2d_4a -> maxpool2 as fused conv+BN+ReLU+max-pool ops ==
     the BasicConv2d + MaxPool2d modules (fp32, CPU): logits, running stats, gradients."""
