@@ -95,6 +95,8 @@ def _done(*ps) -> None:
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
 _SIDE = {"stream": None, "on": False, "used": False}
+# MPA_WGRAD_PRIO=-1: the side stream at high priority (HIP queue priority; A/B knob)
+_WGRAD_PRIO = int(os.environ.get("MPA_WGRAD_PRIO", "0"))
 # MPA_GRAPH_STREAMS=1: the side / branch streams fork from and join a HIP-graph capture
 # stream, and the graph keeps that concurrency (the allocator defers reuse of
 # record_stream'ed blocks until the capture ends; replay == eager bitwise,
@@ -131,7 +133,7 @@ def _run_wgrad(fn, *tensors) -> None:
     main = torch.cuda.current_stream(t0.device)
     side = _SIDE["stream"]
     if side is None or side.device != t0.device:
-        side = _SIDE["stream"] = torch.cuda.Stream(t0.device)
+        side = _SIDE["stream"] = torch.cuda.Stream(t0.device, priority=_WGRAD_PRIO)
     side.wait_stream(main)
     with torch.cuda.stream(side):
         fn()
