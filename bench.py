@@ -275,6 +275,13 @@ def _multi_gpu_decisions(step, data, args, world, sync) -> dict:
 
     res["comm_bf16" if orig_dtype != "bf16" else "comm_fp32"] = _variant(
         step, data, args, world, sync, bf16_on, bf16_off)
+    def wgs_on():
+        step.wgrad_stream_ddp = not orig_wgs
+        return {"wgrad_stream_ddp": step.wgrad_stream_ddp}
+
+    orig_wgs = step.wgrad_stream_ddp
+    res["wgrad_stream_on" if not orig_wgs else "wgrad_stream_off"] = _variant(
+        step, data, args, world, sync, wgs_on, lambda: setattr(step, "wgrad_stream_ddp", orig_wgs))
     res["allreduce_probe"] = probe
     return res
 

@@ -60,6 +60,10 @@ def loss_fn(out, labels, acc=None):
 # the backward it overlaps by more than it hides (same-box A/B, profiles/early_head_ab_r3.txt:
 # ResNet-18 b1024 48.0k vs 48.2k, b128 28.1k vs 28.7k, Inception 6.99k vs 7.09k img/s).
 _EARLY_HEAD = os.environ.get("MPA_EARLY_HEAD_OPT", "0") == "1"
+# MPA_WGRAD_STREAM_DDP=1: side-stream weight gradients with several ranks too (the bucket
+# collectives then wait for both streams, GradBucketer._launch).  Off by default until the
+# 8-GPU run measures it (bench.py records both in its multi_gpu decisions)
+_WGRAD_DDP = os.environ.get("MPA_WGRAD_STREAM_DDP", "0") == "1"
 # MPA_STEP_GC=1 leaves Python's cyclic collector running inside the training loop
 _STEP_GC = os.environ.get("MPA_STEP_GC", "0") == "1"
 
@@ -211,6 +215,7 @@ class TrainStep:
         # heads: 75 % of ResNet-18's parameters); once its gradients are final (and, over
         # RCCL, all-reduced) its optimizer update runs on a side stream under the rest of
         # the backward instead of after it
+        self.wgrad_stream_ddp = _WGRAD_DDP
         self._head = self._early_head()
         self._head_left = 0
         self._head_launched = False
@@ -285,7 +290,7 @@ class TrainStep:
             m.range_pop()
             m.range_push("bwd")
         # (single GPU: conv weight gradients may run on a side stream, joined right after)
-        Fn.wgrad_stream_begin(single)
+        Fn.wgrad_stream_begin(single or self.wgrad_stream_ddp)
         try:
             loss.backward(self._one)
         finally:

@@ -113,6 +113,17 @@ def _capture_blocks_streams() -> bool:
 def wgrad_stream_begin(enabled: bool = True) -> None:
     """Route the following conv weight gradients to the side stream (TrainStep backward)."""
     _SIDE["on"] = bool(enabled and _WGRAD_STREAM)
+    if _SIDE["on"] and torch.cuda.is_available():
+        _SIDE["main"] = torch.cuda.current_stream()
+
+
+def wgrad_streams():
+    """(compute stream, side stream) while side-stream weight gradients are routed and the
+    side stream exists, else None: a gradient bucket launched then must wait for both
+    (parallel/ddp.py GradBucketer._launch)."""
+    if _SIDE["on"] and _SIDE["stream"] is not None and _SIDE.get("main") is not None:
+        return _SIDE["main"], _SIDE["stream"]
+    return None
 
 
 def join_wgrad_stream() -> None:

@@ -98,6 +98,11 @@ def capped_group(max_ctas: int, device: torch.device):
     return None
 
 
+def _wgrad_streams():
+    from ..ops.functional import wgrad_streams
+    return wgrad_streams()
+
+
 class GradBucketer:
     def __init__(self, arena: ParamArena, world_size: int, bucket_mb: float = 16.0,
                  overlap: bool = True, comm_dtype: str = "fp32", group=None,
@@ -139,6 +144,7 @@ class GradBucketer:
             for p in ps:
                 self.bucket_of[id(p)] = bi
         self._pending = [0] * len(self.buckets)
+        self._launch_stream = None  # (side-stream weight gradients under DP: _launch)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._wire: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         # [bucket, wire bytes, work (None once resolved), host t0, host t1 | resolved ms]
@@ -225,16 +231,32 @@ class GradBucketer:
             if not self._reserved:
                 _set_reserve(self.comm_ctas)
                 self._reserved = True
-        if self.comm_dtype == "bf16" and g.is_cuda:
-            g = g.to(torch.bfloat16)
-            self._wire[bi] = g
-        self._works[bi] = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        streams = _wgrad_streams() if g.is_cuda else None
+        if streams is not None:
+            # side-stream weight gradients (TrainStep.wgrad_stream_ddp): this bucket's
+            # gradients come from both the compute and the side stream, so the collective
+            # is issued from a helper stream that waits for both (neither stream blocks)
+            if self._launch_stream is None:
+                self._launch_stream = torch.cuda.Stream(g.device)
+            h = self._launch_stream
+            h.wait_stream(streams[0])
+            h.wait_stream(streams[1])
+            with torch.cuda.stream(h):
+                self._works[bi] = self._issue(bi, g, group)
+        else:
+            self._works[bi] = self._issue(bi, g, group)
         if self._stats is not None and len(self._stats) < self._MAX_STATS:
             self._stats.append([bi, g.numel() * g.element_size(), self._works[bi],
                                 time.perf_counter(), None])
             self._held += 1
             if self._held > self._MAX_HELD:
                 self._resolve_old()
+
+    def _issue(self, bi: int, g: torch.Tensor, group):
+        if self.comm_dtype == "bf16" and g.is_cuda:
+            g = g.to(torch.bfloat16)
+            self._wire[bi] = g
+        return dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group, async_op=True)
 
     def finish(self) -> None:
         """Issue any bucket not yet launched, then make the compute stream wait for all."""
@@ -256,6 +278,8 @@ class GradBucketer:
             if self._wire[bi] is not None:
                 s, e = self.ranges[bi]
                 self.arena.grad[s:e].copy_(self._wire[bi])
+                if self._launch_stream is not None:
+                    self._wire[bi].record_stream(torch.cuda.current_stream())
                 self._wire[bi] = None
         if self._reserved:
             # kernels enqueued from here on (optimizer, next forward) run after the waits

@@ -60,25 +60,31 @@ x = X[w.rank * n:(w.rank + 1) * n].to(w.device)
 y = Y[w.rank * n:(w.rank + 1) * n].to(w.device)
 step(x, y)
 torch.cuda.synchronize()
+from mpi_pytorch_amd.ops import functional as Fn
+if os.environ.get("MPA_WGRAD_STREAM_DDP") == "1":
+    assert Fn._SIDE["stream"] is not None and step.bucketer._launch_stream is not None
 if w.rank == 0:
     torch.save({"master": model._mpa_arena.master.cpu()}, sys.argv[1])
 shutdown()
 '''
 
 
-def test_dp_two_ranks_equals_one_rank_on_gpu(gpu, tmp_path):
+@pytest.mark.parametrize("wgs", ["0", "1"])
+def test_dp_two_ranks_equals_one_rank_on_gpu(gpu, tmp_path, wgs):
     """2 ranks x 16 images: BN takes per-rank batch statistics (as in the reference), so DP
     equals one process stepping on the AVERAGE of the two halves' gradients, computed here
     with the same kernels (two backward passes accumulating in the arena, grad_scale 1/2).
     One SGD step (Adam's first step is sign-like and would amplify rounding-level
-    differences of near-zero gradients), deterministic mode."""
+    differences of near-zero gradients), deterministic mode.  wgs=1: the ranks' conv weight
+    gradients on the side stream, each bucket's collective issued from a stream that waits
+    for both (MPA_WGRAD_STREAM_DDP)."""
     script = tmp_path / "w.py"
     script.write_text(_WORKER)
     out = tmp_path / "dp.pt"
     cmd = [sys.executable, "-m", "mpi_pytorch_amd.launch", "-n", "2", "--timeout", "200",
            str(script), str(out)]
-    r = subprocess.run(cmd, cwd=str(tmp_path), env=_env(), capture_output=True, text=True,
-                       timeout=240)
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=_env(MPA_WGRAD_STREAM_DDP=wgs),
+                       capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     dp = torch.load(str(out))["master"]
     # one process: gradients of the two halves summed in the arena (two backward passes,
