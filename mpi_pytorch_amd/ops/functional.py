@@ -94,6 +94,8 @@ def _done(*ps) -> None:
 # optimizer (join_wgrad_stream); x / dz are record_stream'ed so the caching allocator does
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
+# MPA_FC_WGRAD_STREAM=0: Linear weight gradients stay on the compute stream
+_FC_SIDE = os.environ.get("MPA_FC_WGRAD_STREAM", "1") == "1"
 _SIDE = {"stream": None, "on": False, "used": False}
 # MPA_WGRAD_PRIO=-1: the side stream at high priority (HIP queue priority; A/B knob)
 _WGRAD_PRIO = int(os.environ.get("MPA_WGRAD_PRIO", "0"))
@@ -1013,8 +1015,13 @@ class _LinearAct(torch.autograd.Function):
               else None)
         _done(b)
         if w.requires_grad:
-            k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
-            _done(w)
+            def wgrad():
+                k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
+                _done(w)
+            if _FC_SIDE:
+                _run_wgrad(wgrad, g, x)
+            else:
+                wgrad()
         return dx, None, None, None, None
 
 
