@@ -94,8 +94,10 @@ def _done(*ps) -> None:
 # optimizer (join_wgrad_stream); x / dz are record_stream'ed so the caching allocator does
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
-# MPA_FC_WGRAD_STREAM=0: Linear weight gradients stay on the compute stream
-_FC_SIDE = os.environ.get("MPA_FC_WGRAD_STREAM", "1") == "1"
+# MPA_FC_WGRAD_STREAM=1: Linear weight gradients on the side stream as well.  Off: same-box
+# A/B (profiles/ab_r4.txt call 21) VGG-16 +1.0 %, ResNet-18 +0.1 %, Inception -0.4 %,
+# AlexNet -4.7 % (its three large FC weight gradients then contend with the FC dgrads)
+_FC_SIDE = os.environ.get("MPA_FC_WGRAD_STREAM", "0") == "1"
 _SIDE = {"stream": None, "on": False, "used": False}
 # MPA_WGRAD_PRIO=-1: the side stream at high priority (HIP queue priority; A/B knob)
 _WGRAD_PRIO = int(os.environ.get("MPA_WGRAD_PRIO", "0"))
