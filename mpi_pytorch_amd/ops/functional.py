@@ -94,6 +94,8 @@ def _done(*ps) -> None:
 # optimizer (join_wgrad_stream); x / dz are record_stream'ed so the caching allocator does
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
+# MPA_STEM_WGRAD_STREAM=0: the fused stem's weight gradient stays on the compute stream
+_STEM_SIDE = os.environ.get("MPA_STEM_WGRAD_STREAM", "1") == "1"
 # MPA_FC_WGRAD_STREAM=1: Linear weight gradients on the side stream as well.  Off: same-box
 # A/B (profiles/ab_r4.txt call 21) VGG-16 +1.0 %, ResNet-18 +0.1 %, Inception -0.4 %,
 # AlexNet -4.7 % (its three large FC weight gradients then contend with the FC dgrads)
@@ -780,7 +782,10 @@ class _ConvBNReLUPool(torch.autograd.Function):
                 k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
                 conv.fix_grad(w.grad)
                 _done(w)
-            _run_wgrad(wgrad, dz, x)
+            if _STEM_SIDE:
+                _run_wgrad(wgrad, dz, x)
+            else:
+                wgrad()
         _done(ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:
