@@ -147,13 +147,18 @@ def _run_wgrad(fn, *tensors) -> None:
     if not (_SIDE["on"] and t0.is_cuda) or _capture_blocks_streams():
         fn()
         return
-    main = torch.cuda.current_stream(t0.device)
+    main = torch.cuda.current_stream()
     side = _SIDE["stream"]
     if side is None or side.device != t0.device:
         side = _SIDE["stream"] = torch.cuda.Stream(t0.device, priority=_WGRAD_PRIO)
     side.wait_stream(main)
-    with torch.cuda.stream(side):
+    # (set_stream / restore instead of the torch.cuda.stream context: ~20 us less host
+    # time per weight gradient, which the host-bound small-batch step feels)
+    torch.cuda.set_stream(side)
+    try:
         fn()
+    finally:
+        torch.cuda.set_stream(main)
     for t in tensors:
         t.record_stream(side)
     _SIDE["used"] = True
