@@ -13,6 +13,21 @@ Timing: W untimed warmup steps, then EXACTLY K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the max over ranks is reported.  The timed region
 includes the data path (ring acquire, H2D, preprocess kernel), forward, backward, the
 gradient all-reduce and the optimizer step.  Rank 0 prints one JSON line.
+
+Failure handling (the reference aborts the whole job on any rank's error,
+/root/reference/README.md:38; its blocking per-tensor Allreduce loop, mpi_tools.py:30-37,
+hangs forever on a lost peer):
+  * the process group has a bounded timeout (--pg-timeout) and the self-spawned job a wall
+    clock limit (--job-timeout), both well inside a driver's 600 s command limit;
+  * warm-up and timed steps run under the device-completion watchdog (--watchdog seconds,
+    parallel/watchdog.py): a rank whose GPU stops completing steps dumps its stacks and exits
+    75 with a rank-tagged message, and the launcher tears the job down;
+  * the headline record is built right after the timed steps.  The optional extras after it
+    (multi-GPU decision variants, the small-batch pass) each run in try/except, and all of
+    them under one wall-clock budget (--extras-budget): an error is recorded in the line
+    ("error" fields), a hang prints the headline line anyway and ends every rank with 0.
+  Test hooks (tests/test_launch_cpu.py): MPA_BENCH_INJECT=variant_raise | extras_hang |
+  hang_rank=R.
 """
 from __future__ import annotations
 
@@ -20,6 +35,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -116,8 +132,68 @@ def parse_args(argv=None):
                    help="more than one GPU: after the headline, also time the capped-communicator "
                         "+ reservation and bf16-wire variants and probe the all-reduce bandwidth "
                         "('multi_gpu' in the JSON; 0: off)")
+    p.add_argument("--pg-timeout", type=float, default=240.0,
+                   help="process-group timeout in seconds (rendezvous and every collective)")
+    p.add_argument("--job-timeout", type=float, default=560.0,
+                   help="self-spawned multi-GPU job: wall-clock limit of the whole job (0 off)")
+    p.add_argument("--watchdog", type=float, default=180.0,
+                   help="seconds without a completed step (device events) before a rank "
+                        "dumps its stacks and exits 75 (0 off)")
+    p.add_argument("--extras-budget", type=float, default=150.0,
+                   help="wall-clock budget of everything after the headline measurement "
+                        "(multi-GPU decisions, small-batch pass); on expiry the headline line "
+                        "is printed anyway")
     args = p.parse_args(argv)
     return args
+
+
+def _inject() -> str:
+    return os.environ.get("MPA_BENCH_INJECT", "")
+
+
+class _Emitter:
+    """Prints rank 0's JSON record exactly once, from the main thread or from the extras
+    deadline (whichever comes first)."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+        self._lock = threading.Lock()
+        self.done = False
+
+    def emit(self, rec: dict) -> bool:
+        with self._lock:
+            if self.done:
+                return False
+            self.done = True
+        if self.rank == 0:
+            print(json.dumps(rec), flush=True)
+        return True
+
+
+def _deadline(seconds: float, emitter: _Emitter, rec: dict, rank: int):
+    """Arm the extras budget: on expiry rank 0 prints the headline record (with
+    ``extras_error``) and every rank exits 0 - the headline measurement is complete and
+    valid; only the optional extras after it are lost."""
+    def fire():
+        rec["extras_error"] = "timeout: extras exceeded %.0f s" % seconds
+        sys.stderr.write("bench.py rank %d: %s; headline kept\n" % (rank, rec["extras_error"]))
+        sys.stderr.flush()
+        emitter.emit(rec)
+        sys.stdout.flush()
+        os._exit(0)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def _guarded(name: str, fn):
+    """Run one optional extra; an exception becomes {"error": ...} in the record."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 - any failure of an extra must not lose the headline
+        sys.stderr.write("bench.py: extra %r failed: %r\n" % (name, e))
+        return {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
 
 
 def _launcher_env() -> bool:
@@ -136,7 +212,9 @@ def spawn(argv, nprocs: int) -> int:
         "_mpa_launch", os.path.join(ROOT, "mpi_pytorch_amd", "launch.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    return mod.launch(nprocs, [sys.executable, os.path.abspath(__file__)] + list(argv))
+    a = parse_args(argv)
+    return mod.launch(nprocs, [sys.executable, os.path.abspath(__file__)] + list(argv),
+                      timeout=a.job_timeout)
 
 
 def _timed(step, data, args, world, sync) -> float:
@@ -177,6 +255,8 @@ def _variant(step, data, args, world, sync, configure, restore) -> dict:
     from mpi_pytorch_amd.engine import steps_without_gc
     info = configure() or {}
     try:
+        if _inject() == "variant_raise":
+            raise RuntimeError("injected variant failure")
         for _ in range(max(min(args.warmup, 3), 1)):
             x, y = data.next()
             step(x, y)
@@ -255,7 +335,7 @@ def _multi_gpu_decisions(step, data, args, world, sync) -> dict:
     b = step.bucketer
     res = {}
     orig_ctas, orig_dtype = b.comm_ctas, b.comm_dtype
-    probe = {"default": _allreduce_probe(world)}
+    probe = {"default": _guarded("allreduce_probe", lambda: _allreduce_probe(world))}
 
     def capped_on():
         ok = b.set_comm_ctas(8 if orig_ctas == 0 else 0)
@@ -263,8 +343,8 @@ def _multi_gpu_decisions(step, data, args, world, sync) -> dict:
             probe["capped"] = _allreduce_probe(world, group=b.overlap_group)
         return {"comm_ctas": b.comm_ctas, "capped_communicator": bool(ok)}
 
-    res["comm_ctas8" if orig_ctas == 0 else "comm_ctas0"] = _variant(
-        step, data, args, world, sync, capped_on, lambda: b.set_comm_ctas(orig_ctas))
+    res["comm_ctas8" if orig_ctas == 0 else "comm_ctas0"] = _guarded("comm_ctas", lambda: _variant(
+        step, data, args, world, sync, capped_on, lambda: b.set_comm_ctas(orig_ctas)))
 
     def bf16_on():
         b.comm_dtype = "bf16" if orig_dtype != "bf16" else "fp32"
@@ -273,15 +353,16 @@ def _multi_gpu_decisions(step, data, args, world, sync) -> dict:
     def bf16_off():
         b.comm_dtype = orig_dtype
 
-    res["comm_bf16" if orig_dtype != "bf16" else "comm_fp32"] = _variant(
-        step, data, args, world, sync, bf16_on, bf16_off)
+    res["comm_bf16" if orig_dtype != "bf16" else "comm_fp32"] = _guarded("comm_dtype", lambda: _variant(
+        step, data, args, world, sync, bf16_on, bf16_off))
     def wgs_on():
         step.wgrad_stream_ddp = not orig_wgs
         return {"wgrad_stream_ddp": step.wgrad_stream_ddp}
 
     orig_wgs = step.wgrad_stream_ddp
-    res["wgrad_stream_on" if not orig_wgs else "wgrad_stream_off"] = _variant(
-        step, data, args, world, sync, wgs_on, lambda: setattr(step, "wgrad_stream_ddp", orig_wgs))
+    res["wgrad_stream_on" if not orig_wgs else "wgrad_stream_off"] = _guarded(
+        "wgrad_stream", lambda: _variant(step, data, args, world, sync, wgs_on,
+                                         lambda: setattr(step, "wgrad_stream_ddp", orig_wgs)))
     res["allreduce_probe"] = probe
     return res
 
@@ -295,7 +376,7 @@ def run(args) -> None:
 
     cuda = args.device == "cuda"
     timers = args.timers == "on" or (args.timers == "auto" and args.gpus > 1)
-    world = init_world(args.device, comm_timing=timers and cuda)
+    world = init_world(args.device, timeout_s=args.pg_timeout, comm_timing=timers and cuda)
     if world.world_size != args.gpus:
         raise SystemExit("bench.py: --gpus {} but this job has {} ranks".format(
             args.gpus, world.world_size))
@@ -320,6 +401,23 @@ def run(args) -> None:
         data.next = lambda: (xs, ys)
     if args.emulate_comm:
         _emulate_comm(model, step, args.emulate_comm, dev, args.comm_reserve)
+    # progress watchdog over warm-up and the timed steps: a rank whose device stops
+    # completing steps (a peer lost inside a collective) exits 75 instead of hanging
+    from mpi_pytorch_amd.parallel.watchdog import Watchdog
+    wd = Watchdog(args.watchdog, rank=world.rank, name="bench").start()
+    inject = _inject()
+    hang_rank = int(inject.split("=", 1)[1]) if inject.startswith("hang_rank=") else -1
+    nbeat = [0]
+
+    def beat():
+        nbeat[0] += 1
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            wd.beat_on(nbeat[0], ev)
+        else:
+            wd.beat(nbeat[0])
+
     # eager by default: the step is GPU-bound (host runs ahead), graph replay buys nothing
     # measurable and needs a per-step sync for correctness (engine/step.py)
     use_graph = args.graph == "on" and cuda
@@ -329,6 +427,7 @@ def run(args) -> None:
     for _ in range(args.warmup):
         x, y = data.next()
         loss = step(x, y)
+        beat()
         if args.print_losses and world.rank == 0:
             print("warmup loss %.4f" % float(loss), file=sys.stderr)
     if args.print_losses:
@@ -353,17 +452,21 @@ def run(args) -> None:
     barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == 1 and world.rank == hang_rank:
+            time.sleep(1e6)  # test hook: a rank that never reaches its next collective
         if mk is not None:
             mk.range_push("data")
         x, y = data.next()
         if mk is not None:
             mk.range_pop()
         step(x, y)
+        beat()
     sync()
     barrier()
     sync()
     dt = time.perf_counter() - t0
+    wd.stop()
     loss = step.mean_loss()
     phases = step.timer.summary() if step.timer is not None else None
     comm = step.bucketer.comm_stats()
@@ -375,74 +478,81 @@ def run(args) -> None:
     imgs = args.steps * args.batch * world.world_size
     value = imgs / dt
     ring = data_stats(True)
-    decisions = None
+
+    # ---- the headline record, complete before any optional extra runs
+    metric = "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X"
+    if args.model != "resnet18" or args.image_size != 224:  # a zoo run, not the headline
+        metric = "images/sec (whole node) {} {}x{} training on {} MI355X".format(
+            args.model, args.image_size, args.image_size, world.world_size)
+    rec = {
+        "metric": metric,
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world.world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt * 1000.0 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_IMG_S, 2),
+        "dtype": "bf16" if cuda else "fp32",
+        "data": "synthetic",
+        "config": {
+            "model": args.model,
+            "global_batch": args.batch * world.world_size,
+            "per_gpu_batch": args.batch,
+            "seq_len": None,
+            "image_size": args.image_size,
+            "num_classes": args.classes,
+            "optimizer": args.optimizer,
+            "parallelism": "dp{}".format(world.world_size),
+            "device": args.device,
+            "backend": world.backend,
+            "hip_graph": bool(use_graph),
+            "mean_loss": round(loss, 4),
+        },
+    }
+    if phases is not None:
+        rec["phases_ms"] = phases
+    if world.world_size > 1:
+        rec["grad_allreduce_mb"] = step.bucketer.wire_mb()
+        rec["comm_ctas"] = step.bucketer.comm_ctas if step.bucketer.overlap_group else 0
+    if comm is not None:
+        rec["comm"] = comm
+    if ring is not None:
+        rec["data_ring"] = ring
+    from mpi_pytorch_amd.parallel.dist import affinity
+    if affinity() is not None:
+        rec["host_affinity"] = affinity()
+
+    # ---- optional extras, each guarded, all under one wall-clock budget
+    emitter = _Emitter(world.rank)
+    timer = _deadline(args.extras_budget, emitter, rec, world.rank)
+    if inject == "extras_hang":
+        time.sleep(1e6)
     if world.world_size > 1 and not args.emulate_comm and args.decisions:
-        decisions = _multi_gpu_decisions(step, data, args, world, sync)
-    small = None
+        rec["multi_gpu"] = _guarded("multi_gpu", lambda: _multi_gpu_decisions(
+            step, data, args, world, sync))
     if args.small_batch and args.small_batch != args.batch and cuda and not args.emulate_comm:
-        step.timer = None
-        step.bucketer._stats = None
-        data.close()
-        data = DevicePrefetcher(dev, args.small_batch, hw, hw, args.classes, seed=4321,
-                                rank=world.rank, world=world.world_size, depth=6, threads=2,
-                                cpad=spec["cpad"], pad=spec["pad"])
-        small = {"per_gpu_batch": args.small_batch,
-                 "eager_img_per_s": round(_timed(step, data, args, world, sync), 1)}
-        if world.world_size == 1:
-            x, y = data.next()
-            if step.capture(x, y):
-                small["graph_img_per_s"] = round(_timed(step, data, args, world, sync), 1)
-        step.mean_loss()
-    if world.rank == 0:
-        metric = "images/sec (whole node) ResNet-18 224x224 training at 1/2/4/8 MI355X"
-        if args.model != "resnet18" or args.image_size != 224:  # a zoo run, not the headline
-            metric = "images/sec (whole node) {} {}x{} training on {} MI355X".format(
-                args.model, args.image_size, args.image_size, world.world_size)
-        rec = {
-            "metric": metric,
-            "value": round(value, 2),
-            "unit": "images/sec",
-            "n_gpus": world.world_size,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt * 1000.0 / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_IMG_S, 2),
-            "dtype": "bf16" if cuda else "fp32",
-            "data": "synthetic",
-            "config": {
-                "model": args.model,
-                "global_batch": args.batch * world.world_size,
-                "per_gpu_batch": args.batch,
-                "seq_len": None,
-                "image_size": args.image_size,
-                "num_classes": args.classes,
-                "optimizer": args.optimizer,
-                "parallelism": "dp{}".format(world.world_size),
-                "device": args.device,
-                "backend": world.backend,
-                "hip_graph": bool(use_graph),
-                "mean_loss": round(loss, 4),
-            },
-        }
-        if phases is not None:
-            rec["phases_ms"] = phases
-        if world.world_size > 1:
-            rec["grad_allreduce_mb"] = step.bucketer.wire_mb()
-            rec["comm_ctas"] = step.bucketer.comm_ctas if step.bucketer.overlap_group else 0
-        if comm is not None:
-            rec["comm"] = comm
-        if ring is not None:
-            rec["data_ring"] = ring
-        from mpi_pytorch_amd.parallel.dist import affinity
-        if affinity() is not None:
-            rec["host_affinity"] = affinity()
-        if decisions is not None:
-            rec["multi_gpu"] = decisions
-        if small is not None:
-            rec["small_batch"] = small
-        print(json.dumps(rec), flush=True)
+        def small_pass():
+            nonlocal data
+            step.timer = None
+            step.bucketer._stats = None
+            data.close()
+            data = DevicePrefetcher(dev, args.small_batch, hw, hw, args.classes, seed=4321,
+                                    rank=world.rank, world=world.world_size, depth=6,
+                                    threads=2, cpad=spec["cpad"], pad=spec["pad"])
+            small = {"per_gpu_batch": args.small_batch,
+                     "eager_img_per_s": round(_timed(step, data, args, world, sync), 1)}
+            if world.world_size == 1:
+                x, y = data.next()
+                if step.capture(x, y):
+                    small["graph_img_per_s"] = round(_timed(step, data, args, world, sync), 1)
+            step.mean_loss()
+            return small
+        rec["small_batch"] = _guarded("small_batch", small_pass)
+    timer.cancel()
+    emitter.emit(rec)
     data.close()
     from mpi_pytorch_amd.parallel import shutdown
     shutdown()

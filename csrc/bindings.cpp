@@ -555,52 +555,6 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t 
   mpa::igemm_wgrad(a, vec_width(K), (C % 8 == 0) ? 8 : 1, cur_stream());
 }
 
-// The stem's weight gradient with its max-pool + BN + ReLU backward computed on the fly:
-// dz (the conv output's gradient) is never written.  Needs zsel (the forward's argmax z);
-// returns false - nothing launched - when the shape is not the fused kernel's (the caller
-// then runs maxpool_bn_bwd + conv_wgrad)
-bool stem_wgrad_poolbn(Tensor dp, Tensor idx, Tensor z, Tensor zsel, Tensor mean, Tensor rstd,
-                       Tensor gamma, Tensor beta, Tensor dgamma, Tensor dbeta, Tensor x, Tensor dw,
-                       int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool overwrite) {
-  CHECK_ACT(dp);
-  CHECK_ACT(z);
-  CHECK_ACT(zsel);
-  CHECK_ACT(x);
-  CHECK_CUDA(dw);
-  CHECK_F32(dw);
-  CHECK_CONTIG(dw);
-  TORCH_CHECK(idx.sizes() == dp.sizes() && zsel.sizes() == dp.sizes() &&
-                  idx.scalar_type() == torch::kUInt8 && idx.is_contiguous(),
-              "stem_wgrad_poolbn: pooled tensors");
-  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  const int P = z.size(1), Q = z.size(2), K = z.size(3);
-  TORCH_CHECK(dw.dim() == 4 && dw.size(0) == K && dw.size(3) == C && z.size(0) == N &&
-                  dp.size(0) == N && dp.size(3) == K,
-              "stem_wgrad_poolbn: shapes");
-  for (const Tensor* t : {&mean, &rstd, &gamma, &beta})
-    TORCH_CHECK(t->numel() == K && t->scalar_type() == torch::kFloat32 && t->is_contiguous(),
-                "stem_wgrad_poolbn: per-channel vectors");
-  const c10::OptionalDeviceGuard g(device_of(z));
-  mpa::WGradArgs a{};
-  a.dy = bp(z); a.x = bp(x); a.dw = dw.data_ptr<float>();
-  a.Kout = K; a.C = C; a.H = H; a.W = W; a.P = P; a.Q = Q; a.R = dw.size(1); a.S = dw.size(2);
-  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
-  a.Mpix = N * P * Q;
-  a.Ncols = a.R * a.S * C;
-  a.overwrite = overwrite ? 1 : 0;
-  const int P2 = dp.size(1), Q2 = dp.size(2);
-  Tensor slab;  // (the eligibility check includes the partials slab)
-  a.slab = alloc_ws(slab, z, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
-  if (!mpa::stem_wgrad_pb_ok(a, P2, Q2)) return false;
-  Tensor ws = torch::empty({mpa::maxpool_bn_ws_floats(N * P2 * Q2, K)},
-                           z.options().dtype(torch::kFloat32));
-  mpa::maxpool_bn_sel_sums(bp(dp), bp(zsel), fopt(mean), fopt(rstd), fopt(gamma), fopt(beta), K,
-                           N * P2 * Q2, ws.data_ptr<float>(), cur_stream());
-  return mpa::igemm_wgrad_stem_pb(a, bp(dp), idx.data_ptr<uint8_t>(), bp(z), fopt(mean),
-                                  fopt(rstd), fopt(gamma), fopt(beta), ws.data_ptr<float>(),
-                                  fopt_mut(dgamma), fopt_mut(dbeta), P2, Q2, cur_stream());
-}
-
 Tensor act_bwd(Tensor dy, Tensor y, Tensor dbias) {
   CHECK_ACT(dy);
   const int C = dy.size(-1);
@@ -1638,8 +1592,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma") = py::none(), py::arg("beta") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("act_bwd", &act_bwd);
-  m.def("stem_wgrad_poolbn", &stem_wgrad_poolbn,
-        "stem weight gradient with the max-pool + BN + ReLU backward fused into its staging");
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("stats"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"),
         py::arg("res"), py::arg("relu"), py::arg("counter") = py::none(),

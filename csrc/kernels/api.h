@@ -183,24 +183,6 @@ void igemm_set_halo_strip(int mode);  // MPA_HALO_STRIP (0 off, 1 wide images, 2
 bool stem_wgrad_ok(const WGradArgs& a);
 int stem_wgrad(WGradArgs a, hipStream_t s);
 int64_t stem_wgrad_ws_floats();
-// the same with dz = the stem's max-pool + BN + ReLU backward computed while staging (a.dy
-// unused; dp / idx pooled [N][P2][Q2][64], z the conv output, sums [2][64] from
-// maxpool_bn_sel_sums); block 0 adds the sums to dgamma / dbeta
-bool stem_wgrad_pb_ok(const WGradArgs& a, int P2, int Q2);
-int stem_wgrad_pb(WGradArgs a, const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z,
-                  const float* mean, const float* rstd, const float* gamma, const float* beta,
-                  const float* sums, float* dgamma, float* dbeta, int P2, int Q2,
-                  hipStream_t s);
-// stem_wgrad_pb + the slab reduction into a.dw; false (nothing launched) if not eligible
-bool igemm_wgrad_stem_pb(WGradArgs a, const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z,
-                         const float* mean, const float* rstd, const float* gamma,
-                         const float* beta, const float* sums, float* dgamma, float* dbeta,
-                         int P2, int Q2, hipStream_t s);
-// (sum g, sum g * xhat) of a fused stem BN + ReLU + max-pool backward from pooled tensors
-// only (dp, zsel); ws holds maxpool_bn_ws_floats floats, the sums land in ws[0 : 2C]
-void maxpool_bn_sel_sums(const bf16_raw* dp, const bf16_raw* zsel, const float* mean,
-                         const float* rstd, const float* gamma, const float* beta, int C, int MP,
-                         float* ws, hipStream_t s);
 bool conv3_halo_wgrad_ok(const WGradArgs& a);
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);

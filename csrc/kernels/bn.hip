@@ -34,46 +34,18 @@ __device__ __forceinline__ ColMap colmap(int cpr) {
   return m;
 }
 
-// Tuning knobs (tools/bench_bn.py): MPA_BN_GRID = target block count, MPA_BN_UNR = rows in
-// flight per thread (1, 2 or 4).  Default 2: in the batch-512 ResNet-18 step (gpu_ab.sh,
-// two alternating repeats) UNR 2 runs 13.47 ms/step against 13.63 (UNR 1) and 13.49 (UNR 4).
-static int bn_grid_target() {  // 0: size-based default
-  static const int v = [] {
-    const char* e = getenv("MPA_BN_GRID");
-    return e ? std::max(64, atoi(e)) : 0;
-  }();
-  return v;
-}
-static int bn_unr() {
-  static const int v = [] {
-    const char* e = getenv("MPA_BN_UNR");
-    const int u = e ? atoi(e) : 2;
-    return (u == 1 || u == 4) ? u : 2;
-  }();
-  return v;
-}
+// Rows in flight per thread: 2 (batch-512 ResNet-18 step 13.47 ms against 13.63 with 1
+// and 13.49 with 4, round 1 gpu_ab.sh, two alternating repeats).
 // as BN_LAUNCH, for kernels with a second (bool) template parameter
-#define BN_LAUNCH_T(kern, T, grid, ...)                                                   \
-  do {                                                                                    \
-    const int u_ = bn_unr();                                                              \
-    if (u_ == 4) hipLaunchKernelGGL((kern<4, T>), grid, dim3(256), 0, __VA_ARGS__);       \
-    else if (u_ == 2) hipLaunchKernelGGL((kern<2, T>), grid, dim3(256), 0, __VA_ARGS__);  \
-    else hipLaunchKernelGGL((kern<1, T>), grid, dim3(256), 0, __VA_ARGS__);               \
-  } while (0)
-#define BN_LAUNCH(kern, grid, ...)                                                        \
-  do {                                                                                    \
-    const int u_ = bn_unr();                                                              \
-    if (u_ == 4) hipLaunchKernelGGL(kern<4>, grid, dim3(256), 0, __VA_ARGS__);            \
-    else if (u_ == 2) hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, __VA_ARGS__);       \
-    else hipLaunchKernelGGL(kern<1>, grid, dim3(256), 0, __VA_ARGS__);                    \
-  } while (0)
+#define BN_LAUNCH_T(kern, T, grid, ...) \
+  hipLaunchKernelGGL((kern<2, T>), grid, dim3(256), 0, __VA_ARGS__)
+#define BN_LAUNCH(kern, grid, ...) hipLaunchKernelGGL(kern<2>, grid, dim3(256), 0, __VA_ARGS__)
 
 // Default block count, measured on the ResNet-18 batch-256 shapes (tools/bench_bn.py,
 // profiles/bn_grid_sweep.txt): 512 blocks stream 5.5 TB/s on the 411 MB stem activations
 // (1024: 5.2, 2048: 4.7 - more blocks only add slab rows and tail waves); tensors under
 // 2M 16-B chunks (layer3/4) are tail-bound and fastest at 256.
 static dim3 grid_for(int M, int C, int target = 0) {
-  if (target <= 0) target = bn_grid_target();
   if (target <= 0) target = ((int64_t)M * (C / 8) >= (2 << 20)) ? 512 : 256;
   const int cpr = C / 8;
   const int gy = (cpr + 255) / 256;
@@ -1682,21 +1654,13 @@ void bn_bwd(const bf16_raw* dy, const bf16_raw* x, const bf16_raw* y, const floa
             ldx, lddy);
   slab_reduce(slab, gr.x, 2 * C, ws, false, s);
   if (gacc) {  // dense-block accumulator: dx added into gacc (no ymask, no g)
-    const int u = bn_unr();
     const dim3 ga = grid_for(M, C);
 #define BN_ACC_LAUNCH(U, A)                                                                 \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<U, false, A>), ga, dim3(256), 0, s, dy, x, y, mean, \
                      rstd, gamma, zb, ws, dgamma, dbeta, M, C, (bf16_t*)nullptr,             \
                      (bf16_t*)nullptr, (const uint8_t*)nullptr, ldx, gacc, ldg, C, lddy)
-    if (gacc_bf16) {
-      if (u == 4) BN_ACC_LAUNCH(4, 2);
-      else if (u == 2) BN_ACC_LAUNCH(2, 2);
-      else BN_ACC_LAUNCH(1, 2);
-    } else {
-      if (u == 4) BN_ACC_LAUNCH(4, 1);
-      else if (u == 2) BN_ACC_LAUNCH(2, 1);
-      else BN_ACC_LAUNCH(1, 1);
-    }
+    if (gacc_bf16) BN_ACC_LAUNCH(2, 2);
+    else BN_ACC_LAUNCH(2, 1);
 #undef BN_ACC_LAUNCH
   } else if (ymask)
     BN_LAUNCH_T(bn_bwd_apply_kernel, true, grid_for(M, C), s, dy, x, y, mean, rstd, gamma, zb, ws,
@@ -1790,11 +1754,8 @@ void relu_fwd(const bf16_raw* x, int64_t n, bf16_raw* y, hipStream_t s) {
 // grid targets of the fused stem kernels (forward, backward reduce, backward apply); the
 // gathers are latency-bound, so they want more waves in flight than the streaming passes
 static int stem_grid(int which) {
-  static const int v[3] = {
-      [] { const char* e = getenv("MPA_STEM_GRID_F"); return e ? atoi(e) : 1024; }(),
-      [] { const char* e = getenv("MPA_STEM_GRID_R"); return e ? atoi(e) : 1024; }(),
-      [] { const char* e = getenv("MPA_STEM_GRID_A"); return e ? atoi(e) : 4096; }()};
-  return std::max(64, v[which]);
+  static const int v[3] = {1024, 1024, 4096};
+  return v[which];
 }
 
 void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gamma,
@@ -1816,16 +1777,6 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
 
 int64_t maxpool_bn_ws_floats(int M, int C) {
   return (int64_t)grid_for(M, C, stem_grid(1)).x * 2 * C + 2 * C;
-}
-
-void maxpool_bn_sel_sums(const bf16_raw* dp, const bf16_raw* zsel, const float* mean,
-                         const float* rstd, const float* gamma, const float* beta, int C, int MP,
-                         float* ws, hipStream_t s) {
-  float* slab = ws + 2 * C;
-  const dim3 gr = grid_for(MP, C, stem_grid(1));
-  hipLaunchKernelGGL(maxpool_bn_bwd_sel_reduce_kernel, gr, dim3(256), 0, s, dp, zsel, mean, rstd,
-                     gamma, beta, C, MP, slab, ws);
-  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
 }
 
 void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,

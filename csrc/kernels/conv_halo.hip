@@ -62,7 +62,6 @@ struct HaloPlan {
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;  // floor(2^32 / d) + 1: exact n / d for n*d < 2^32
   int tiles_m, tiles_total, cc;
   uint32_t a_bytes, b_bytes;
-  int dbg;              // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
 };
 
 __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
@@ -361,7 +360,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     // stage k & 1 (every producer has waited for its DMAs) and frees stage (k + 1) & 1 (every
     // MFMA wave is done with item k - 1), so item k + 1's DMAs go out right behind it and get
     // the whole of item k to land.  The MFMA waves' instruction streams carry no DMA at all:
-    // issuing the 18 per item between the MFMAs cost those waves ~10 % (MPA_HALO_DBG=1 A/B,
+    // issuing the 18 per item between the MFMAs cost those waves ~10 % (round-2 A/B,
     // docs/KERNELS.md), waiting for them nothing measurable.  Barrier count per wave:
     // nitems (+1 for the statistics flush) on both sides.
     if (wave_all >= HB_NW) {
@@ -372,7 +371,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
           if (++cc1 == CC) cc1 = 0;
           if (k + 1 < nitems) {
             if (cc1 == 0) prep_tile((k + 1) / CC);
-            if (!h.dbg) issue(cc1, (k + 1) & 1);
+            issue(cc1, (k + 1) & 1);
           }
         }
       });
@@ -557,7 +556,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
         if (more && cc1 == 0) prep_tile(tk + 1);
       }
       auto nd = [&](auto j) {
-        if (more && !h.dbg) dma(cc1, st ^ 1, j);
+        if (more) dma(cc1, st ^ 1, j);
       };
       if (cc == 0) {
         const int img0 = m0 / HW;
@@ -956,7 +955,6 @@ struct HaloWPlan {
   uint32_t mag_w, mag_w2, mag_h1, mag_hw;
   int tiles_m, parts, kparts, Z;
   uint32_t dy_bytes, x_bytes;
-  int dbg;  // MPA_HALO_DBG bit 0: skip the in-loop DMAs (timing diagnostics only)
   // STRIP: tiles of tr rows x tw columns of one image (w2 = tw + 2 rounded up to 16), for
   // images too wide for the 128-pixel linear tiles' halo (VGG 224^2 / 112^2)
   int tr, tw, tiles_c, tiles_img;
@@ -1201,10 +1199,6 @@ static bool g_halo = [] {
   return !(e && e[0] == '0');
 }();
 void igemm_set_halo(int on) { g_halo = on != 0; }
-static const int g_halo_dbg = [] {
-  const char* e = getenv("MPA_HALO_DBG");
-  return e ? atoi(e) : 0;
-}();
 bool igemm_halo_enabled() { return g_halo; }
 
 static uint32_t magic(uint32_t d) { return (uint32_t)((1ull << 32) / d + 1); }
@@ -1485,7 +1479,6 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
     if (use_strip(a, linear)) return conv3_strip(a, s);
   }
   HaloPlan h{};
-  h.dbg = g_halo_dbg & 1;
   const int W2 = halo_pitch(a.aW);
   h.w2 = W2;
   for (int t = 0; t < 9; ++t) {  // raster (dh, dw) order, whatever order the table had
@@ -1608,7 +1601,6 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
 // slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   HaloWPlan h{};
-  h.dbg = g_halo_dbg & 1;
   if (!halo_wgrad_geom(a) && halo_wgrad_strip_plan(a, h)) {
     const int W2 = h.w2;
     for (int t = 0; t < 9; ++t) h.toff[t] = (t / 3 - 1) * W2 + (t % 3 - 1);

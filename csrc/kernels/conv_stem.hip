@@ -215,13 +215,8 @@ bool conv_stem_ok(const IGemmArgs& a) {
   return true;
 }
 
-// block shape: 0 = 8 waves x 8-row items, one block per CU; 1 = 4 waves x 4-row items, two
-// blocks per CU (one block's barrier / LDS-commit phase overlaps the other's MFMAs).
-// Measured equal at batch 512 (37.96k vs 38.01k img/s), so the default is the simpler 0.
-static int g_stem_cfg = [] {
-  const char* e = getenv("MPA_STEM_CFG");
-  return e ? atoi(e) : 0;
-}();
+// block shape: 8 waves x 8-row items, one block per CU (4 waves x 4-row items, two blocks
+// per CU, measured equal at batch 512 - 37.96k vs 38.01k img/s - and was removed)
 
 template <int NW, int ROWS, int OCC>
 static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
@@ -238,7 +233,6 @@ static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
 
 int conv_stem(IGemmArgs a, hipStream_t s) {
   // one statistics-slab row per block: the caller's slab holds >= slab_rows_max(M) rows
-  if (g_stem_cfg == 1 && (a.M + 127) / 128 >= 512) return launch_stem<4, 4, 2>(a, 512, s);
   return launch_stem<8, 8, 1>(a, std::min(HALO_MAX_ROWS, active_cus()), s);
 }
 
@@ -408,277 +402,6 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       const int j = wave + 4 * i;
       *(f32x4*)(dst + (16 * km + li) * 224 + 16 * j + 4 * g) = acc[km][i];
     }
-}
-
-// ======================================================================================
-//  Stem weight gradient with the stem's max-pool + BN + ReLU backward computed on the fly.
-//  The stem's z gradient (dz, [N][112][112][64] at 224^2: 1.6 GB at batch 1024) feeds ONLY
-//  this weight gradient (the image needs no gradient), so instead of a cell pass that
-//  writes dz and this kernel re-reading it, the staging step of each item builds the dz
-//  tile itself: it loads z (in place of dz - the same bytes) and the two pooled rows the
-//  item's two output rows map to (dp + argmax, 4x smaller), and computes
-//    dz = a g + b + c z,  g = sum of dp over the 3x3/s2/p1 windows whose argmax is this
-//    pixel, masked by bn(z) > 0  (maxpool_bn_bwd_cell_kernel's arithmetic)
-//  with the (sum g, sum g*xhat) of the pooled-only reduction (maxpool_bn_bwd_sel_reduce).
-//  An item's rows 2p, 2p+1 are covered by pooled rows p (taps 1 / 2) and p+1 (tap 0):
-//  those rows are staged raw in LDS once per item.  Block 0 folds the sums into the BN
-//  parameter gradients.  Saves the 2 x 1.6 GB write + read of dz.
-// ======================================================================================
-struct StemPoolBN {
-  const bf16_t* dp;       // pooled gradient [N][P2][Q2][64]
-  const uint8_t* idx;     // window argmax (kh * 3 + kw) per channel, same shape
-  const bf16_t* z;        // stem conv output [N][P][Q][64] (dz's shape)
-  const float* mean;      // BN batch statistics, affine
-  const float* rstd;
-  const float* gamma;
-  const float* beta;
-  const float* sums;      // [2][64]: sum g | sum g * xhat
-  float* dgamma;          // += sum g * xhat (nullable)
-  float* dbeta;           // += sum g (nullable)
-  int P2, Q2;
-  float invM;             // 1 / (N P Q)
-};
-constexpr int SP_Q2 = 64;                                 // pooled columns per row (max)
-constexpr int SP_POOL = 2 * SP_Q2 * 128 + 2 * SP_Q2 * 64;  // dp + argmax of 2 pooled rows
-
-template <int KS>
-__global__ __launch_bounds__(256, 1) void stem_wgrad_pb_kernel(WGradArgs p, StemWPlan h,
-                                                               StemPoolBN pb) {
-  __shared__ __attribute__((aligned(16))) char smem[SW_LDS + SP_POOL];
-  char* const pdp = smem + SW_LDS;                 // [2][Q2][64] bf16
-  char* const pix = pdp + 2 * SP_Q2 * 128;         // [2][Q2][64] u8
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W, P2 = pb.P2, Q2 = pb.Q2;
-  const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
-  const int nfr = wave < 2 ? 4 : 3;
-
-  if (blockIdx.x == 0 && tid < 64) {  // BN parameter gradients (maxpool_bn_bwd_cell's)
-    if (pb.dgamma) pb.dgamma[tid] += pb.sums[64 + tid];
-    if (pb.dbeta) pb.dbeta[tid] += pb.sums[tid];
-  }
-  // this thread's 8 channels: every staging vector v = tid + 256 i has chunk v & 7 = tid & 7
-  const int c0 = (tid & 7) * 8;
-  float sc[8], sh[8], ca[8], cb[8], cc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float rs = pb.rstd[c0 + j], mu = pb.mean[c0 + j];
-    sc[j] = pb.gamma[c0 + j] * rs;
-    sh[j] = pb.beta[c0 + j] - mu * sc[j];
-    const float sg = pb.sums[c0 + j], sgx = pb.sums[64 + c0 + j];
-    ca[j] = sc[j];
-    cc[j] = -sc[j] * rs * sgx * pb.invM;
-    cb[j] = -sc[j] * sg * pb.invM - cc[j] * mu;
-  }
-
-  int bb[KS][2];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int pl = min(32 * ks + 8 * g + qd + 4 * e, 2 * Q - 1);
-      const int prow = pl >= Q ? 1 : 0;
-      const int ow = pl - prow * Q;
-      bb[ks][e] = ((2 * prow) * Wc + ow + (pp >> 1)) * 16 + (pp & 1) * 8;
-    }
-  int dzoff[KS];
-#pragma unroll
-  for (int i = 0; i < KS; ++i) {
-    const int v = tid + 256 * i, row = v >> 3, chunk = v & 7;
-    dzoff[i] = (row >> 5) * 4096 + mn_off<64>(row & 31, chunk * 8);
-  }
-  const u32x4* const zsrc = (const u32x4*)pb.z;     // [pix][8 vectors], dz's layout
-  const u32x4* const cvsrc = (const u32x4*)p.x;
-  constexpr int PV = (2 * SP_Q2 * 8 + 255) / 256;   // pooled vectors per thread (4)
-  u32x4 pz[KS], pcv[SW_CVPT], pdv[PV];
-  uint2 piv[PV];
-  int cur_nval = 0, cur_p0 = 0;
-  auto fetch = [&](int it) {
-    const int n = it / h.items_img, oh0 = (it - n * h.items_img) * 2;
-    const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
-    const size_t cv0 = ((size_t)n * Hc + 2 * oh0) * Wc;
-    const int cvlim = min(SW_CROWS, Hc - 2 * oh0) * Wc;
-#pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const int v = tid + 256 * i;
-      pz[i] = (v >> 3) < nval ? zsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
-                              : u32x4{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int i = 0; i < SW_CVPT; ++i) {
-      const int v = tid + 256 * i;
-      pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
-    }
-    // pooled rows oh0/2 and oh0/2 + 1 of image n: vector v -> (row r, column q, chunk)
-    const int p0 = oh0 >> 1;
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / (Q2 * 8), rem = v - r * (Q2 * 8);
-      const bool ok = r < 2 && p0 + r < P2;
-      const size_t o = (((size_t)n * P2 + p0 + r) * Q2) * 64 + (size_t)rem * 8;
-      pdv[i] = ok ? *(const u32x4*)(pb.dp + o) : u32x4{0u, 0u, 0u, 0u};
-      piv[i] = ok ? *(const uint2*)(pb.idx + o) : make_uint2(~0u, ~0u);
-    }
-    cur_nval = nval;
-    cur_p0 = p0;
-  };
-  auto commit = [&](int stage) {
-    char* st = smem + stage * SW_STAGE;
-    // 1. the raw pooled rows to the shared scratch (every thread reads any of them)
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int v = tid + 256 * i;
-      if (v < 2 * Q2 * 8) {
-        *LDS_PTR(u32x4, pdp + v * 16) = pdv[i];
-        *LDS_PTR(uint64_t, pix + v * 8) = ((uint64_t)piv[i].y << 32) | piv[i].x;
-      }
-    }
-    __syncthreads();
-    // 2. this thread's dz vectors of the item (output row oh0 + prow, column ow)
-#pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const int v = tid + 256 * i;
-      const int pl = v >> 3;
-      float dz[8];
-      if (pl < cur_nval) {
-        const int prow = pl >= Q ? 1 : 0;  // = row parity (oh0 is even)
-        const int ow = pl - prow * Q;
-        const int b0 = ow & 1, q = ow >> 1;
-        float zr[8], gr[8];
-        unpack8(__builtin_bit_cast(uint4, pz[i]), zr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gr[j] = 0.f;
-        // pooled neighbours: rows {0: tap 1 + prow} (+ {1: tap 0} if prow), columns
-        // {q: tap 1 + b0} (+ {q + 1: tap 0} if b0) - maxpool_bn_bwd_cell_kernel<*, 1>
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int du = u >> 1, eu = u & 1;
-          if ((du && !prow) || (eu && !b0)) continue;
-          const int qq = q + eu;
-          if (qq >= Q2 || (du && cur_p0 + 1 >= P2)) continue;
-          const int ti = du ? 0 : 1 + prow, tk = eu ? 0 : 1 + b0;
-          const int me = ti * 3 + tk;
-          const int off = (du * Q2 + qq) * 8 + (tid & 7);  // pooled vector index
-          float d[8];
-          unpack8(__builtin_bit_cast(uint4, *LDS_PTR(const u32x4, pdp + off * 16)), d);
-          const uint64_t iw64 = *LDS_PTR(const uint64_t, pix + off * 8);
-          const uint2 iw = make_uint2((uint32_t)iw64, (uint32_t)(iw64 >> 32));
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t word = j < 4 ? iw.x : iw.y;
-            if ((int)((word >> (8 * (j & 3))) & 0xff) == me) gr[j] += d[j];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float gj = (zr[j] * sc[j] + sh[j] > 0.f) ? gr[j] : 0.f;
-          dz[j] = ca[j] * gj + cb[j] + cc[j] * zr[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dz[j] = 0.f;
-      }
-      // (bf16-rounded like the dz tensor the unfused path writes and re-reads)
-      *LDS_PTR(u32x4, st + dzoff[i]) = __builtin_bit_cast(u32x4, pack8(dz));
-    }
-#pragma unroll
-    for (int i = 0; i < SW_CVPT; ++i) {
-      const int v = tid + 256 * i;
-      if (v < SW_CVV) *LDS_PTR(u32x4, st + SW_DZ + v * 16) = pcv[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int km = 0; km < 4; ++km)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[km][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto load_frags = [&](const char* sdz, const char* scv, int ks, bf16x8 (&af)[4],
-                        bf16x8 (&bf)[4]) {
-#pragma unroll
-    for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sdz + ks * 4096, 16 * km, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = min(wave + 4 * i, 13);
-      const int toff = ((j >> 1) * Wc + 2 * (j & 1)) * 16;
-      const s16x4 lo =
-          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][0] + toff));
-      const s16x4 hi =
-          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][1] + toff));
-      s16x8 r;
-      r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-      r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-      bf[i] = __builtin_bit_cast(bf16x8, r);
-    }
-  };
-
-  const int G = gridDim.x;
-  int it = blockIdx.x;
-  if (it < h.items) {
-    fetch(it);
-    commit(0);
-  }
-  for (int k = 0; it < h.items; ++k, it += G) {
-    const int st = k & 1;
-    __syncthreads();  // item k's stage written; every wave is done with item k-1's stage
-    const bool more = it + G < h.items;
-    if (more) fetch(it + G);
-    const char* sdz = smem + st * SW_STAGE;
-    const char* scv = sdz + SW_DZ;
-    bf16x8 af[2][4], bf[2][4];
-    load_frags(sdz, scv, 0, af[0], bf[0]);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) load_frags(sdz, scv, ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int km = 0; km < 4; ++km)
-          acc[km][i] = mfma16(bf[ks & 1][i], af[ks & 1][km], acc[km][i]);
-    }
-    if (more) commit(st ^ 1);  // (its scratch barrier: every wave has passed item k's)
-  }
-  float* dst = p.slab + (size_t)blockIdx.x * 64 * 224;
-#pragma unroll
-  for (int km = 0; km < 4; ++km)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= nfr) break;
-      const int j = wave + 4 * i;
-      *(f32x4*)(dst + (16 * km + li) * 224 + 16 * j + 4 * g) = acc[km][i];
-    }
-}
-
-// 3x3 / stride 2 / pad 1 pool over an even stem output, 64 channels, pooled width <= 64
-bool stem_wgrad_pb_ok(const WGradArgs& a, int P2, int Q2) {
-  return stem_wgrad_ok(a) && a.Kout == 64 && a.P % 2 == 0 && a.Q % 2 == 0 && P2 == a.P / 2 &&
-         Q2 == a.Q / 2 && Q2 <= SP_Q2;
-}
-
-// partials into a.slab ([Z][64][224]); returns Z
-int stem_wgrad_pb(WGradArgs a, const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z,
-                  const float* mean, const float* rstd, const float* gamma, const float* beta,
-                  const float* sums, float* dgamma, float* dbeta, int P2, int Q2,
-                  hipStream_t s) {
-  StemWPlan h{};
-  const int nimg = a.Mpix / (a.P * a.Q);
-  h.items_img = (a.P + 1) / 2;
-  h.items = nimg * h.items_img;
-  h.ks = (2 * a.Q + 31) / 32;
-  StemPoolBN pb{(const bf16_t*)dp, idx, (const bf16_t*)z, mean, rstd, gamma, beta, sums,
-                dgamma, dbeta, P2, Q2, 1.f / (float)a.Mpix};
-  const int grid = std::max(1, std::min(h.items, std::min(HALO_MAX_ROWS, active_cus())));
-  switch (h.ks) {
-#define SP_CASE(K)                                                                       \
-  case K:                                                                                \
-    hipLaunchKernelGGL(stem_wgrad_pb_kernel<K>, dim3(grid), dim3(256), 0, s, a, h, pb);  \
-    break;
-    SP_CASE(1) SP_CASE(2) SP_CASE(3) SP_CASE(4) SP_CASE(5) SP_CASE(6) SP_CASE(7) SP_CASE(8)
-#undef SP_CASE
-  }
-  return grid;
 }
 
 bool stem_wgrad_ok(const WGradArgs& a) {

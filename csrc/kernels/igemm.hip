@@ -531,15 +531,8 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(
 // ======================================================================================
 // Occupancy target (waves per SIMD) for the MFMA kernels: 3 fits every tile in <= 168
 // VGPRs with no spills (accumulators move from AGPRs to VGPRs); 4 (<= 128 VGPRs) spills a
-// few registers on the large tiles.  MPA_IGEMM_OCC selects it (tuning).
-static int occ_target() {
-  static int v = [] {
-    const char* e = getenv("MPA_IGEMM_OCC");
-    const int o = e ? atoi(e) : 3;
-    return (o == 2 || o == 4) ? o : 3;
-  }();
-  return v;
-}
+// few registers on the large tiles.
+static int occ_target() { return 3; }
 
 // Staging engine for 16-B-granular operands: 0 = register-staged (this file),
 // 1 = tuned default: LDS-DMA (igemm_dma.hip) for the rows GEMMs (fwd / dgrad / linear);
@@ -776,16 +769,12 @@ static std::string rows_key(const IGemmArgs& a, bool bkc, bool split) {
 static const int kRowsCands[][2] = {{128, 128}, {256, 128}, {128, 64}, {256, 64}, {128, 32},
                                     {256, 256}};
 
-// MPA_TUNE_256=1 adds the 8-wave 256 x 256 tile to the rows autotuner's candidates.  Off:
-// same-box A/B, round 3 - ResNet-18 b1024 47.73k/47.89k vs 47.67k/47.85k img/s, Inception
-// 7.24k vs 7.26k, ResNet-34 25.35k vs 25.39k (noise), for a longer first-step tuning pass.
-static const bool g_tune256 = [] {
-  const char* e = getenv("MPA_TUNE_256");
-  return e && atoi(e) == 1;
-}();
+// The 8-wave 256 x 256 rows tile is not an autotuner candidate: same-box A/B, round 3 -
+// ResNet-18 b1024 47.73k/47.89k vs 47.67k/47.85k img/s, Inception 7.24k vs 7.26k,
+// ResNet-34 25.35k vs 25.39k (noise) - for a longer first-step tuning pass.
 
 static bool rows_cand_ok(int bm, int bn, int N) {
-  if (bm == 256 && bn == 256 && (!g_tune256 || N <= 128)) return false;
+  if (bm == 256 && bn == 256) return false;
   if (bn == 128 && N <= 64) return false;  // half-empty tiles
   if (bn == 64 && (N <= 32 || N > 1024)) return false;
   if (bn == 32 && N > 32) return false;
@@ -1186,20 +1175,6 @@ static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s
     if (t < best) { best = t; tbm = c[0]; tbn = c[1]; }
   }
   if (tbm) tuned_store(key, tbm, tbn);
-}
-
-bool igemm_wgrad_stem_pb(WGradArgs a, const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z,
-                         const float* mean, const float* rstd, const float* gamma,
-                         const float* beta, const float* sums, float* dgamma, float* dbeta,
-                         int P2, int Q2, hipStream_t s) {
-  if (igemm_engine() < 1 || !stem_wgrad_pb_ok(a, P2, Q2)) return false;
-  const int z_ = stem_wgrad_pb(a, dp, idx, z, mean, rstd, gamma, beta, sums, dgamma, dbeta, P2,
-                               Q2, s);
-  const int64_t n = (int64_t)a.Kout * a.Ncols;
-  const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z_, n, a.dw,
-                     a.overwrite);
-  return true;
 }
 
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {

@@ -223,29 +223,19 @@ __global__ __launch_bounds__(256) void ce_loss_sum_kernel(const float* __restric
   }
   if (threadIdx.x == 0) {
     const float v = weight * red[0];
-    if (accumulate == 2) atomicAdd(loss, v);  // (diagnostics: MPA_DIAG_CE_MEMSET)
-    else if (accumulate) *loss += v;
+    if (accumulate) *loss += v;
     else *loss = v;
     if (acc) *acc += v;  // the trainer's running loss sum (one host sync per epoch)
   }
 }
 
-// Diagnostics only (MPA_DIAG_CE_MEMSET=1): the round-2 form of the loss - a memset of the
-// scalar followed by an atomic accumulation into it - for the HIP-graph replay A/B of
-// tools/graph_bisect.py (docs/NOTES.md "HIP graph replay")
-static bool g_diag_memset = [] {
-  const char* e = getenv("MPA_DIAG_CE_MEMSET");
-  return e && e[0] == '1';
-}();
-
 // loss: [1 + B] floats - the mean loss at [0], the per-row terms after it
 void ce_fwd(const bf16_raw* logits, const int64_t* labels, int B, int NC, int ld, float* loss,
             float* lse, hipStream_t s) {
   float* rows = loss + 1;
-  if (g_diag_memset) (void)hipMemsetAsync(loss, 0, sizeof(float), s);
   ce_fwd_rows(logits, labels, B, NC, ld, rows, lse, s);
   hipLaunchKernelGGL(ce_loss_sum_kernel, dim3(1), dim3(256), 0, s, rows, B, loss,
-                     g_diag_memset ? 2 : 0, 1.f, (float*)nullptr);
+                     0, 1.f, (float*)nullptr);
 }
 
 // out[0] = (or +=) weight * mean CE; acc[0] += the same (when acc is set).  rows: B floats of

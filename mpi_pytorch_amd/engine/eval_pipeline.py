@@ -390,8 +390,13 @@ def run_pipeline(cfg: Config, ckpt_path: Optional[str] = None, max_images: int =
     total = reduce_scalar(acc_local, root=0)
     if world.rank == 0:
         log.info("Accuracy is {}".format(total))
-        log.info("_Throughput: {:.1f} img/s ({} images, {} lanes x {} ranks)".format(
-            dataset_size / dt if dt > 0 else 0.0, dataset_size, pipe.lanes, world.world_size))
+        # the source extent is part of the number: a synthetic source at the model's input
+        # size skips the downscale real ~1000x677 herbarium JPEGs need (cfg.eval_src)
+        src = "real images" if isinstance(source, FolderImages) else \
+            "synthetic {}x{} source".format(*source.hw)
+        log.info("_Throughput: {:.1f} img/s ({} images, {} lanes x {} ranks, {})".format(
+            dataset_size / dt if dt > 0 else 0.0, dataset_size, pipe.lanes, world.world_size,
+            src))
     return float(total) if total is not None else acc_local
 
 

@@ -55,11 +55,6 @@ def loss_fn(out, labels, acc=None):
     return Fn.cross_entropy(out, labels, acc=acc)
 
 
-# MPA_EARLY_HEAD_OPT=1: the classifier's optimizer update runs on a side stream under the
-# rest of the backward.  Off by default: on one MI355X the concurrent streaming update slows
-# the backward it overlaps by more than it hides (same-box A/B, profiles/early_head_ab_r3.txt:
-# ResNet-18 b1024 48.0k vs 48.2k, b128 28.1k vs 28.7k, Inception 6.99k vs 7.09k img/s).
-_EARLY_HEAD = os.environ.get("MPA_EARLY_HEAD_OPT", "0") == "1"
 # MPA_WGRAD_STREAM_DDP=1: side-stream weight gradients with several ranks too (the bucket
 # collectives then wait for both streams, GradBucketer._launch).  Off by default until the
 # 8-GPU run measures it (bench.py records both in its multi_gpu decisions)
@@ -205,58 +200,15 @@ class TrainStep:
         self._static_loss = None
         # Back-to-back replays need no host sync: in deterministic mode 100 replays equal
         # 100 eager steps bitwise (tests/test_determinism_gpu.py, tools/graph_bisect.py;
-        # docs/NOTES.md "HIP graph replay").  MPA_GRAPH_SYNC=1 restores a sync per replay.
-        self._sync_replay = os.environ.get("MPA_GRAPH_SYNC", "0") == "1"
+        # docs/NOTES.md "HIP graph replay").
         self.timer: Optional[StepTimer] = None
         # roctx ranges fwd / bwd / comm_wait / opt around the host enqueue of each phase
         # (rocprofv3 --marker-trace shows them beside the kernels); MPA_ROCTX=1
         self.markers = markers() if os.environ.get("MPA_ROCTX", "0") == "1" else None
-        # early classifier update: the arena's first bucket is the classifier (64,500-class
-        # heads: 75 % of ResNet-18's parameters); once its gradients are final (and, over
-        # RCCL, all-reduced) its optimizer update runs on a side stream under the rest of
-        # the backward instead of after it
         self.wgrad_stream_ddp = _WGRAD_DDP
-        self._head = self._early_head()
-        self._head_left = 0
-        self._head_launched = False
-        self._side = None
-        if self._head is not None:
-            self._side = torch.cuda.Stream(dev)
-            self.arena.add_listener(self._on_grad)
-
-    def _early_head(self):
-        if not _EARLY_HEAD or self.arena.device.type != "cuda":
-            return None
-        b = self.bucketer
-        if not b.buckets or b.comm_dtype == "bf16" or not hasattr(self.opt, "step_range"):
-            return None
-        if b.active and not b.overlap:  # (the head's all-reduce would only start at finish)
-            return None
-        from ..models.layers import Linear
-        lin = {id(p) for m in self.model.modules() if isinstance(m, Linear)
-               for p in m.parameters()}
-        lo, hi = b.ranges[0]
-        ps = b.buckets[0]
-        if lo != 0 or not all(id(p) in lin for p in ps) or hi < 0.2 * self.arena.n_train:
-            return None
-        return hi, {id(p) for p in ps}
-
-    def _on_grad(self, p) -> None:
-        """Arena listener: the classifier's last gradient landed (its dgrad was enqueued
-        before - _LinearAct.backward) -> its update goes out on the side stream, after
-        the compute stream's work so far and, with several ranks, after its all-reduce."""
-        if self._head_left <= 0 or id(p) not in self._head[1]:
-            return
-        self._head_left -= 1
-        if self._head_left:
-            return
-        self._side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._side):
-            w = self.bucketer._works[0] if self.bucketer.active else None
-            if w is not None:
-                w.wait()  # (the side stream waits for the bucket's all-reduce)
-            self.opt.step_range(self._head[0])
-        self._head_launched = True
+        # (an early classifier update on a side stream under the rest of the backward was
+        # measured slower on one MI355X - ResNet-18 b1024 48.0k vs 48.2k, Inception 6.99k vs
+        # 7.09k img/s, profiles/early_head_ab_r3.txt - and removed in round 5)
 
     def enable_timers(self) -> StepTimer:
         """Turn on per-phase HIP-event timing of eager steps (GPU only)."""
@@ -272,8 +224,6 @@ class TrainStep:
         if m is not None:
             m.range_push("fwd")
         self.arena.zero_grad()
-        if self._head is not None:
-            self._head_left = len(self._head[1])
         # (single GPU: an Inception block's longest branch chain may run on a second
         # stream, forward and backward; joined after the backward)
         single = self.bucketer is None or not self.bucketer.active
@@ -309,10 +259,6 @@ class TrainStep:
         if m is not None:
             m.range_pop()
             m.range_push("opt")
-        if self._head_launched:  # the step counter advances after both updates read it
-            torch.cuda.current_stream().wait_stream(self._side)
-            self._head_launched = False
-        self._head_left = 0
         self.opt.step()
         if t is not None:
             t.mark(4)
@@ -325,8 +271,6 @@ class TrainStep:
             self._static_x.copy_(x)
             self._static_y.copy_(y)
             self._graph.replay()
-            if self._sync_replay:
-                torch.cuda.current_stream().synchronize()
             loss = self._static_loss
         else:  # eager (also a short last batch of a graph-captured loop)
             loss = self._eager(x, y)

@@ -200,7 +200,7 @@ def run_training(cfg: Config) -> dict:
     # the reference's exact string (main.py:133 logs "CPU" whatever the device); the
     # actual compute device goes on a line of its own
     log.info("_Model loaded to CPU")
-    log.info("_Compute device: %s", dev)
+    log.debug("_Compute device: %s", dev)  # (no such line in the reference)
     log.info("_Entering training Loop")
 
     if cfg.step_timers:

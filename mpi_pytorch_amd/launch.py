@@ -48,16 +48,20 @@ def launch(nprocs: int, cmd, env_extra=None, timeout: float = 0.0) -> int:
     try:
         while True:
             alive = False
-            for p in procs:
+            for r, p in enumerate(procs):
                 code = p.poll()
                 if code is None:
                     alive = True
                 elif code != 0 and rc == 0:
                     rc = code
+                    sys.stderr.write("launch: rank %d exited with code %d; stopping the job\n"
+                                     % (r, code))
             if rc != 0 or not alive:
                 break
             if timeout and time.time() - t0 > timeout:
                 rc = 124
+                sys.stderr.write("launch: job exceeded its %.0f s limit; stopping ranks %s\n"
+                                 % (timeout, [r for r, p in enumerate(procs) if p.poll() is None]))
                 break
             time.sleep(0.1)
     finally:

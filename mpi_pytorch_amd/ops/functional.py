@@ -33,16 +33,6 @@ from ..parallel.arena import weight_of, weight_t_of, grad_sink, grad_done
 
 _EMPTY = {}
 _NO_SHIFT = os.environ.get("MPA_NO_STATS_SHIFT", "0") == "1"  # diagnostics only
-_NO_STEM_FUSE = os.environ.get("MPA_NO_STEM_FUSE", "0") == "1"  # A/B: unfused stem
-_NO_ZSEL = os.environ.get("MPA_NO_ZSEL", "0") == "1"  # A/B: stem backward reduce from full z
-# MPA_FUSE_STEM_BWD=1: the stem's max-pool + BN backward computed inside the stem
-# weight-gradient kernel's staging (dz never written).  Off by default: measured ~1 ms
-# SLOWER per ResNet-18 b1024 step than the separate cell backward + wgrad (48.5-48.7k vs
-# 49.6k img/s, profiles/ab_r4.txt) - the fused kernel runs at one wave per SIMD (256 VGPRs
-# + 147 AGPRs) and its dz build serialises with the staging.
-_FUSE_STEM_BWD = os.environ.get("MPA_FUSE_STEM_BWD", "0") == "1"
-# A/B: residual blocks' backward reads y for the ReLU mask instead of a 1-bit-per-element mask
-_NO_YMASK = os.environ.get("MPA_NO_YMASK", "0") == "1"
 
 
 def K(t: torch.Tensor):
@@ -94,26 +84,17 @@ def _done(*ps) -> None:
 # optimizer (join_wgrad_stream); x / dz are record_stream'ed so the caching allocator does
 # not hand their memory out while the side stream still reads it.
 _WGRAD_STREAM = os.environ.get("MPA_WGRAD_STREAM", "1") == "1"
-# MPA_STEM_WGRAD_STREAM=0: the fused stem's weight gradient stays on the compute stream
-_STEM_SIDE = os.environ.get("MPA_STEM_WGRAD_STREAM", "1") == "1"
-# MPA_FC_WGRAD_STREAM=1: Linear weight gradients on the side stream as well.  Off: same-box
-# A/B (profiles/ab_r4.txt call 21) VGG-16 +1.0 %, ResNet-18 +0.1 %, Inception -0.4 %,
-# AlexNet -4.7 % (its three large FC weight gradients then contend with the FC dgrads)
-_FC_SIDE = os.environ.get("MPA_FC_WGRAD_STREAM", "0") == "1"
+# (Linear weight gradients stay on the compute stream: on the side stream AlexNet lost
+# 4.7 %, its three large FC weight gradients contending with the FC dgrads; round-4 A/B,
+# profiles/ab_r4.txt call 21.)
 _SIDE = {"stream": None, "on": False, "used": False}
-# MPA_WGRAD_PRIO=-1: the side stream at high priority (HIP queue priority; A/B knob)
-_WGRAD_PRIO = int(os.environ.get("MPA_WGRAD_PRIO", "0"))
-# MPA_GRAPH_STREAMS=1: the side / branch streams fork from and join a HIP-graph capture
-# stream, and the graph keeps that concurrency (the allocator defers reuse of
-# record_stream'ed blocks until the capture ends; replay == eager bitwise,
-# tests/test_determinism_gpu.py).  Off by default: replaying the multi-stream graph measured
-# slower than the one-stream graph (DenseNet-121 8.93k vs 9.07k img/s), and both slower
-# than eager with streams (9.53k; profiles/ab_r4.txt call 15).
-_GRAPH_STREAMS = os.environ.get("MPA_GRAPH_STREAMS", "0") == "1"
 
 
 def _capture_blocks_streams() -> bool:
-    return not _GRAPH_STREAMS and torch.cuda.is_current_stream_capturing()
+    """A HIP-graph capture keeps one stream: replaying a multi-stream graph measured slower
+    than the one-stream graph, and both slower than eager with streams (DenseNet-121 8.93k /
+    9.07k / 9.53k img/s, profiles/ab_r4.txt call 15)."""
+    return torch.cuda.is_current_stream_capturing()
 
 
 def wgrad_stream_begin(enabled: bool = True) -> None:
@@ -150,7 +131,7 @@ def _run_wgrad(fn, *tensors) -> None:
     main = torch.cuda.current_stream()
     side = _SIDE["stream"]
     if side is None or side.device != t0.device:
-        side = _SIDE["stream"] = torch.cuda.Stream(t0.device, priority=_WGRAD_PRIO)
+        side = _SIDE["stream"] = torch.cuda.Stream(t0.device)
     side.wait_stream(main)
     # (set_stream / restore instead of the torch.cuda.stream context: ~20 us less host
     # time per weight gradient, which the host-bound small-batch step feels)
@@ -184,7 +165,7 @@ def branch_streams(enabled: bool) -> None:
 
 def branch_stream(x: torch.Tensor):
     """The stream a side branch reading ``x`` runs on, or None (off, CPU, no grad, or a
-    HIP-graph capture with MPA_GRAPH_STREAMS=0)."""
+    HIP-graph capture)."""
     if not (_BR["on"] and x.is_cuda and torch.is_grad_enabled()):
         return None
     if _capture_blocks_streams():
@@ -441,7 +422,7 @@ class _ConvBNAct(torch.autograd.Function):
         # relu(bn(z) + residual): the backward's ReLU mask as one bit per element, written by
         # the forward, so neither backward pass reads y (two activation-sized reads less)
         ymask = None
-        if relu and residual is not None and not _NO_YMASK:
+        if relu and residual is not None:
             ymask = torch.empty(z.numel() // 8, device=z.device, dtype=torch.uint8)
         if defer is not None:  # statistics only; the consumer applies this BN (BNDefer)
             mean, rstd, defer.aff = k.bn_stats_affine(z, stats, gamma, beta, bn.running_mean,
@@ -742,12 +723,10 @@ class _ConvBNReLUPool(torch.autograd.Function):
                        _empty(x) if _NO_SHIFT else bn.running_mean)
         # zsel: raw z at each window's argmax, so the backward's reduction pass reads only
         # pooled-size tensors (maxpool_bn_bwd_sel_reduce_kernel)
-        zsel = None
-        if not _NO_ZSEL:
-            N, H, W, C_ = z.shape
-            zsel = torch.empty(N, _pool_out(H, cfg[0], cfg[2], cfg[4], cfg[6]),
-                               _pool_out(W, cfg[1], cfg[3], cfg[5], cfg[6]), C_,
-                               device=z.device, dtype=z.dtype)
+        N, H, W, C_ = z.shape
+        zsel = torch.empty(N, _pool_out(H, cfg[0], cfg[2], cfg[4], cfg[6]),
+                           _pool_out(W, cfg[1], cfg[3], cfg[5], cfg[6]), C_,
+                           device=z.device, dtype=z.dtype)
         y, idx, mean, rstd = k.bn_relu_maxpool_fwd(z, stats, gamma, beta, bn.running_mean,
                                                    bn.running_var, bn.momentum_value(), bn.eps,
                                                    *cfg, bn.num_batches_tracked, zsel_out=zsel)
@@ -767,18 +746,6 @@ class _ConvBNReLUPool(torch.autograd.Function):
         k = K(dy)
         sh, sw, ph, pw = conv.kgeom
         dy = dy.contiguous()
-        if (dy.is_cuda and _FUSE_STEM_BWD and zsel is not None and w.requires_grad
-                and not ctx.needs_input_grad[0] and gamma is not None and beta is not None):
-            # the image needs no gradient, so dz feeds only the weight gradient: build it
-            # inside that kernel's staging instead of writing and re-reading it
-            if k.stem_wgrad_poolbn(dy, idx, z, zsel, mean, rstd, gamma, beta,
-                                   _sink(gamma, dy), _sink(beta, dy), x, w.grad, sh, sw, ph,
-                                   pw, _fresh(w)):
-                _done(gamma, beta)
-                conv.fix_grad(w.grad)
-                _done(w)
-                _done(ctx.bias)
-                return None, None, None, None, None, None, None, None
         dz = k.maxpool_bn_bwd(dy, idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
                               _sink(beta, dy), *ctx.cfg[:6], zsel=zsel)
         _done(gamma, beta)
@@ -787,10 +754,7 @@ class _ConvBNReLUPool(torch.autograd.Function):
                 k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
                 conv.fix_grad(w.grad)
                 _done(w)
-            if _STEM_SIDE:
-                _run_wgrad(wgrad, dz, x)
-            else:
-                wgrad()
+            _run_wgrad(wgrad, dz, x)
         _done(ctx.bias)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -803,7 +767,7 @@ def conv_bn_relu_maxpool(x, conv, bn, pool):
     """``pool(relu(bn(conv(x))))`` for a MaxPool2d ``pool``; fused in train mode."""
     cfg = (pool.kernel_size[0], pool.kernel_size[1], pool.stride[0], pool.stride[1],
            pool.padding[0], pool.padding[1], bool(pool.ceil_mode))
-    if bn.training and not _NO_STEM_FUSE and cfg[0] * cfg[1] <= 256:
+    if bn.training and cfg[0] * cfg[1] <= 256:
         x = conv.fit_input(x)
         return _ConvBNReLUPool.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, conv, bn,
                                      cfg)
@@ -1027,13 +991,8 @@ class _LinearAct(torch.autograd.Function):
               else None)
         _done(b)
         if w.requires_grad:
-            def wgrad():
-                k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
-                _done(w)
-            if _FC_SIDE:
-                _run_wgrad(wgrad, g, x)
-            else:
-                wgrad()
+            k.linear_wgrad(g, x, w.grad, overwrite=_fresh(w))
+            _done(w)
         return dx, None, None, None, None
 
 

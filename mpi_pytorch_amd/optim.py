@@ -44,7 +44,6 @@ class _FlatOptimizer:
         dev = arena.device
         self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
         self.grad_scale = 1.0
-        self._done_lo = 0  # [0, _done_lo) already updated this step (step_range)
         self.param_groups = [self._group_defaults()]
         self.param_groups[0]["params"] = self.params
 
@@ -65,14 +64,6 @@ class _FlatOptimizer:
 
     def _update(self, lo: int, hi: int) -> None:
         raise NotImplementedError
-
-    def step_range(self, hi: int) -> None:
-        """Update the arena prefix [0, hi) now (its gradients are final); the next
-        ``step()`` updates only the rest and then advances the step counter, so both
-        launches use the same step.  (TrainStep's early classifier update.)"""
-        if hi > 0:
-            self._update(0, hi)
-            self._done_lo = hi
 
     def _kernel(self):
         return Fn.K(self.arena.master)
@@ -139,9 +130,7 @@ class FusedAdam(_FlatOptimizer):
     def step(self) -> None:
         if self.arena.n_train == 0:
             return
-        lo, self._done_lo = self._done_lo, 0
-        if lo < self.arena.n_train:
-            self._update(lo, self.arena.n_train)
+        self._update(0, self.arena.n_train)
         self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):
@@ -184,9 +173,7 @@ class FusedSGD(_FlatOptimizer):
     def step(self) -> None:
         if self.arena.n_train == 0:
             return
-        lo, self._done_lo = self._done_lo, 0
-        if lo < self.arena.n_train:
-            self._update(lo, self.arena.n_train)
+        self._update(0, self.arena.n_train)
         self.arena.refresh_transposed(step_inc=self.step_t)
 
     def _param_state(self, p, o, e, step):

@@ -147,9 +147,11 @@ class GradBucketer:
         self._launch_stream = None  # (side-stream weight gradients under DP: _launch)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._wire: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
-        # [bucket, wire bytes, work (None once resolved), host t0, host t1 | resolved ms]
+        # [bucket, wire bytes, work (None once resolved), host t0, host t1 | resolved ms,
+        #  step number]
         self._stats: Optional[list] = None
         self._held = 0
+        self._steps_done = 0
         self.active = world_size > 1
         # RCCL reports each collective's own device time; other backends are host-timed
         self._host_timed = self.active and dist.is_initialized() and \
@@ -246,8 +248,10 @@ class GradBucketer:
         else:
             self._works[bi] = self._issue(bi, g, group)
         if self._stats is not None and len(self._stats) < self._MAX_STATS:
-            self._stats.append([bi, g.numel() * g.element_size(), self._works[bi],
-                                time.perf_counter(), None])
+            # bytes actually sent: the bf16 wire copy is made inside _issue(), g is the
+            # fp32 arena slice
+            self._stats.append([bi, g.numel() * self.wire_elem_bytes, self._works[bi],
+                                time.perf_counter(), None, self._steps_done])
             self._held += 1
             if self._held > self._MAX_HELD:
                 self._resolve_old()
@@ -285,6 +289,7 @@ class GradBucketer:
             # kernels enqueued from here on (optimizer, next forward) run after the waits
             _set_reserve(0)
             self._reserved = False
+        self._steps_done += 1  # every record of this step has been waited on
         self.reset()
 
     @property
@@ -314,14 +319,16 @@ class GradBucketer:
         that is a fresh bucket-sized tensor per launch - holding every step's Works until
         comm_stats() grew device memory by half the gradient size per step.  The records
         resolved here are steps old, so reading their duration does not stall the step."""
-        held = [r for r in self._stats if r[2] is not None]
-        for rec in held[: len(held) // 2]:
+        # only records of steps whose collectives finish() has already waited on: their
+        # device events are complete (RCCL) and their host end stamps set (gloo)
+        held = [r for r in self._stats if r[2] is not None and r[5] < self._steps_done]
+        for rec in held[: max(len(held) // 2, 1)]:
             rec[4] = self._duration_ms(rec)
             rec[2] = None
         self._held = sum(1 for r in self._stats if r[2] is not None)
 
     def _duration_ms(self, rec) -> Optional[float]:
-        bi, nbytes, work, t0, t1 = rec
+        bi, nbytes, work, t0, t1 = rec[:5]
         if t1 is not None and work is None:
             return t1
         if self._host_timed:

@@ -131,10 +131,12 @@ def pin_host_to_gpu(dev: torch.device, sysfs: str = "/sys/bus/pci/devices",
     device's PCI ``local_cpulist``.  One process per GPU on a two-socket node otherwise lets
     the scheduler place a rank's producers on the far socket, so its pinned ring slots and
     H2D copies cross the inter-socket link.  Kept within the CPUs the process may already
-    use (container / cgroup limits); a no-op when sysfs does not say (MPA_NUMA_PIN=0: off).
+    use (container / cgroup limits); a no-op when sysfs does not say.  Opt-in (MPA_NUMA_PIN=1)
+    until an 8-GPU run measures it: several ranks share a node's CPUs, and each torch
+    intra-op pool is still sized for the whole machine (the pool is capped below).
     Returns {"pci", "numa_node", "cpus"} or None."""
     global _AFFINITY
-    if os.environ.get("MPA_NUMA_PIN", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+    if os.environ.get("MPA_NUMA_PIN", "0") != "1" or not hasattr(os, "sched_setaffinity"):
         return None
     addr = addr or _pci_addr(dev)
     if addr is None:
@@ -159,7 +161,12 @@ def pin_host_to_gpu(dev: torch.device, sysfs: str = "/sys/bus/pci/devices",
         os.sched_setaffinity(0, cpus)
     except OSError:
         return None
-    _AFFINITY = {"pci": addr, "numa_node": node, "cpus": len(cpus)}
+    # the ranks of this node that share the pinned CPUs split them: cap the intra-op pool
+    sharing = max(_env_int("LOCAL_WORLD_SIZE", default=1), 1)
+    threads = max(len(cpus) // sharing, 1)
+    if torch.get_num_threads() > threads:
+        torch.set_num_threads(threads)
+    _AFFINITY = {"pci": addr, "numa_node": node, "cpus": len(cpus), "threads": threads}
     return _AFFINITY
 
 

@@ -98,3 +98,38 @@ def test_densenet_feature_buffer_block_matches_plain(gpu):
     # entries), in direction and norm they agree
     assert _cos(dx1, dx2) > 0.999 and abs(float(dx1.float().norm() / dx2.float().norm()) - 1) < 1e-2
     assert _cos(g1, g2) > 0.999 and abs(float(g1.norm() / g2.norm()) - 1) < 1e-2
+
+
+@pytest.mark.parametrize("name,cin,hw", [("denseblock1", 64, 28), ("denseblock3", 256, 14)])
+def test_densenet_bf16_block_gradient_accumulator(gpu, name, cin, hw, monkeypatch):
+    """The dense block's gradient accumulator G in bf16 (the default: each contribution
+    added in fp32 and rounded once) vs in fp32 (MPA_DENSE_GRAD_BF16=0), one whole
+    DenseNet-121 block (6 / 24 layers), same inputs and output gradient: the block-input
+    gradient and every parameter gradient agree in direction (cosine >= 0.999), in norm
+    and elementwise to a bounded relative error.  Reference model: torchvision
+    densenet121 reached from /root/reference/models.py:77."""
+    import mpi_pytorch_amd.models.densenet as D
+    torch.manual_seed(0)
+    model, _o, _s, _ = build_training("densenet", 100, gpu, World(device=gpu), 1e-3)
+    a = model._mpa_arena
+    blk = getattr(model.features, name)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x0 = torch.randn(16, hw, hw, cin, generator=g).to(gpu, torch.bfloat16)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    res = []
+    for bf16 in (True, False):
+        monkeypatch.setattr(D, "_GRAD_BF16", bf16)
+        blk.load_state_dict(sd)
+        a.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        out, _stats = blk(x, True)
+        w = torch.linspace(-1, 1, out.numel(), device=gpu).view_as(out)
+        (out.float() * w).sum().backward()
+        torch.cuda.synchronize()
+        res.append((x.grad.float().clone(), _param_grads(a, [blk])))
+    (dx_b, g_b), (dx_f, g_f) = res
+    assert float(dx_f.abs().max()) > 0 and float(g_f.abs().max()) > 0
+    assert _cos(dx_b, dx_f) > 0.999 and abs(float(dx_b.norm() / dx_f.norm()) - 1) < 5e-3
+    assert _cos(g_b, g_f) > 0.999 and abs(float(g_b.norm() / g_f.norm()) - 1) < 5e-3
+    assert _rel(dx_b, dx_f) < 3e-2, _rel(dx_b, dx_f)
+    assert _rel(g_b, g_f) < 3e-2, _rel(g_b, g_f)

@@ -1556,34 +1556,3 @@ def test_wgrad_overwrite(gpu, kind):
     assert rel(acc - junk, zero) < 1e-3
 
 
-@pytest.mark.parametrize("hw,N", [(224, 4), (64, 3)])
-def test_stem_wgrad_fused_pool_bn_backward(gpu, hw, N, monkeypatch):
-    """The stem's weight gradient with its max-pool + BN + ReLU backward computed inside
-    the weight-gradient kernel's staging (stem_wgrad_poolbn: dz never written) == the
-    unfused maxpool_bn_bwd -> conv_wgrad path (weight and BN parameter gradients), for
-    the ResNet stem (7x7/s2 pixel-pair conv -> BN -> ReLU -> 3x3/s2/p1 max-pool)."""
-    import mpi_pytorch_amd.ops.functional as F_
-    from mpi_pytorch_amd.engine import build_training
-    from mpi_pytorch_amd.parallel import World
-    torch.manual_seed(5)
-    model = build_training("resnet18", 10, gpu, World(device=gpu), 1e-3)[0]
-    x = (torch.randn(N, hw, hw, 8) * (torch.arange(8) < 3)).to(gpu, torch.bfloat16)
-    a = model._mpa_arena
-    ext = C()
-    real = ext.stem_wgrad_poolbn
-    ran = []
-    monkeypatch.setattr(ext, "stem_wgrad_poolbn", lambda *t: ran.append(real(*t)) or ran[-1])
-    grads = []
-    for fused in (True, False):
-        monkeypatch.setattr(F_, "_FUSE_STEM_BWD", fused)
-        a.zero_grad()
-        y = F_.conv_bn_relu_maxpool(x, model.conv1, model.bn1, model.maxpool)
-        g = torch.linspace(-1, 1, y.numel(), device=gpu).reshape(y.shape).to(y.dtype)
-        y.backward(g)
-        torch.cuda.synchronize()
-        grads.append([p.grad.clone() for p in (model.conv1.weight, model.bn1.weight,
-                                                model.bn1.bias)])
-    assert ran == [True], ran  # the fused kernel ran (no silent fallback)
-    for u, v in zip(*grads):
-        assert float(v.abs().max()) > 0
-        assert rel(u, v) < 1e-2, rel(u, v)

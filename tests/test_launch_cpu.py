@@ -66,6 +66,56 @@ def test_bench_rejects_rank_count_mismatch(tmp_path):
     assert r.returncode != 0 and "ranks" in (r.stderr + r.stdout)
 
 
+def _bench_cpu(tmp_path, inject, extra=(), timeout=300):
+    env = _env()
+    env["MPA_BENCH_INJECT"] = inject
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--image-size", "32", "--batch", "2", "--classes", "10", "--steps", "3",
+           "--warmup", "1"] + list(extra)
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=timeout)
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    return r, lines, time.time() - t0
+
+
+def test_bench_keeps_headline_when_a_variant_throws(tmp_path):
+    """Every multi-GPU decision variant raises: the headline line is still printed once,
+    each variant carries its error, and the job exits 0."""
+    r, lines, _ = _bench_cpu(tmp_path, "variant_raise")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["n_gpus"] == 2
+    mg = rec["multi_gpu"]
+    for k in ("comm_ctas8", "comm_bf16", "wgrad_stream_on"):
+        assert "injected variant failure" in mg[k]["error"]
+    assert mg["allreduce_probe"]["default"]["ms"] > 0
+
+
+def test_bench_prints_headline_when_extras_hang(tmp_path):
+    """The extras after the headline never finish: the extras budget prints the headline
+    record anyway (with extras_error) and every rank exits 0."""
+    r, lines, dt = _bench_cpu(tmp_path, "extras_hang", ["--extras-budget", "5"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and "timeout" in rec["extras_error"]
+
+
+def test_bench_hanging_rank_exits_rank_tagged_nonzero(tmp_path):
+    """Rank 1 stops before its second timed step (its peer blocks in the all-reduce): the
+    device-progress watchdog ends the job with exit 75 and a rank-tagged message well
+    inside the driver's command limit, and no headline line is printed."""
+    r, lines, dt = _bench_cpu(tmp_path, "hang_rank=1", ["--watchdog", "6"], timeout=200)
+    assert r.returncode == 75, (r.returncode, r.stderr[-3000:])
+    assert lines == []
+    err = r.stderr
+    assert "no bench progress" in err and ("rank 1:" in err or "rank 0:" in err)
+    assert "launch: rank" in err
+    assert dt < 150
+
+
 def test_training_driver_two_ranks_logs_every_rank(tmp_path):
     """main.py under the launcher at world size 2: the shared training.log holds both
     ranks' epoch lines, each with its own rank tag, written whole by rank 0."""

@@ -205,10 +205,18 @@ def test_numa_pin_from_sysfs(tmp_path):
     dev.mkdir()
     (dev / "local_cpulist").write_text(",".join(str(c) for c in keep) + "\n")
     (dev / "numa_node").write_text("1\n")
+    import torch
+    nthr = torch.get_num_threads()
+    assert D.pin_host_to_gpu(None, sysfs=str(tmp_path), addr="0000:c1:00.0") is None  # opt-in
+    _os.environ["MPA_NUMA_PIN"] = "1"
     try:
         info = D.pin_host_to_gpu(None, sysfs=str(tmp_path), addr="0000:c1:00.0")
-        assert info == {"pci": "0000:c1:00.0", "numa_node": 1, "cpus": len(keep)}
+        assert {k: info[k] for k in ("pci", "numa_node", "cpus")} == \
+            {"pci": "0000:c1:00.0", "numa_node": 1, "cpus": len(keep)}
+        assert torch.get_num_threads() <= max(len(keep), 1)
         assert _os.sched_getaffinity(0) == set(keep)
         assert D.pin_host_to_gpu(None, sysfs=str(tmp_path), addr="0000:c2:00.0") is None
     finally:
+        _os.environ.pop("MPA_NUMA_PIN", None)
         _os.sched_setaffinity(0, allowed)
+        torch.set_num_threads(nthr)

@@ -1,5 +1,5 @@
 """BatchNorm kernel bandwidth at the ResNet-18 batch-256 shapes.  Knobs are read once per
-process: MPA_BN_GRID (target blocks), MPA_BN_UNR (rows in flight per thread).
+process (grid and rows-in-flight are fixed in bn.hip since round 5).
     python tools/bench_bn.py [iters]"""
 import os
 import sys
@@ -28,7 +28,7 @@ def timeit(fn):
     return s.elapsed_time(e) / IT * 1e-3
 
 
-print("grid=%s unr=%s" % (os.environ.get("MPA_BN_GRID", "2048"), os.environ.get("MPA_BN_UNR", "1")))
+
 tot = 0.0
 for M, C in SHAPES:
     x = torch.randn(M, C, device=dev).to(torch.bfloat16)

@@ -5,8 +5,7 @@ shapes at a given batch, reported as TFLOP/s.
     python tools/bench_kernels.py [batch] [iters] sweep    every tile on the DMA engine
     (MPA_SWEEP_SHAPES=s2,ds: only the shapes whose name contains one of those)
 
-MPA_BENCH_ENGINES=0,1,1h,2 selects engines ("1h": halo 3x3/s1 kernel on); MPA_IGEMM_OCC=2|3|4 the register engine's
-occupancy target.  Sweep rows print each tile's time (us) with its split count forced to
+MPA_BENCH_ENGINES=0,1,1h,2 selects engines ("1h": halo 3x3/s1 kernel on).  Sweep rows print each tile's time (us) with its split count forced to
 auto; the `auto` column is what the planner picks."""
 import os
 import sys
@@ -94,7 +93,7 @@ for spec in ENGINES:
     C.igemm_set_halo(1 if spec.endswith("h") else 0)
     print("== engine %s (%s%s)" % (spec, ["register", "dma rows", "dma all"][eng],
                                    " + halo 3x3/s1" if spec.endswith("h") else ""))
-    print("occ=%s batch=%d" % (os.environ.get("MPA_IGEMM_OCC", "3"), B))
+    print("batch=%d" % B)
     tot = [0.0, 0.0, 0.0]
     for name, H, Ci, Co, R, st, pd in SHAPES:
         flop, fns = tensors(H, Ci, Co, R, st, pd)

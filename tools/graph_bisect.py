@@ -58,7 +58,6 @@ def eager_ref(n):
 
 def run_step_graph(sep, n):
     model, opt, step = fresh()
-    step._sync_replay = False
     step.capture(x, y, warmup=2)
     losses, sums = [], []
     ev = torch.cuda.Event()
