@@ -116,6 +116,9 @@ struct IGemmArgs {
   // kernels only; dense [M][N] rows)
   const bf16_raw* ep_res;
   const uint8_t* ep_rmask;
+  // BN in the operand path (3x3/s1 halo forward only, see WGradArgs::pre_aff): A is the raw
+  // z of the previous conv, staged as relu(z * pre_aff[c] + pre_aff[aC + c]) in bf16
+  const float* pre_aff;
 };
 constexpr short TAP_SRC2 = 0x2000;
 
@@ -141,6 +144,10 @@ struct WGradArgs {
   int tiles_n, tiles_total;
   int overwrite;  // 1: dw holds nothing to keep (first gradient since zero_grad): store, no
                   // read-modify-write of the fp32 arena
+  // BN in the operand path (3x3/s1 halo wgrad only): x is the raw output z of the previous
+  // conv and the operand is relu(z * pre_aff[c] + pre_aff[C + c]) rounded to bf16 (a
+  // train-mode BN + ReLU whose output is never written); padding stays zero.  null: none
+  const float* pre_aff;
 };
 
 // igemm.hip
@@ -160,6 +167,10 @@ int64_t igemm_bnred_slab_floats(int M, int N, int nphase);
 void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* sums,
                             hipStream_t s);
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
+// whether a launch with a.pre_aff set (BN in the operand path) runs on a kernel that applies
+// it while staging (else the caller materializes the operand first: affine_act)
+bool igemm_rows_pre_ok(const IGemmArgs& a, int vw);
+bool igemm_wgrad_pre_ok(const WGradArgs& a);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
 int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LDS-DMA all
@@ -184,6 +195,7 @@ bool stem_wgrad_ok(const WGradArgs& a);
 int stem_wgrad(WGradArgs a, hipStream_t s);
 int64_t stem_wgrad_ws_floats();
 bool conv3_halo_wgrad_ok(const WGradArgs& a);
+void igemm_set_halo_wprod(int on);  // producer-wave halo weight gradients (MPA_HALO_WPROD)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);
 bool igemm_halo_enabled();
@@ -244,6 +256,9 @@ void bn_stats_affine(const float* stats, const float* gamma, const float* beta, 
 // avgpool2x2/s2(relu(z * aff0 + aff1)) without writing the BN output (H, W even, C % 8 == 0)
 void bn_relu_avgpool2_fwd(const bf16_raw* z, const float* aff, int N, int H, int W, int C,
                           bf16_raw* y, hipStream_t s);
+// y = relu?(x * aff[c] + aff[C + c]) (aff [2][C]: bn_stats_affine's scale | shift)
+void affine_act(const bf16_raw* x, const float* aff, int relu, int M, int C, bf16_raw* y,
+                hipStream_t s);
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,
                  const float* rvar, float eps, const bf16_raw* res, int relu, int M, int C,
                  bf16_raw* y, hipStream_t s, int ldx = 0);

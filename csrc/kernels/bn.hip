@@ -227,6 +227,25 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
       });
 }
 
+// y = relu?(x * aff[c] + aff[C + c]): a BN whose affine was computed by bn_stats_affine,
+// materialized (the fallback of the operand-path BN when the consumer's kernel cannot apply
+// it while staging)
+template <int UNR>
+__global__ __launch_bounds__(256) void affine_act_kernel(const bf16_t* __restrict__ x,
+                                                         const float* __restrict__ aff, int relu,
+                                                         int M, int C, bf16_t* __restrict__ y) {
+  const ColMap cm = colmap(C / 8);
+  if (!cm.active) return;
+  const int c0 = cm.cc * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = aff[c0 + j];
+    sh[j] = aff[C + c0 + j];
+  }
+  bn_apply_rows<UNR>(cm, M, C, C, c0, sc, sh, x, nullptr, relu, y);
+}
+
 // ------------------------------------------------------------------- forward (train)
 template <int UNR, bool YM>
 __global__ __launch_bounds__(256) void bn_fwd_train_kernel(
@@ -1628,6 +1647,11 @@ void bn_stats_affine(const float* stats, const float* gamma, const float* beta, 
   hipLaunchKernelGGL(bn_stats_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats,
                      gamma, beta, rmean, rvar, momentum, eps, M, C, mean, rstd, aff,
                      (unsigned long long*)counter);
+}
+
+void affine_act(const bf16_raw* x, const float* aff, int relu, int M, int C, bf16_raw* y,
+                hipStream_t s) {
+  BN_LAUNCH(affine_act_kernel, grid_for(M, C), s, (const bf16_t*)x, aff, relu, M, C, (bf16_t*)y);
 }
 
 void bn_fwd_eval(const bf16_raw* x, const float* gamma, const float* beta, const float* rmean,

@@ -68,8 +68,24 @@ __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
   return __builtin_bit_cast(bf16x8, *LDS_PTR(const u32x4, lds_byte));
 }
 
+// Operand BN (PRE): relu(v * sc + sh) of one staged 16-B piece (8 channels), in place, with
+// bn_fwd_train's arithmetic and rounding (fma, max, RNE to bf16), so the operand equals the
+// BN output the forward would have written
+__device__ __forceinline__ void pre_xform(char* lds, const float (&sc)[8], const float (&sh)[8]) {
+  const u32x4 v = *LDS_PTR(const u32x4, lds);
+  float f[8];
+  unpack8(make_uint4(v[0], v[1], v[2], v[3]), f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = fmaxf(__builtin_fmaf(f[e], sc[e], sh[e]), 0.f);
+  const uint4 r = pack8(f);
+  *LDS_PTR(u32x4, lds) = u32x4{r.x, r.y, r.z, r.w};
+}
+
 // Epilogue flavours (compile-time, so the fused epilogue below is one straight-line block)
-enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16 };
+enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16,
+              // not an epilogue: the A operand is z of a BN + ReLU applied while staging
+              // (IGemmArgs::pre_aff; producer-wave blocks)
+              EP_PRE = 32 };
 
 // Per-tile operands the epilogue reads from memory (accumulate: the old output; fused
 // BN-backward reduction: z, whose ReLU mask is recomputed like bn_fwd_train rounded y, so
@@ -336,7 +352,31 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
                   wv[j - HB_HIW]);
       }
     };
+    // operand BN (EP_PRE): this lane's 16-B halo pieces hold channels 32 cc + 8 lc .. +7 (lc
+    // fixed per lane); the chunk's scale / shift are loaded with its DMAs (the vmcnt wait
+    // that covers the DMAs covers them) and applied to the landed pieces in place
+    float psc[8], psh[8];
+    const int plc = (lane & 3) ^ (((lane >> 4) & 1) << 1);
+    auto pre_coef = [&](int cc) {
+      if constexpr (EPI & EP_PRE) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          psc[e] = p.pre_aff[cc * 32 + plc * 8 + e];
+          psh[e] = p.pre_aff[aC + cc * 32 + plc * 8 + e];
+        }
+      }
+    };
+    auto xform = [&](int stage) {
+      if constexpr (EPI & EP_PRE) {
+        char* hb = hal + stage * HB_HBYTES + wave * HB_HIW * 1024 + lane * 16;
+#pragma unroll
+        for (int j = 0; j < HB_HIW; ++j)
+          if (hv[j] != 0x80000000u) pre_xform(hb + j * 1024, psc, psh);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    };
     auto issue = [&](int cc, int stage) {
+      pre_coef(cc);
 #pragma unroll
       for (int j = 0; j < HB_HIW + HB_WIW; ++j) dma(cc, stage, j);
     };
@@ -352,7 +392,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       prep_tile(0);
       issue(0, 0);
     }
-    body(prep_tile, dma, issue);
+    body(prep_tile, dma, issue, xform);
   };
 
   if constexpr (PROD) {
@@ -364,9 +404,13 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     // docs/KERNELS.md), waiting for them nothing measurable.  Barrier count per wave:
     // nitems (+1 for the statistics flush) on both sides.
     if (wave_all >= HB_NW) {
-      stager([&](auto& prep_tile, auto&, auto& issue) {
+      stager([&](auto& prep_tile, auto&, auto& issue, auto& xform) {
         int cc1 = 0;
         for (int k = 0; k < nitems; ++k) {
+          if constexpr (EPI & EP_PRE) {  // item k landed: transform it before publishing
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            xform(k & 1);
+          }
           wait_all_barrier();
           if (++cc1 == CC) cc1 = 0;
           if (k + 1 < nitems) {
@@ -595,7 +639,8 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     int none = 0;
     tiles(none, none);
   } else {
-    stager([&](auto& prep_tile, auto& dma, auto&) { tiles(prep_tile, dma); });
+    static_assert(!(EPI & EP_PRE), "the operand transform runs on producer waves");
+    stager([&](auto& prep_tile, auto& dma, auto&, auto&) { tiles(prep_tile, dma); });
   }
   if (ntiles > 0) epi_tile(m0_of(ntiles - 1), std::integral_constant<bool, FULL>{});
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush<TRED>(p, ss, sq, red, n0, wave, tid);
@@ -968,12 +1013,20 @@ struct HaloWPlan {
 // of a stage hold ONE 896-pixel halo image of the first chunk (14 DMA instructions per
 // wave instead of 2 x 7).  Waves 2 and 3 then read chunk 0 as well; their partials are
 // duplicates of waves 0 / 1 and are not stored.
-template <int W2T, bool ONECH = false, bool STRIP = false>
-__global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
+// PROD: 8-wave blocks; waves 4..7 are producers (every tile's index math, LDS-DMAs and - PRE -
+// the operand BN transform of the landed halo), waves 0..3 run only fragment reads and
+// MFMAs.  One barrier per tile on both sides: tile k's barrier publishes stage k & 1 and
+// frees stage (k + 1) & 1.  PRE (BN in the operand path, WGradArgs::pre_aff): each producer
+// lane transforms the halo pieces its own DMAs wrote, after its vmcnt wait and before the
+// barrier; out-of-image pieces (DMA offset past num_records, zeros) stay zero.
+template <int W2T, bool ONECH = false, bool STRIP = false, bool PROD = false, bool PRE = false>
+__global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
+  static_assert(PROD || !PRE, "the operand transform runs on producer waves");
   constexpr int HIW = ONECH ? 2 * HW_HIW : HW_HIW;  // halo DMA instructions per wave (chunk)
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = wave_all & 3;  // MFMA channel group / DMA lane group
   const int H = p.H, W = p.W, HW = H * W, W2 = W2T ? W2T : h.w2, C = p.C, K = p.Kout;
   const int M = p.Mpix, nimg = M / HW;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
@@ -1017,7 +1070,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
   const int cbyte = ((2 * (wave & 1) + (pp >> 1)) << 4) + 8 * (pp & 1);
   // B-row addresses per (k-step, lo/hi, column tap dw): the swizzle bit is pixel bit 3,
   // and the row pitch W2 is a multiple of 16, so a tap's row offset dh * W2 never changes
-  // it - the swizzled address of pixel (hp + dh*W2 + dw) is hbw[dw] + dh*W2*64
+  // it - the swizzled address of pixel (hp + dh*W2 + dw) is hbw[dw] + dh*W2*64.  hbw holds
+  // the CURRENT tile's addresses at row tap dh = -1 including its stage's base (one set of
+  // 24 registers: the MFMA waves of an 8-wave block have 256), and the next tile's are
+  // computed after the current tile's MFMAs are issued
+  const int hoff = HW_DBYTES + (ONECH ? 0 : (wave >> 1) * HW_HBYTES);
+  auto stage_base = [&](int st) { return st * HW_STAGE + hoff - W2 * 64; };
   int hbw[4][2][3];
   const int tpx = STRIP ? h.tr * h.tw : HW_BM;
   if constexpr (STRIP) {
@@ -1033,11 +1091,12 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
           const int x = (hp + d - 1) * 64 + cbyte;
-          hbw[ks][e][d] = x ^ ((x >> 4) & 32);
+          hbw[ks][e][d] = (x ^ ((x >> 4) & 32)) + stage_base(0);
         }
       }
   }
-  auto prep = [&](int mt) {
+  // a tile's DMA source offsets (halo hv, dy rows dv)
+  auto prep_dma = [&](int mt) {
     if constexpr (STRIP) {
       const int img = (int)udiv1((uint32_t)mt, h.mag_timg);
       const uint32_t rem = (uint32_t)(mt - img * h.tiles_img);
@@ -1083,23 +1142,41 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       const int row = 8 * (4 * wave + j) + (lane >> 3);
       dv[j] = (m0 + row < M && kok[j]) ? drow[j] + (uint32_t)m0 * K * 2 : 0x80000000u;
     }
-    const int mlast = M - 1 - img0 * HW;
+  };
+  // tile mt's B-row addresses in stage st (STRIP: tile-independent, only the stage moves)
+  auto prep_b = [&](int mt, int st) {
+    if constexpr (STRIP) {
+      const int dlt = st ? HW_STAGE : -HW_STAGE;  // called for alternating stages
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+      for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const uint32_t n = (uint32_t)min(r0 + ks * 32 + 8 * g + 4 * e + q, mlast);
-        const uint32_t di = udiv(n, h.mag_hw);
-        const uint32_t rem = n - di * HW;
-        const uint32_t oh = udiv(rem, h.mag_w);
-        const uint32_t ow = rem - oh * W;
-        const int hp = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+        for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const int x = (hp + d - 1) * 64 + cbyte;
-          hbw[ks][e][d] = x ^ ((x >> 4) & 32);
+          for (int d = 0; d < 3; ++d) hbw[ks][e][d] += dlt;
+    } else {
+      const int hb0 = stage_base(st);
+      const int m0 = mt * HW_BM;
+      const int img0 = m0 / HW;
+      const int r0 = m0 - img0 * HW;
+      const int oh0 = r0 / W;
+      const int mlast = M - 1 - img0 * HW;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t n = (uint32_t)min(r0 + ks * 32 + 8 * g + 4 * e + q, mlast);
+          const uint32_t di = udiv(n, h.mag_hw);
+          const uint32_t rem = n - di * HW;
+          const uint32_t oh = udiv(rem, h.mag_w);
+          const uint32_t ow = rem - oh * W;
+          const int hp = ((int)(di * (H + 1) + oh) - oh0 + 1) * W2 + (int)ow + 1;
+#pragma unroll
+          for (int d = 0; d < 3; ++d) {
+            const int x = (hp + d - 1) * 64 + cbyte;
+            hbw[ks][e][d] = (x ^ ((x >> 4) & 32)) + hb0;
+          }
         }
-      }
+    }
   };
   // DMA instruction j of a tile: dy rows (0..3), halo chunk 0 (4..10), halo chunk 1 (11..17)
   const uint32_t sw = lds_base(smem) + wave * 4096;  // this wave's DMA pieces: + 1 KiB each
@@ -1121,35 +1198,83 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
     for (int j = 0; j < 4 + 2 * HW_HIW; ++j) dmaw(stage, j);
   };
 
+  if constexpr (PROD) {
+    if (wave_all >= 4) {
+      // ---- producers
+      float psc[2][8], psh[2][8];
+      if constexpr (PRE) {
+        // this lane's 16-B pieces hold channels c0 + 32 ch + 8 lc .. +7 (lc fixed per lane)
+        const int lc = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int c = c0 + 32 * ch + 8 * lc + e;
+            psc[ch][e] = c < C ? p.pre_aff[c] : 0.f;
+            psh[ch][e] = c < C ? p.pre_aff[C + c] : 0.f;
+          }
+      }
+      if (ntiles > 0) {
+        prep_dma(z);
+        issue(0);
+      }
+      for (int k = 0; k < ntiles; ++k) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k landed (this wave's part)
+        if constexpr (PRE) {
+          char* hb = smem + (k & 1) * HW_STAGE + HW_DBYTES + lane * 16;
+          if constexpr (ONECH) {
+#pragma unroll
+            for (int jj = 0; jj < HIW; ++jj)
+              if (hv[jj] != 0x80000000u) pre_xform(hb + (wave * HIW + jj) * 1024, psc[0], psh[0]);
+          } else {
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+              for (int jj = 0; jj < HW_HIW; ++jj)
+                if (hv[jj] != 0x80000000u)
+                  pre_xform(hb + ch * HW_HBYTES + (wave * HW_HIW + jj) * 1024, psc[ch], psh[ch]);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // publishes stage k & 1, frees stage (k + 1) & 1
+        if (k + 1 < ntiles) {
+          prep_dma(z + (k + 1) * h.Z);
+          issue((k + 1) & 1);
+        }
+      }
+      return;
+    }
+  }
+
   f32x4 acc[4][9];
 #pragma unroll
   for (int km = 0; km < 4; ++km)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[km][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int hoff = HW_DBYTES + (ONECH ? 0 : (wave >> 1) * HW_HBYTES);
   if (ntiles > 0) {
-    prep(z);
-    issue(0);
+    if constexpr (!STRIP) prep_b(z, 0);
+    if constexpr (!PROD) {
+      prep_dma(z);
+      issue(0);
+    }
   }
   // tile k from stage k & 1; MORE (all but the block's last tile): prepare tile k + 1 and
-  // issue its 18 DMAs into the other stage inside this tile's MFMA stream, one per two
-  // tap-steps.  The last tile is peeled so the loop body carries no per-DMA branch.
+  // (without producer waves) issue its 18 DMAs into the other stage inside this tile's MFMA
+  // stream, one per two tap-steps.  The last tile is peeled so the loop body carries no
+  // per-DMA branch.
   auto tile = [&](int k, auto nmore) {
     constexpr bool MORE = decltype(nmore)::value;
     const int st = k & 1;
-    wait_all_barrier();
-    // this tile's B-row bases at row tap dh = -1 in stage st (tap dh adds (dh+1)*W2*64: an
-    // immediate offset when W2T != 0); also frees hbw for the next tile's prep
-    int hbk[4][2][3];
-    const int hb0 = st * HW_STAGE + hoff - W2 * 64;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int d = 0; d < 3; ++d) hbk[ks][e][d] = hbw[ks][e][d] + hb0;
-    if constexpr (MORE) prep(z + (k + 1) * h.Z);
+    if constexpr (PROD) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+    } else {
+      wait_all_barrier();
+    }
+    // (hbw: this tile's B-row bases at row tap dh = -1 in stage st; tap dh adds
+    // (dh+1)*W2*64, an immediate offset when W2T != 0)
+    if constexpr (MORE && !PROD) prep_dma(z + (k + 1) * h.Z);
     const char* sbase = smem + st * HW_STAGE;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -1160,20 +1285,23 @@ __global__ __launch_bounds__(256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, H
       for (int t = 0; t < 9; ++t) {
         const int off = (t / 3) * W2 * 64;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + hbk[ks][0][t % 3] + off));
+            LDS_PTR(s16x4, smem + hbw[ks][0][t % 3] + off));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + hbk[ks][1][t % 3] + off));
+            LDS_PTR(s16x4, smem + hbw[ks][1][t % 3] + off));
         s16x8 r;
         r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
         r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
         for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
-        if constexpr (MORE) {
+        if constexpr (MORE && !PROD) {
           if (((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
         }
       }
     }
+    // the next tile's B-row addresses (its stage is the other one), after this tile's last
+    // fragment reads
+    if constexpr (MORE) prep_b(z + (k + 1) * h.Z, st ^ 1);
     // (no barrier: tile k + 2's DMAs into stage st follow tile k + 1's top barrier)
   };
   for (int k = 0; k + 1 < ntiles; ++k) tile(k, std::true_type{});
@@ -1417,15 +1545,15 @@ static bool use_strip(const IGemmArgs& a, bool linear) {
 bool conv3_halo_ok(const IGemmArgs& a) {
   bool linear;
   if (!halo_ok_impl(a, linear)) return false;
+  if (a.pre_aff)  // operand BN: linear tiles, statistics epilogue, 64-wide column tiles
+    return linear && !use_strip(a, linear) && halo_epi(a) == EP_STATS && a.N % HB_BN == 0;
   return linear || use_strip(a, linear);
 }
 
 // Producer waves (PROD: 8-wave blocks, DMAs off the MFMA waves; each MFMA wave then has
-// 256 registers, which every flavour fits).  MPA_HALO_PROD=0: 4-wave blocks.
-static const bool g_halo_prod = [] {
-  const char* e = getenv("MPA_HALO_PROD");
-  return !(e && atoi(e) == 0);
-}();
+// 256 registers, which every flavour fits) for every launch: issuing the DMAs between the
+// MFMAs cost the MFMA waves ~10 % (round-2 A/B), and the fused BN-backward reduction
+// flavour, reduced per column group (TRED), fits 256 registers without scratch
 
 template <int EPI, bool PROD, int NJ>
 static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
@@ -1446,21 +1574,10 @@ static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPla
                        a, h);
 }
 
-// MPA_HALO_BNRED_PROD=0: the fused BN-backward reduction flavour in 4-wave blocks.  With
-// producer waves a wave has 256 registers in all; that flavour used to spill 250-550
-// B/lane there (its column sums lived across a whole tile's epilogue).  Reduced per column
-// group (TRED) it needs ~216 VGPRs and no scratch, so it follows MPA_HALO_PROD.
-static const bool g_halo_bnred_prod = [] {
-  const char* e = getenv("MPA_HALO_BNRED_PROD");
-  return !(e && atoi(e) == 0);
-}();
-
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  const bool prod = g_halo_prod && (!(EPI & EP_BNRED) || g_halo_bnred_prod);
-  if (prod) launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
-  else launch_halo_k<EPI, false, 4>(wres, grid, a, h, s);
+  launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
 }
 
 // N == 32 (plain and statistics epilogues only; producer-wave blocks)
@@ -1501,6 +1618,10 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
   const bool wres = g_halo_wres && a.tiles_n == 1 && h.cc <= 2;
+  if (a.pre_aff) {  // (conv3_halo_ok: statistics epilogue, N % 64 == 0)
+    launch_halo_k<EP_STATS | EP_PRE, true, 4>(wres, grid, a, h, s);
+    return grid;
+  }
   if (a.N == 32) {
     if (halo_epi(a) == EP_STATS) launch_halo32<EP_STATS>(wres, grid, a, h, s);
     else launch_halo32<0>(wres, grid, a, h, s);
@@ -1598,6 +1719,33 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
   return halo_wgrad_strip_plan(a, h);
 }
 
+// Producer-wave weight-gradient kernels (PROD): MPA_HALO_WPROD=1 for every launch (A/B until
+// measured); the operand-BN form (a.pre_aff) always runs on them
+static bool g_wprod = [] {
+  const char* e = getenv("MPA_HALO_WPROD");
+  return e && e[0] == '1';
+}();
+void igemm_set_halo_wprod(int on) { g_wprod = on != 0; }
+
+// (8-wave forms use the run-time pitch: with a compile-time pitch the MFMA waves' hoisted
+// tap addresses spill past their 256 registers)
+template <int W2T, bool ONECH = false, bool STRIP = false>
+static void launch_halo_wgrad(const WGradArgs& a, const HaloWPlan& h, dim3 grid, hipStream_t s) {
+  if (a.pre_aff) {
+    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, STRIP, true, true>), grid, dim3(512),
+                       0, s, a, h);
+    return;
+  }
+  if constexpr (!STRIP) {
+    if (g_wprod) {
+      hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false>), grid,
+                         dim3(512), 0, s, a, h);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv3_halo_wgrad_kernel<W2T, ONECH, STRIP>), grid, dim3(256), 0, s, a, h);
+}
+
 // slab partials -> returns Z (slabs of [Kout][9C] to sum into dw)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   HaloWPlan h{};
@@ -1611,8 +1759,7 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
     h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
     h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
     h.x_bytes = (uint32_t)((int64_t)(a.Mpix / ((int64_t)a.P * a.Q)) * a.H * a.W * a.C * 2);
-    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, false, true>), dim3(h.parts * h.Z), dim3(256),
-                       0, s, a, h);
+    launch_halo_wgrad<0, false, true>(a, h, dim3(h.parts * h.Z), s);
     return h.Z;
   }
   const int W2 = halo_wgrad_pitch(a.W);
@@ -1629,17 +1776,17 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
   h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
-  const dim3 grid(h.parts * h.Z), blk(256);
+  const dim3 grid(h.parts * h.Z);
   if (halo_wgrad_onech(a)) {
-    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, true>), grid, blk, 0, s, a, h);
+    launch_halo_wgrad<0, true>(a, h, grid, s);
     return h.Z;
   }
   switch (W2) {
-    case 16: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<16>, grid, blk, 0, s, a, h); break;
-    case 32: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<32>, grid, blk, 0, s, a, h); break;
-    case 48: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<48>, grid, blk, 0, s, a, h); break;
-    case 64: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<64>, grid, blk, 0, s, a, h); break;
-    default: hipLaunchKernelGGL(conv3_halo_wgrad_kernel<0>, grid, blk, 0, s, a, h); break;
+    case 16: launch_halo_wgrad<16>(a, h, grid, s); break;
+    case 32: launch_halo_wgrad<32>(a, h, grid, s); break;
+    case 48: launch_halo_wgrad<48>(a, h, grid, s); break;
+    case 64: launch_halo_wgrad<64>(a, h, grid, s); break;
+    default: launch_halo_wgrad<0>(a, h, grid, s); break;
   }
   return h.Z;
 }

@@ -292,6 +292,18 @@ __device__ __forceinline__ void rows_epilogue(const IGemmArgs& p,
               }
             }
           }
+          if (!p.ep_y && p.ep_gamma && p.ep_beta && mok) {
+            // y never written (BN in the operand path): the mask from z with the forward's
+            // exact affine and rounding, as the halo kernels recompute it
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (n + r < p.N) {
+                const float sc = p.ep_gamma[n + r] * shift[j][r];
+                const float sh = __builtin_fmaf(-bias[j][r], sc, p.ep_beta[n + r]);
+                live[r] = bf2f(f2bf(__builtin_fmaf(zr[r], sc, sh))) > 0.f;
+              }
+            }
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float d = bf2f(f2bf(acc[i][j][r]));

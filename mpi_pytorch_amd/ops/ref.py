@@ -47,7 +47,17 @@ def conv_out_hw(H, W, R, S, sh, sw, ph, pw):
     return (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1
 
 
-def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None):
+def affine_act(x, aff, relu):
+    """relu?(x * aff[0] + aff[1]) per channel, in x's dtype (aff: bn_stats_affine's [2, C])."""
+    y = _f(x) * aff[0].float() + aff[1].float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None, pre=None):
+    if _opt(pre) is not None:  # x is z of a BN + ReLU applied here (operand-path BN)
+        x = affine_act(x, pre, True)
     y = F.conv2d(_nchw(_f(x)), _f(w).permute(0, 3, 1, 2), None if _opt(bias) is None else _f(bias),
                  (sh, sw), (ph, pw))
     y = _nhwc(y)
@@ -110,7 +120,9 @@ def conv_dgrad_pair(dy, w, wt, H, W, sh, sw, ph, pw, dy2, w2, wt2, ph2, pw2, acc
     return tot.to(dy.dtype)
 
 
-def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False):
+def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False, pre=None):
+    if _opt(pre) is not None:
+        x = affine_act(x, pre, True)
     K, R, S, C = dw.shape
     gw = torch.ops.aten.convolution_backward(
         _nchw(_f(dy)).contiguous(), _nchw(_f(x)).contiguous(),
