@@ -301,7 +301,10 @@ static Tensor conv_dgrad_impl(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t
     a.ep_rstd = fopt(bnred->rstd);
     a.ep_gamma = fopt(bnred->gamma);
     a.ep_beta = fopt(bnred->beta);
-    TORCH_CHECK(a.ep_y, "conv_dgrad_bnred: needs y (the implicit GEMM's ReLU mask)");
+    // without y (BN in the operand path: never written) every kernel recomputes the ReLU
+    // mask from z with gamma / beta
+    TORCH_CHECK(a.ep_y || (a.ep_gamma && a.ep_beta),
+                "conv_dgrad_bnred: needs y or gamma / beta for the ReLU mask");
     TORCH_CHECK(!a.ep_gamma == !a.ep_beta, "conv_dgrad_bnred: gamma and beta go together");
     for (const Tensor* t : {&bnred->mean, &bnred->rstd, &bnred->gamma, &bnred->beta})
       TORCH_CHECK(!has(*t) || t->numel() == C, "conv_dgrad_bnred: per-channel vector size");
