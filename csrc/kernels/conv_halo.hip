@@ -71,14 +71,24 @@ __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
 // Operand BN (PRE): relu(v * sc + sh) of one staged 16-B piece (8 channels), in place, with
 // bn_fwd_train's arithmetic and rounding (fma, max, RNE to bf16), so the operand equals the
 // BN output the forward would have written
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void pre_xform(char* lds, const float (&sc)[8], const float (&sh)[8]) {
   const u32x4 v = *LDS_PTR(const u32x4, lds);
-  float f[8];
-  unpack8(make_uint4(v[0], v[1], v[2], v[3]), f);
+  u32x4 r;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) f[e] = fmaxf(__builtin_fmaf(f[e], sc[e], sh[e]), 0.f);
-  const uint4 r = pack8(f);
-  *LDS_PTR(u32x4, lds) = u32x4{r.x, r.y, r.z, r.w};
+  for (int i = 0; i < 4; ++i) {
+    // two channels per packed fma (v_pk_fma_f32: the same IEEE fma per element), RNE to
+    // bf16, then the ReLU as a packed signed 16-bit max with 0 (a bf16 with the sign bit set
+    // is a negative int16: every negative value and -0 become +0, as fmaxf(x, 0) followed by
+    // the rounding gives)
+    f32x2 f = {__uint_as_float(v[i] << 16), __uint_as_float(v[i] & 0xffff0000u)};
+    f = __builtin_elementwise_fma(f, f32x2{sc[2 * i], sc[2 * i + 1]},
+                                  f32x2{sh[2 * i], sh[2 * i + 1]});
+    const s16x2 h = __builtin_bit_cast(s16x2, pack2(f[0], f[1]));
+    r[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, s16x2{0, 0}));
+  }
+  *LDS_PTR(u32x4, lds) = r;
 }
 
 // Epilogue flavours (compile-time, so the fused epilogue below is one straight-line block)
@@ -407,8 +417,11 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
       stager([&](auto& prep_tile, auto&, auto& issue, auto& xform) {
         int cc1 = 0;
         for (int k = 0; k < nitems; ++k) {
-          if constexpr (EPI & EP_PRE) {  // item k landed: transform it before publishing
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if constexpr (EPI & EP_PRE) {
+            // item k's halo landed (its weight DMAs, issued after it, may still be in
+            // flight: the transform overlaps their landing); transform before publishing
+            if constexpr (WRES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HB_WIW) : "memory");
             xform(k & 1);
           }
           wait_all_barrier();
