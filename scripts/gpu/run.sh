@@ -15,8 +15,11 @@
 #   stats[=ARGS]     rocprofv3 --kernel-trace --stats over bench.py -> TAG_stats/
 #   ab=SPEC;SPEC..   bench A/B, two alternating repeats; SPEC = "ENV=V ... | --args"
 #   kern[=ARGS]      tools/bench_kernels.py ARGS                 -> TAG_kern.txt
-#   pmc=REGEX:CTRS   one rocprofv3 PMC pass over two bench steps, kernels matching REGEX,
-#                    counters CTRS (space separated)             -> TAG_pmc_N/
+#   pmc=REGEX:CTRS   one rocprofv3 PMC pass over two bench steps, kernels matching REGEX
+#                    (empty: all), counters CTRS (space separated) -> TAG_pmc_N/
+#   trace            kernel trace of the pmc passes' run shape   -> TAG_trace/
+#   gaps=ARGS        kernel trace of bench.py ARGS, inter-kernel gap distribution (tools/gap_stats.py)
+#   (PMC_ARGS in the environment: extra bench.py arguments of pmc / trace)
 #   py=SCRIPT,ARGS   python SCRIPT ARGS under a 300 s limit      -> TAG_py_N.log
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -79,11 +82,25 @@ for step in "$@"; do
       tail -12 ${O}_kern.txt ;;
     pmc)
       rx=${val%%:*}; ctrs=${val#*:}
-      timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex "$rx" \
+      inc=(); [ -n "$rx" ] && inc=(--kernel-include-regex "$rx")
+      timeout -s KILL 120 rocprofv3 --pmc $ctrs "${inc[@]}" \
         --output-format csv -d $R/${O}_pmc_$n -o p \
-        -- python3 $R/bench.py --steps 2 --warmup 2 --small-batch 0 \
+        -- python3 $R/bench.py --steps 2 --warmup 2 --small-batch 0 $PMC_ARGS \
         > ${O}_pmc_$n.log 2>&1 || { tail -20 ${O}_pmc_$n.log; exit 1; }
       echo "pmc pass $n done" ;;
+    gaps)
+      # inter-kernel gap distribution of bench.py ARGS (e.g. --batch,128,--graph,on)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/${O}_gaps_$n -o g \
+        -- python3 $R/bench.py --steps 8 --warmup 3 --small-batch 0 $(args_of "$val") \
+        > ${O}_gaps_$n.log 2>&1 || { tail -20 ${O}_gaps_$n.log; exit 1; }
+      f=$(find ${O}_gaps_$n -name "*kernel_trace.csv" | head -1)
+      python3 tools/gap_stats.py $f 5 > ${O}_gaps_$n.txt; rm -f $f; tail -1 ${O}_gaps_$n.txt ;;
+    trace)
+      # kernel trace of the same run shape as the pmc passes (durations for pmc_dispatch.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/${O}_trace -o t \
+        -- python3 $R/bench.py --steps 2 --warmup 2 --small-batch 0 $PMC_ARGS \
+        > ${O}_trace.log 2>&1 || { tail -20 ${O}_trace.log; exit 1; }
+      echo "trace done" ;;
     py)
       s=${val%%,*}; a=""
       [[ "$val" == *","* ]] && a=${val#*,}
