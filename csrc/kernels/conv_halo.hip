@@ -1732,11 +1732,13 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
   return halo_wgrad_strip_plan(a, h);
 }
 
-// Producer-wave weight-gradient kernels (PROD): MPA_HALO_WPROD=1 for every launch (A/B until
-// measured); the operand-BN form (a.pre_aff) always runs on them
+// Producer-wave weight-gradient kernels (PROD) for the linear tiles: the 13 ResNet-18 halo
+// weight gradients take 3.14 ms instead of 3.63 ms per b1024 step, +2.4 % single-stream
+// (round-5 A/B, profiles/wprod_pre_ab_r5.txt).  MPA_HALO_WPROD=0: the 4-wave form (the
+// MFMA waves issue the DMAs).  The operand-BN form (a.pre_aff) always runs on them.
 static bool g_wprod = [] {
   const char* e = getenv("MPA_HALO_WPROD");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }();
 void igemm_set_halo_wprod(int on) { g_wprod = on != 0; }
 

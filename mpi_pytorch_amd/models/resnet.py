@@ -28,8 +28,12 @@ _JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
 _DS_DEFER = os.environ.get("MPA_DS_DEFER", "1") == "1"
 # BN in the operand path (Fn.BNLink.want_pre): bn1 + ReLU applied by conv2's forward and
 # weight-gradient kernels while they stage conv1's raw output, so y1 is never written.
-# MPA_BN_PRE=0 turns it off (A/B).
-_PRE = os.environ.get("MPA_BN_PRE", "1") == "1"
+# Opt-in (MPA_BN_PRE=1): bitwise equal to the written y1 (tests/test_pre_bn_gpu.py) but
+# measured SLOWER - 47.4k vs 49.2k img/s single-stream, b1024 (profiles/wprod_pre_ab_r5.txt):
+# the producer waves' transform of each landed halo sits on the critical path between the
+# DMAs landing and the barrier that publishes them (+50-95 us per forward, +60 % per weight
+# gradient) and costs more than the 8 bn1 apply passes (645 us) it removes.
+_PRE = os.environ.get("MPA_BN_PRE", "0") == "1"
 _PRE_CPU = False  # (tests: the same op sequence on the CPU reference ops)
 
 

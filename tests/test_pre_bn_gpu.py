@@ -111,7 +111,7 @@ def test_halo_wgrad_producer_waves_bitwise(gpu, case):
             C().conv_wgrad(dy, x, dw, 1, 1, 1, 1, overwrite=True)
             out.append(dw)
     finally:
-        C().igemm_set_halo_wprod(0)
+        C().igemm_set_halo_wprod(1)  # (the default)
     torch.cuda.synchronize()
     assert torch.equal(out[0], out[1])
 
