@@ -281,9 +281,8 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
 
 // NJ: 16-column fragment groups per wave (4: 64-wide column tiles; 2: N == 32 - the weight
 // image's upper 32 columns are zero-filled DMAs and never read, no MFMA touches them)
-template <bool WRES, int EPI, bool FULL, bool PROD, int NJ>
-__global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
-  constexpr int HB_DPT = WRES ? 2 : 4;  // next-item DMAs per tap (no producer waves)
+template <bool WRES, int EPI, bool FULL, int NJ>
+__global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
   __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
   char* const hal = smem;
   char* const wst = smem + 2 * HB_HBYTES;
@@ -405,7 +404,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     body(prep_tile, dma, issue, xform);
   };
 
-  if constexpr (PROD) {
+  {
     // Producer waves 4..7: all of the block's LDS-DMAs.  Item k's top barrier publishes
     // stage k & 1 (every producer has waited for its DMAs) and frees stage (k + 1) & 1 (every
     // MFMA wave is done with item k - 1), so item k + 1's DMAs go out right behind it and get
@@ -544,6 +543,9 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
         }
       }
     } else {
+      // (the per-column operands are re-read from LDS per tile: an empty asm memory clobber
+      // keeps the compiler from hoisting 32 VGPRs of them out of the tile loop)
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -551,39 +553,43 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     }
   };
 
-  // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + 4 B fragments (the next
-  // tap's 8 reads in flight under this tap's 16 MFMAs) and, without producer waves, four of
-  // the next item's LDS-DMAs in the MFMA shadow (front-loaded: all by tap 4, so the
-  // top-of-item wait finds them done).  FIRST: the tile's first chunk (accumulators start
-  // at 0).  (Measured: a row-major body that held the chunk's B fragments in registers and
+  // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + NJ B fragments, the next
+  // tap's in flight under this tap's 4 NJ MFMAs.  The schedule is fenced (sched_barrier):
+  // the next tap's B fragments go out in front of this tap's MFMAs and its A row fragment i
+  // right behind MFMA group i (which frees that register), so every read has a whole tap to
+  // land.  Left to itself the scheduler (at ~230 live VGPRs) sank every read to just in
+  // front of its first use, so each group of 4 MFMAs waited out an LDS round trip.  Fenced:
+  // 7-10 % faster in isolation, neutral inside the training step, where the LDS array (the
+  // fragment reads plus the DMA writes, ~90 % of the MFMA time per item) and not the read
+  // latency sets the pace (round 5, profiles/halo_sched_r5.txt).
+  // (Measured earlier: a row-major body that held the chunk's B fragments in registers and
   // ran the previous tile's epilogue interleaved with the next tile's MFMAs was 10-15 %
-  // slower once the DMA issue moved into the MFMA stream and the A addresses were
-  // precomputed.)
-  auto mma_chunk = [&](int st, int cc, auto first, auto nd) {
-    constexpr bool FIRST = decltype(first)::value;
+  // slower.)
+  auto mma_chunk = [&](int st, int cc) {
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    bf16x8 a2[2][4], b2[2][4];
-    auto ld = [&](int t, int b) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
+    bf16x8 a2[4], b2[2][4];
+    auto ld_b = [&](int t, int b) {
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
-    ld(0, 0);
+    auto ld_a = [&](int t, int i) {
+      a2[i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
+    };
+    ld_b(0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ld_a(0, i);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+      if (t + 1 < 9) ld_b(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int jn = 0; jn < NJ; ++jn)
-          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
-                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
-      if constexpr (!PROD) {
-#pragma unroll
-        for (int d = 0; d < HB_DPT; ++d) nd(HB_DPT * t + d);
+        for (int jn = 0; jn < NJ; ++jn) acc[i][jn] = mfma16(b2[t & 1][jn], a2[i], acc[i][jn]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < 9) ld_a(t + 1, i);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
@@ -592,29 +598,16 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
   // (accumulate: old output; fused BN reduction: z, y) are loaded right after the top wait
   // of the tile's second-to-last item, so they are in flight under its MFMAs (a load issued
   // in front of a wait would be waited for with the DMAs).
-  auto run_tile = [&](int tk, auto& prep_tile, auto& dma) {
+  auto run_tile = [&](int tk) {
     const int m0 = m0_of(tk);
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       const int st = k & 1;
-      // this item's DMAs were issued during the previous item; the next item's are issued
-      // during this one's (stage st ^ 1 was freed by this barrier).  The MFMA waves of a
-      // producer block have no DMA of their own to wait for.
-      if constexpr (PROD) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-      } else {
-        wait_all_barrier();
-      }
+      // this item's DMAs were issued by the producers during the previous item (stage st ^ 1
+      // was freed by this barrier); the MFMA waves have no DMA of their own to wait for
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
       if (cc == max(CC - 2, 0)) epi_preload<EPI, NJ>(p, ein, m0, n0, wave, lane);
-      const bool more = k + 1 < nitems;
-      const int cc1 = cc + 1 == CC ? 0 : cc + 1;
-      if constexpr (!PROD) {
-        if (more && cc1 == 0) prep_tile(tk + 1);
-      }
-      auto nd = [&](auto j) {
-        if (more) dma(cc1, st ^ 1, j);
-      };
       if (cc == 0) {
         const int img0 = m0 / HW;
         const int r0 = m0 - img0 * HW;
@@ -634,10 +627,14 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
             xbw[i][d] = x ^ ((x >> 3) & 32);
           }
         }
-        mma_chunk(st, 0, std::true_type{}, nd);
-      } else {
-        mma_chunk(st, cc, std::false_type{}, nd);
+        // (zeroed here, not by a zero-C first chunk on a second MFMA path: with two paths
+        // the accumulators lived in two register sets joined by 64 copies per item)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      mma_chunk(st, cc);
       if (cc == CC - 1 && tk + 1 < ntiles)  // full tile (only the last can end past M)
         epi_tile(m0, std::true_type{});
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
@@ -645,16 +642,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_kernel(IGemmAr
     }
   };
 
-  auto tiles = [&](auto& prep_tile, auto& dma) {
-    for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, prep_tile, dma);
-  };
-  if constexpr (PROD) {
-    int none = 0;
-    tiles(none, none);
-  } else {
-    static_assert(!(EPI & EP_PRE), "the operand transform runs on producer waves");
-    stager([&](auto& prep_tile, auto& dma, auto&, auto&) { tiles(prep_tile, dma); });
-  }
+  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk);
   if (ntiles > 0) epi_tile(m0_of(ntiles - 1), std::integral_constant<bool, FULL>{});
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush<TRED>(p, ss, sq, red, n0, wave, tid);
 }
@@ -946,39 +934,49 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
         }
     }
   };
-  // one 32-channel chunk, all 9 taps (as conv3_halo_kernel's mma_chunk)
-  auto mma_chunk = [&](int st, int cc, auto first) {
-    constexpr bool FIRST = decltype(first)::value;
+  // one 32-channel chunk, all 9 taps: conv3_halo_kernel's fenced schedule (next tap's B
+  // fragments ahead of this tap's MFMAs, A row fragment i behind MFMA group i) and one MFMA
+  // path (accumulators zeroed per tile)
+  auto mma_chunk = [&](int st, int cc) {
     const int hbase = st * HBY;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    bf16x8 a2[2][4], b2[2][4];
-    auto ld = [&](int t, int b) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * P * 64 + xbw[i][t % 3]);
+    bf16x8 a2[4], b2[2][4];
+    auto ld_b = [&](int t, int b) {
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
-    ld(0, 0);
+    auto ld_a = [&](int t, int i) {
+      a2[i] = frag16(hal + hbase + (t / 3 - 1) * P * 64 + xbw[i][t % 3]);
+    };
+    ld_b(0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ld_a(0, i);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+      if (t + 1 < 9) ld_b(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int jn = 0; jn < NJ; ++jn)
-          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
-                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+        for (int jn = 0; jn < NJ; ++jn) acc[i][jn] = mfma16(b2[t & 1][jn], a2[i], acc[i][jn]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < 9) ld_a(t + 1, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   for (int tk = 0; tk < ntiles; ++tk) {
     set_rows(tk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
       if (cc == max(CC - 2, 0)) preload();
-      if (cc == 0) mma_chunk(k % NS, 0, std::true_type{});
-      else mma_chunk(k % NS, cc, std::false_type{});
+      mma_chunk(k % NS, cc);
     }
     epi_tile();
   }
@@ -1568,36 +1566,31 @@ bool conv3_halo_ok(const IGemmArgs& a) {
 // MFMAs cost the MFMA waves ~10 % (round-2 A/B), and the fused BN-backward reduction
 // flavour, reduced per column group (TRED), fits 256 registers without scratch
 
-template <int EPI, bool PROD, int NJ>
+template <int EPI, int NJ>
 static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                           hipStream_t s) {
   const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
-  const dim3 blk(PROD ? 512 : 256);
   if (wres && full)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, PROD, NJ>), dim3(grid), blk, 0, s, a,
-                       h);
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, NJ>), dim3(grid), dim3(512), 0, s, a, h);
   else if (wres)
-    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false, PROD, NJ>), dim3(grid), blk, 0, s, a,
-                       h);
+    hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, false, NJ>), dim3(grid), dim3(512), 0, s, a, h);
   else if (full)
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true, PROD, NJ>), dim3(grid), blk, 0, s, a,
-                       h);
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, true, NJ>), dim3(grid), dim3(512), 0, s, a, h);
   else
-    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false, PROD, NJ>), dim3(grid), blk, 0, s,
-                       a, h);
+    hipLaunchKernelGGL((conv3_halo_kernel<false, EPI, false, NJ>), dim3(grid), dim3(512), 0, s, a, h);
 }
 
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                         hipStream_t s) {
-  launch_halo_k<EPI, true, 4>(wres, grid, a, h, s);
+  launch_halo_k<EPI, 4>(wres, grid, a, h, s);
 }
 
 // N == 32 (plain and statistics epilogues only; producer-wave blocks)
 template <int EPI>
 static void launch_halo32(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
                           hipStream_t s) {
-  launch_halo_k<EPI, true, 2>(wres, grid, a, h, s);
+  launch_halo_k<EPI, 2>(wres, grid, a, h, s);
 }
 
 // Launch (conv3_halo_ok(a) must hold; B K-contiguous with the tap map in a.taps.bt);
@@ -1632,7 +1625,7 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   const int grid = 8 * g8;
   const bool wres = g_halo_wres && a.tiles_n == 1 && h.cc <= 2;
   if (a.pre_aff) {  // (conv3_halo_ok: statistics epilogue, N % 64 == 0)
-    launch_halo_k<EP_STATS | EP_PRE, true, 4>(wres, grid, a, h, s);
+    launch_halo_k<EP_STATS | EP_PRE, 4>(wres, grid, a, h, s);
     return grid;
   }
   if (a.N == 32) {
