@@ -27,8 +27,10 @@ SHAPES = [  # name, H, Cin, Cout, R, stride, pad
     ("l2.ds1x1", 56, 64, 128, 1, 2, 0),
     ("l2.3x3", 28, 128, 128, 3, 1, 1),
     ("l3.3x3s2", 28, 128, 256, 3, 2, 1),
+    ("l3.ds1x1", 28, 128, 256, 1, 2, 0),
     ("l3.3x3", 14, 256, 256, 3, 1, 1),
     ("l4.3x3s2", 14, 256, 512, 3, 2, 1),
+    ("l4.ds1x1", 14, 256, 512, 1, 2, 0),
     ("l4.3x3", 7, 512, 512, 3, 1, 1),
 ]
 ROWS_TILES = [(0, 0), (256, 128), (128, 128), (256, 64), (128, 64)]

@@ -8,10 +8,12 @@ If the host enqueue time per step is close to the synchronized step time, the st
 host-bound and kernel work cannot make it faster.
 """
 import cProfile
+import os
 import pstats
 import sys
 import time
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from mpi_pytorch_amd.engine import build_training
