@@ -1030,7 +1030,10 @@ struct HaloWPlan {
 // frees stage (k + 1) & 1.  PRE (BN in the operand path, WGradArgs::pre_aff): each producer
 // lane transforms the halo pieces its own DMAs wrote, after its vmcnt wait and before the
 // barrier; out-of-image pieces (DMA offset past num_records, zeros) stay zero.
-template <int W2T, bool ONECH = false, bool STRIP = false, bool PROD = false, bool PRE = false>
+// KM: 16-row k fragments per partition (4; 2 when Kout == 32 - DenseNet's growth-rate
+// convs - so the partition's zero upper half costs no MFMA and no fragment read)
+template <int W2T, bool ONECH = false, bool STRIP = false, bool PROD = false, bool PRE = false,
+          int KM = 4>
 __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
   static_assert(PROD || !PRE, "the operand transform runs on producer waves");
   constexpr int HIW = ONECH ? 2 * HW_HIW : HW_HIW;  // halo DMA instructions per wave (chunk)
@@ -1257,9 +1260,9 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
     }
   }
 
-  f32x4 acc[4][9];
+  f32x4 acc[KM][9];
 #pragma unroll
-  for (int km = 0; km < 4; ++km)
+  for (int km = 0; km < KM; ++km)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[km][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -1287,26 +1290,60 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
     // (dh+1)*W2*64, an immediate offset when W2T != 0)
     if constexpr (MORE && !PROD) prep_dma(z + (k + 1) * h.Z);
     const char* sbase = smem + st * HW_STAGE;
+    auto ld_b = [&](int j, s16x4& lo, s16x4& hi) {  // B fragment of step j = 9 ks + t
+      const int ks = j / 9, t = j % 9, off = (t / 3) * W2 * 64;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hbw[ks][0][t % 3] + off));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hbw[ks][1][t % 3] + off));
+    };
+    auto mma = [&](int t, const s16x4& lo, const s16x4& hi, const bf16x8 (&af)[KM]) {
+      s16x8 r;
+      r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+      r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 af[4];
+      for (int km = 0; km < KM; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
+    };
+    if constexpr (PROD) {
+      // Fenced schedule (sched_barrier), as the halo forward: the B fragment of step j + PD
+      // and the next k-step's A fragments (4 steps ahead) are read in front of step j's
+      // MFMAs and cannot sink below them.  Left to itself the scheduler read each tap's B
+      // fragment right in front of its KM MFMAs (64 / 32 cycles), exposing an LDS round
+      // trip per tap.  With KM = 2 for DenseNet's 32-output convs: +0.9 % DenseNet-121,
+      // ResNet-18 within noise (round-5 same-box A/B, profiles/halo_sched_r5.txt).
+      constexpr int PD = KM == 2 ? 6 : 3;
+      s16x4 blo[PD + 1], bhi[PD + 1];
+      bf16x8 af[2][KM];
 #pragma unroll
-      for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sbase + ks * 4096, 16 * km, lane);
+      for (int km = 0; km < KM; ++km) af[0][km] = frag_mn<64>(sbase, 16 * km, lane);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int off = (t / 3) * W2 * 64;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + hbw[ks][0][t % 3] + off));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, smem + hbw[ks][1][t % 3] + off));
-        s16x8 r;
-        r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-        r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, r);
+      for (int j = 0; j < PD; ++j) ld_b(j, blo[j], bhi[j]);
 #pragma unroll
-        for (int km = 0; km < 4; ++km) acc[km][t] = mfma16(bfr, af[km], acc[km][t]);
-        if constexpr (MORE && !PROD) {
-          if (((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
+      for (int j = 0; j < 36; ++j) {
+        const int ks = j / 9, t = j % 9;
+        if (j + PD < 36) ld_b(j + PD, blo[(j + PD) % (PD + 1)], bhi[(j + PD) % (PD + 1)]);
+        if (t == 4 && ks + 1 < 4) {
+#pragma unroll
+          for (int km = 0; km < KM; ++km)
+            af[(ks + 1) & 1][km] = frag_mn<64>(sbase + (ks + 1) * 4096, 16 * km, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(t, blo[j % (PD + 1)], bhi[j % (PD + 1)], af[ks & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 af[KM];
+#pragma unroll
+        for (int km = 0; km < KM; ++km) af[km] = frag_mn<64>(sbase + ks * 4096, 16 * km, lane);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          s16x4 lo, hi;
+          ld_b(ks * 9 + t, lo, hi);
+          mma(t, lo, hi, af);
+          if constexpr (MORE && !PROD) {
+            if (((ks * 9 + t) & 1) == 0) dmaw(st ^ 1, (ks * 9 + t) >> 1);
+          }
         }
       }
     }
@@ -1323,7 +1360,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
   float* dst = p.slab + (int64_t)z * K * ncols;
   const int cw = c0 + 16 * wave;  // this wave's 16 channels (wave-uniform validity)
 #pragma unroll
-  for (int km = 0; km < 4; ++km) {
+  for (int km = 0; km < KM; ++km) {
     const int kk = k0 + 16 * km + li;
     if (k0 + 16 * km >= K || cw >= C) continue;
 #pragma unroll
@@ -1746,8 +1783,12 @@ static void launch_halo_wgrad(const WGradArgs& a, const HaloWPlan& h, dim3 grid,
   }
   if constexpr (!STRIP) {
     if (g_wprod) {
-      hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false>), grid,
-                         dim3(512), 0, s, a, h);
+      if (a.Kout == 32)
+        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false, 2>), grid,
+                           dim3(512), 0, s, a, h);
+      else
+        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false>), grid,
+                           dim3(512), 0, s, a, h);
       return;
     }
   }
