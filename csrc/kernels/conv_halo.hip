@@ -553,44 +553,36 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     }
   };
 
-  // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + NJ B fragments, the next
-  // tap's in flight under this tap's 4 NJ MFMAs.  The schedule is fenced (sched_barrier):
-  // the next tap's B fragments go out in front of this tap's MFMAs and its A row fragment i
-  // right behind MFMA group i (which frees that register), so every read has a whole tap to
-  // land.  Left to itself the scheduler (at ~230 live VGPRs) sank every read to just in
-  // front of its first use, so each group of 4 MFMAs waited out an LDS round trip.  Fenced:
-  // 7-10 % faster in isolation, neutral inside the training step, where the LDS array (the
-  // fragment reads plus the DMA writes, ~90 % of the MFMA time per item) and not the read
-  // latency sets the pace (round 5, profiles/halo_sched_r5.txt).
-  // (Measured earlier: a row-major body that held the chunk's B fragments in registers and
-  // ran the previous tile's epilogue interleaved with the next tile's MFMAs was 10-15 %
-  // slower.)
-  auto mma_chunk = [&](int st, int cc) {
+  // One 32-channel chunk, all 9 taps, tap-outer: per tap 4 A + NJ B fragments (the next
+  // tap's reads issued ahead of this tap's 4 NJ MFMAs).  FIRST: the tile's first chunk
+  // (accumulators start at 0).  (Measured: fencing the reads a tap ahead with
+  // sched_barrier and zeroing the accumulators per tile instead of the FIRST path was 7-10 %
+  // faster in isolation but 0.7 % slower in the training step with side-stream weight
+  // gradients - profiles/halo_sched_r5.txt; a row-major body that held the chunk's B
+  // fragments in registers and ran the previous tile's epilogue interleaved with the next
+  // tile's MFMAs was 10-15 % slower.)
+  auto mma_chunk = [&](int st, int cc, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HB_HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    bf16x8 a2[4], b2[2][4];
-    auto ld_b = [&](int t, int b) {
+    bf16x8 a2[2][4], b2[2][4];
+    auto ld = [&](int t, int b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
-    auto ld_a = [&](int t, int i) {
-      a2[i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
-    };
-    ld_b(0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ld_a(0, i);
+    ld(0, 0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ld_b(t + 1, (t + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jn = 0; jn < NJ; ++jn) acc[i][jn] = mfma16(b2[t & 1][jn], a2[i], acc[i][jn]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < 9) ld_a(t + 1, i);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int jn = 0; jn < NJ; ++jn)
+          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
+                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
     }
   };
 
@@ -627,14 +619,10 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
             xbw[i][d] = x ^ ((x >> 3) & 32);
           }
         }
-        // (zeroed here, not by a zero-C first chunk on a second MFMA path: with two paths
-        // the accumulators lived in two register sets joined by 64 copies per item)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_chunk(st, 0, std::true_type{});
+      } else {
+        mma_chunk(st, cc, std::false_type{});
       }
-      mma_chunk(st, cc);
       if (cc == CC - 1 && tk + 1 < ntiles)  // full tile (only the last can end past M)
         epi_tile(m0, std::true_type{});
       // (no barrier here: item k + 2's DMAs into stage st are issued during item k + 1,
@@ -934,49 +922,39 @@ __global__ __launch_bounds__(512, 1) void conv3_strip_kernel(IGemmArgs p, StripP
         }
     }
   };
-  // one 32-channel chunk, all 9 taps: conv3_halo_kernel's fenced schedule (next tap's B
-  // fragments ahead of this tap's MFMAs, A row fragment i behind MFMA group i) and one MFMA
-  // path (accumulators zeroed per tile)
-  auto mma_chunk = [&](int st, int cc) {
+  // one 32-channel chunk, all 9 taps (as conv3_halo_kernel's mma_chunk)
+  auto mma_chunk = [&](int st, int cc, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
     const int hbase = st * HBY;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
-    bf16x8 a2[4], b2[2][4];
-    auto ld_b = [&](int t, int b) {
+    bf16x8 a2[2][4], b2[2][4];
+    auto ld = [&](int t, int b) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a2[b][i] = frag16(hal + hbase + (t / 3 - 1) * P * 64 + xbw[i][t % 3]);
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
     };
-    auto ld_a = [&](int t, int i) {
-      a2[i] = frag16(hal + hbase + (t / 3 - 1) * P * 64 + xbw[i][t % 3]);
-    };
-    ld_b(0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ld_a(0, i);
+    ld(0, 0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ld_b(t + 1, (t + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jn = 0; jn < NJ; ++jn) acc[i][jn] = mfma16(b2[t & 1][jn], a2[i], acc[i][jn]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < 9) ld_a(t + 1, i);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int jn = 0; jn < NJ; ++jn)
+          acc[i][jn] = mfma16(b2[t & 1][jn], a2[t & 1][i],
+                              (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
     }
   };
   for (int tk = 0; tk < ntiles; ++tk) {
     set_rows(tk);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
       if (cc == max(CC - 2, 0)) preload();
-      mma_chunk(k % NS, cc);
+      if (cc == 0) mma_chunk(k % NS, 0, std::true_type{});
+      else mma_chunk(k % NS, cc, std::false_type{});
     }
     epi_tile();
   }
@@ -1288,12 +1266,29 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
     }
     // (hbw: this tile's B-row bases at row tap dh = -1 in stage st; tap dh adds
     // (dh+1)*W2*64, an immediate offset when W2T != 0)
-    if constexpr (MORE && !PROD) prep_dma(z + (k + 1) * h.Z);
+    // 4-wave form: this tile's B-row bases are copied (hbk) and the next tile's DMA offsets
+    // and bases computed up front, where their index math overlaps this tile's MFMA stream
+    // (computed after the MFMAs instead, as the producer-wave form must for its register
+    // budget, the 4-wave kernel was ~7 % slower: round-5 bisection)
+    int hbk[4][2][3];
+    if constexpr (!PROD) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int d = 0; d < 3; ++d) hbk[ks][e][d] = hbw[ks][e][d];
+      if constexpr (MORE) {
+        prep_dma(z + (k + 1) * h.Z);
+        if constexpr (!STRIP) prep_b(z + (k + 1) * h.Z, st ^ 1);
+      }
+    }
     const char* sbase = smem + st * HW_STAGE;
     auto ld_b = [&](int j, s16x4& lo, s16x4& hi) {  // B fragment of step j = 9 ks + t
       const int ks = j / 9, t = j % 9, off = (t / 3) * W2 * 64;
-      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hbw[ks][0][t % 3] + off));
-      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hbw[ks][1][t % 3] + off));
+      const int (&hb)[4][2][3] = PROD ? hbw : hbk;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hb[ks][0][t % 3] + off));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, smem + hb[ks][1][t % 3] + off));
     };
     auto mma = [&](int t, const s16x4& lo, const s16x4& hi, const bf16x8 (&af)[KM]) {
       s16x8 r;
@@ -1349,7 +1344,7 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
     }
     // the next tile's B-row addresses (its stage is the other one), after this tile's last
     // fragment reads
-    if constexpr (MORE) prep_b(z + (k + 1) * h.Z, st ^ 1);
+    if constexpr (MORE && (PROD || STRIP)) prep_b(z + (k + 1) * h.Z, st ^ 1);
     // (no barrier: tile k + 2's DMAs into stage st follow tile k + 1's top barrier)
   };
   for (int k = 0; k + 1 < ntiles; ++k) tile(k, std::true_type{});

@@ -97,11 +97,26 @@ def _capture_blocks_streams() -> bool:
     return torch.cuda.is_current_stream_capturing()
 
 
+# Halo weight-gradient form per step (unless MPA_HALO_WPROD pins it): the 4-wave kernel
+# while the weight gradients run on the side stream, the producer-wave kernel when they
+# share the compute stream (data parallelism).  Same-box round-5 A/B, ResNet-18 b1024:
+# side stream 51.9k (4-wave) vs 51.0k (producer waves) img/s, one stream 50.4k vs 50.7k
+# (profiles/halo_sched_r5.txt).
+_WPROD_PINNED = "MPA_HALO_WPROD" in os.environ
+
+
+def _halo_wgrad_form(side_on: bool) -> None:
+    if not _WPROD_PINNED:
+        _ext.ext().igemm_set_halo_wprod(0 if side_on else 1)
+
+
 def wgrad_stream_begin(enabled: bool = True) -> None:
     """Route the following conv weight gradients to the side stream (TrainStep backward)."""
     _SIDE["on"] = bool(enabled and _WGRAD_STREAM)
-    if _SIDE["on"] and torch.cuda.is_available():
-        _SIDE["main"] = torch.cuda.current_stream()
+    if torch.cuda.is_available():
+        _halo_wgrad_form(_SIDE["on"])
+        if _SIDE["on"]:
+            _SIDE["main"] = torch.cuda.current_stream()
 
 
 def wgrad_streams():
