@@ -32,7 +32,6 @@
 #include <map>
 #include <mutex>
 #include <string>
-#include <type_traits>
 #include "igemm_common.h"
 
 namespace mpa {
@@ -410,58 +409,37 @@ __global__ __launch_bounds__(256, OCC) void igemm_wgrad_kernel(WGradArgs p) {
 
 }
 
-// dw[i] += sum_z slab[z][i] (dw[i] = ... when overwrite).  A block owns 256/G float4
-// columns; its G thread groups sum disjoint z-strided shares of the splits with 8 float4
-// loads in flight per lane, then combine through LDS in a fixed order.  The halo weight
-// gradients of a small layer write ~256 splits of a 64 x 576 output (37.7 MB): with 4 groups
-// of 64 columns that was 144 blocks with 4 loads in flight per lane, latency-bound at
-// ~2.4 TB/s (16 us per launch, 20 per ResNet-18 step); G = 16 gives 576 blocks and 4x the
-// bytes in flight.
-template <int G>
+// dw[i] += sum_z slab[z][i] (dw[i] = ... when overwrite).  A block owns 64 float4 columns; its 4 waves sum disjoint
+// quarters of the splits (4 float4 loads in flight per lane), then reduce through LDS.
+// With ~100 splits of a small layer (ResNet-18 layer1: 64 x 576 outputs) a
+// one-thread-per-column walk over the splits ran at ~0.6 TB/s on 36 blocks.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int S,
                                                             int64_t n, float* __restrict__ dw,
                                                             int overwrite) {
-  constexpr int CW = 256 / G;
-  __shared__ f32x4 red[G][CW];
+  __shared__ f32x4 red[4][64];
   const int64_t n4 = n / 4;
-  const int cl = threadIdx.x % CW, g = threadIdx.x / CW;
-  const int64_t c = blockIdx.x * (int64_t)CW + cl;
+  const int64_t c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   if (c < n4) {
     const f32x4* src = (const f32x4*)slab + c;
+    const int64_t stride = n4;  // one split = n4 float4
     int z = g;
-    for (; z + 7 * G < S; z += 8 * G) {
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(z + u * G) * n4];
-      acc += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    for (; z + 12 < S; z += 16) {
+      const f32x4 a = src[(int64_t)z * stride], b = src[(int64_t)(z + 4) * stride];
+      const f32x4 d = src[(int64_t)(z + 8) * stride], e = src[(int64_t)(z + 12) * stride];
+      acc += (a + b) + (d + e);
     }
-    for (; z < S; z += G) acc += src[(int64_t)z * n4];
+    for (; z < S; z += 4) acc += src[(int64_t)z * stride];
   }
-  red[g][cl] = acc;
+  red[g][threadIdx.x & 63] = acc;
   __syncthreads();
   if (g == 0 && c < n4) {
+    const int t = threadIdx.x;
     f32x4 v = overwrite ? f32x4{0.f, 0.f, 0.f, 0.f} : ((f32x4*)dw)[c];
-    f32x4 t = red[0][cl];
-#pragma unroll
-    for (int k = 1; k < G; ++k) t += red[k][cl];
-    ((f32x4*)dw)[c] = v + t;
+    v += (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    ((f32x4*)dw)[c] = v;
   }
-}
-
-// float4 rows (n % 4 == 0): more split groups per block the more splits there are
-static void wgrad_reduce4(const float* slab, int S, int64_t n, float* dw, int overwrite,
-                          hipStream_t s) {
-  const int64_t n4 = n / 4;
-  auto go = [&](auto gc) {
-    constexpr int G = decltype(gc)::value;
-    const int blocks = (int)std::max<int64_t>(1, (n4 + 256 / G - 1) / (256 / G));
-    hipLaunchKernelGGL((wgrad_reduce_kernel<G>), dim3(blocks), dim3(256), 0, s, slab, S, n, dw,
-                       overwrite);
-  };
-  if (S >= 64) go(std::integral_constant<int, 16>{});
-  else if (S >= 16) go(std::integral_constant<int, 8>{});
-  else go(std::integral_constant<int, 4>{});
 }
 
 // any n (split rows not 16-B aligned when n % 4 != 0): one thread per element
@@ -1210,13 +1188,18 @@ static void tuned_wgrad_tile(const WGradArgs& a, int vwa, int vwb, hipStream_t s
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s) {
   if (igemm_engine() >= 1 && conv3_halo_wgrad_ok(a)) {  // 3x3 / stride 1: halo-staged
     const int z = conv3_halo_wgrad(a, s);
-    // Ncols = 9C, C % 32 == 0: float4 rows
-    wgrad_reduce4(a.slab, z, (int64_t)a.Kout * a.Ncols, a.dw, a.overwrite, s);
+    const int64_t n = (int64_t)a.Kout * a.Ncols;  // Ncols = 9C, C % 32 == 0: float4 rows
+    const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
+                       a.overwrite);
     return;
   }
   if (igemm_engine() >= 1 && stem_wgrad_ok(a)) {  // pixel-pair 7x7 stem: halo-staged
     const int z = stem_wgrad(a, s);
-    wgrad_reduce4(a.slab, z, (int64_t)a.Kout * a.Ncols, a.dw, a.overwrite, s);
+    const int64_t n = (int64_t)a.Kout * a.Ncols;
+    const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
+                       a.overwrite);
     return;
   }
   const bool dma_ok = vwa == 8 && vwb == 8 && igemm_engine() >= 1;
@@ -1245,7 +1228,9 @@ static void wgrad_run_plan(WGradArgs a, int vwa, int vwb, hipStream_t s, int tbm
   if (splits > 1) {
     const int64_t n = (int64_t)a.Kout * a.Ncols;
     if (n % 4 == 0) {  // float4 path: 16-B aligned split rows
-      wgrad_reduce4(a.slab, splits, n, a.dw, a.overwrite, s);
+      const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, splits, n,
+                         a.dw, a.overwrite);
     } else {
       const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
       hipLaunchKernelGGL(wgrad_reduce_scalar_kernel, dim3(blocks), dim3(256), 0, s, a.slab,
