@@ -22,16 +22,24 @@ hangs forever on a lost peer):
   * warm-up and timed steps run under the device-completion watchdog (--watchdog seconds,
     parallel/watchdog.py): a rank whose GPU stops completing steps dumps its stacks and exits
     75 with a rank-tagged message, and the launcher tears the job down;
-  * the headline record is built right after the timed steps.  The optional extras after it
-    (multi-GPU decision variants, the small-batch pass) each run in try/except, and all of
-    them under one wall-clock budget (--extras-budget): an error is recorded in the line
-    ("error" fields), a hang prints the headline line anyway and ends every rank with 0.
+  * the headline record is built AND PRINTED (flushed) right after the timed steps, before
+    any optional extra runs.  The extras after it (multi-GPU decision variants, the
+    small-batch pass) each run in try/except, all under one wall-clock budget
+    (--extras-budget); when they finish, rank 0 prints a second, complete record (the same
+    headline fields plus the extras).  An extra's exception is recorded in that record
+    ("error" fields); a hang ends every rank with 0 after the budget (the headline is
+    already out); a native abort or GPU fault inside an extra ends the job non-zero with
+    the launcher naming the rank, and the headline line is still on stdout.  A backstop
+    that needs no Python thread (faulthandler.dump_traceback_later) ends a rank stuck in a
+    native call that holds the GIL, where neither the watchdog thread nor the budget timer
+    can run: stacks on stderr, exit 1.
   Test hooks (tests/test_launch_cpu.py): MPA_BENCH_INJECT=variant_raise | extras_hang |
-  hang_rank=R.
+  hang_rank=R | extras_abort=R (rank R dies with os._exit(134) inside the extras).
 """
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -152,38 +160,57 @@ def _inject() -> str:
 
 
 class _Emitter:
-    """Prints rank 0's JSON record exactly once, from the main thread or from the extras
-    deadline (whichever comes first)."""
+    """Rank 0's JSON lines: the headline record as soon as it is built, then - once the
+    extras are done - one complete record (headline fields + extras).  The final record is
+    printed at most once, from the main thread or not at all (the extras deadline)."""
 
     def __init__(self, rank: int):
         self.rank = rank
         self._lock = threading.Lock()
         self.done = False
 
-    def emit(self, rec: dict) -> bool:
+    def _print(self, rec: dict) -> None:
+        if self.rank == 0:
+            print(json.dumps(rec), flush=True)
+
+    def headline(self, rec: dict) -> None:
+        with self._lock:
+            self._print(dict(rec))
+
+    def final(self, rec: dict) -> bool:
         with self._lock:
             if self.done:
                 return False
             self.done = True
-        if self.rank == 0:
-            print(json.dumps(rec), flush=True)
-        return True
+            self._print(dict(rec))
+            return True
+
+    def expire(self) -> bool:
+        """The extras budget ran out: no final record (the headline is already out)."""
+        with self._lock:
+            if self.done:
+                return False
+            self.done = True
+            return True
 
 
-def _deadline(seconds: float, emitter: _Emitter, rec: dict, rank: int):
-    """Arm the extras budget: on expiry rank 0 prints the headline record (with
-    ``extras_error``) and every rank exits 0 - the headline measurement is complete and
-    valid; only the optional extras after it are lost."""
+def _deadline(seconds: float, emitter: _Emitter, rank: int):
+    """Arm the extras budget: on expiry every rank exits 0 - the headline measurement is
+    complete, valid and already printed; only the optional extras after it are lost.  A
+    faulthandler backstop (no Python thread, no GIL) ends a rank whose main thread is stuck
+    inside a native call 30 s later."""
     def fire():
-        rec["extras_error"] = "timeout: extras exceeded %.0f s" % seconds
-        sys.stderr.write("bench.py rank %d: %s; headline kept\n" % (rank, rec["extras_error"]))
-        sys.stderr.flush()
-        emitter.emit(rec)
-        sys.stdout.flush()
-        os._exit(0)
+        try:
+            if emitter.expire():
+                sys.stderr.write("bench.py rank %d: timeout: extras exceeded %.0f s; headline "
+                                 "kept\n" % (rank, seconds))
+                sys.stderr.flush()
+        finally:
+            os._exit(0)
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
+    faulthandler.dump_traceback_later(seconds + 30.0, exit=True)
     return t
 
 
@@ -405,12 +432,16 @@ def run(args) -> None:
     # completing steps (a peer lost inside a collective) exits 75 instead of hanging
     from mpi_pytorch_amd.parallel.watchdog import Watchdog
     wd = Watchdog(args.watchdog, rank=world.rank, name="bench").start()
+    if args.watchdog > 0:  # (no Python thread: fires even with the GIL held by a native call)
+        faulthandler.dump_traceback_later(args.watchdog + 60.0, exit=True)
     inject = _inject()
     hang_rank = int(inject.split("=", 1)[1]) if inject.startswith("hang_rank=") else -1
     nbeat = [0]
 
     def beat():
         nbeat[0] += 1
+        if args.watchdog > 0:  # re-arm the GIL-free backstop: it measures time since a beat
+            faulthandler.dump_traceback_later(args.watchdog + 60.0, exit=True)
         if cuda:
             ev = torch.cuda.Event()
             ev.record()
@@ -467,6 +498,7 @@ def run(args) -> None:
     sync()
     dt = time.perf_counter() - t0
     wd.stop()
+    faulthandler.cancel_dump_traceback_later()
     loss = step.mean_loss()
     phases = step.timer.summary() if step.timer is not None else None
     comm = step.bucketer.comm_stats()
@@ -525,11 +557,15 @@ def run(args) -> None:
     if affinity() is not None:
         rec["host_affinity"] = affinity()
 
-    # ---- optional extras, each guarded, all under one wall-clock budget
+    # ---- the headline line goes out now: nothing after this point can lose it
     emitter = _Emitter(world.rank)
-    timer = _deadline(args.extras_budget, emitter, rec, world.rank)
+    emitter.headline(rec)
+    # ---- optional extras, each guarded, all under one wall-clock budget
+    timer = _deadline(args.extras_budget, emitter, world.rank)
     if inject == "extras_hang":
         time.sleep(1e6)
+    if inject.startswith("extras_abort=") and world.rank == int(inject.split("=", 1)[1]):
+        os._exit(134)  # test hook: a native abort inside an extra
     if world.world_size > 1 and not args.emulate_comm and args.decisions:
         rec["multi_gpu"] = _guarded("multi_gpu", lambda: _multi_gpu_decisions(
             step, data, args, world, sync))
@@ -552,7 +588,9 @@ def run(args) -> None:
             return small
         rec["small_batch"] = _guarded("small_batch", small_pass)
     timer.cancel()
-    emitter.emit(rec)
+    faulthandler.cancel_dump_traceback_later()
+    if "multi_gpu" in rec or "small_batch" in rec:
+        emitter.final(rec)
     data.close()
     from mpi_pytorch_amd.parallel import shutdown
     shutdown()

@@ -1035,6 +1035,85 @@ Tensor maxpool_bn_bwd(Tensor dp, Tensor idx, Tensor z, Tensor mean, Tensor rstd,
   return dz;
 }
 
+// ---- fused stem backward (round 6): pooled-only sums, then the weight gradient that forms
+// dz in its operand staging (conv_stem.hip stem_wgrad_kernel<KS, true>)
+Tensor maxpool_bn_bwd_sums(Tensor dp, Tensor zsel, Tensor mean, Tensor rstd, Tensor gamma,
+                           Tensor beta, Tensor dgamma, Tensor dbeta) {
+  CHECK_ACT(dp);
+  CHECK_ACT(zsel);
+  TORCH_CHECK(zsel.sizes() == dp.sizes() && dp.dim() == 4 && dp.size(3) % 8 == 0,
+              "maxpool_bn_bwd_sums: shapes");
+  const int C = dp.size(3);
+  const int MP = dp.numel() / C;
+  const c10::OptionalDeviceGuard g(device_of(dp));
+  Tensor ws = torch::empty({mpa::maxpool_bn_ws_floats(MP, C)}, dp.options().dtype(torch::kFloat32));
+  mpa::maxpool_bn_bwd_sums(bp(dp), bp(zsel), fopt(mean), fopt(rstd), fopt(gamma), fopt(beta),
+                           fopt_mut(dgamma), fopt_mut(dbeta), MP, C, ws.data_ptr<float>(),
+                           cur_stream());
+  return ws.narrow(0, 0, 2 * C);
+}
+
+static mpa::WGradArgs stem_pool_args(const Tensor& z, const Tensor& x, const Tensor& dw,
+                                     int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                                     bool overwrite) {
+  mpa::WGradArgs a{};
+  a.dy = bp(z); a.x = bp(x); a.dw = dw.data_ptr<float>();
+  a.Kout = z.size(3); a.C = x.size(3); a.H = x.size(1); a.W = x.size(2);
+  a.P = z.size(1); a.Q = z.size(2); a.R = dw.size(1); a.S = dw.size(2);
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
+  a.Mpix = z.size(0) * a.P * a.Q;
+  a.Ncols = a.R * a.S * a.C;
+  a.overwrite = overwrite ? 1 : 0;
+  return a;
+}
+
+static mpa::StemPoolArgs stem_pool_q(const Tensor& dp, const Tensor& idx, const Tensor& mean,
+                                     const Tensor& rstd, const Tensor& gamma, const Tensor& beta,
+                                     const Tensor& sums) {
+  mpa::StemPoolArgs q{};
+  q.dp = bp(dp); q.idx = idx.data_ptr<uint8_t>();
+  q.mean = fopt(mean); q.rstd = fopt(rstd); q.gamma = fopt(gamma); q.beta = fopt(beta);
+  q.sums = fopt(sums);
+  q.PP = dp.size(1); q.PQ = dp.size(2);
+  return q;
+}
+
+bool stem_pool_wgrad_ok(Tensor dp, Tensor idx, Tensor z, Tensor x, Tensor dw, int64_t sh,
+                        int64_t sw, int64_t ph, int64_t pw) {
+  if (!dp.is_cuda() || !z.is_cuda() || !x.is_cuda() || dp.dim() != 4 || z.dim() != 4 ||
+      x.dim() != 4 || dw.dim() != 4 || !dp.is_contiguous() || !z.is_contiguous() ||
+      !x.is_contiguous() || !idx.is_contiguous() || idx.sizes() != dp.sizes() ||
+      dp.size(0) != z.size(0) || x.size(0) != z.size(0) || dp.size(3) != z.size(3) ||
+      dw.size(0) != z.size(3) || dw.size(3) != x.size(3) ||
+      dp.scalar_type() != torch::kBFloat16 || z.scalar_type() != torch::kBFloat16 ||
+      x.scalar_type() != torch::kBFloat16 || dw.scalar_type() != torch::kFloat32)
+    return false;
+  mpa::WGradArgs a = stem_pool_args(z, x, dw, sh, sw, ph, pw, false);
+  a.slab = reinterpret_cast<float*>(16);  // (checked for presence and alignment only)
+  mpa::StemPoolArgs q{};
+  q.dp = bp(dp); q.idx = idx.data_ptr<uint8_t>();
+  q.mean = q.rstd = q.gamma = q.beta = q.sums = reinterpret_cast<const float*>(16);
+  q.PP = dp.size(1); q.PQ = dp.size(2);
+  return mpa::igemm_engine() >= 1 && mpa::stem_pool_wgrad_ok(a, q);
+}
+
+void stem_pool_wgrad(Tensor dp, Tensor idx, Tensor z, Tensor mean, Tensor rstd, Tensor gamma,
+                     Tensor beta, Tensor sums, Tensor x, Tensor dw, int64_t sh, int64_t sw,
+                     int64_t ph, int64_t pw, bool overwrite) {
+  CHECK_ACT(dp);
+  CHECK_ACT(z);
+  CHECK_ACT(x);
+  CHECK_F32(dw);
+  CHECK_CONTIG(dw);
+  const c10::OptionalDeviceGuard g(device_of(z));
+  mpa::WGradArgs a = stem_pool_args(z, x, dw, sh, sw, ph, pw, overwrite);
+  Tensor slab;
+  a.slab = alloc_ws(slab, z, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
+  const mpa::StemPoolArgs q = stem_pool_q(dp, idx, mean, rstd, gamma, beta, sums);
+  TORCH_CHECK(mpa::stem_pool_wgrad_ok(a, q), "stem_pool_wgrad: unsupported geometry");
+  mpa::igemm_stem_pool_wgrad(a, q, cur_stream());
+}
+
 // x: contiguous NHWC or a channel-window view of a wider buffer (pixel stride ldx)
 Tensor avgpool_fwd(Tensor x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
                    int64_t pw, bool ceil, bool cip) {
@@ -1609,6 +1688,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fixed-order reductions + no timing-based autotuning (MPA_DETERMINISTIC)");
   m.def("deterministic", &mpa::deterministic);
   m.def("igemm_tuned_table", &mpa::igemm_tuned_table, "autotuned GEMM tiles so far");
+  m.def("igemm_tuned_load", &mpa::igemm_tuned_load, py::arg("table"), py::arg("replace") = true,
+        "adopt an igemm_tuned_table() dump (data-parallel ranks take rank 0's)");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");
   m.def("igemm_set_halo_strip", &mpa::igemm_set_halo_strip,
@@ -1683,6 +1764,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("ceil"), py::arg("counter") = py::none(),
         py::arg("zsel_out") = py::none());
+  m.def("maxpool_bn_bwd_sums", &maxpool_bn_bwd_sums);
+  m.def("stem_pool_wgrad_ok", &stem_pool_wgrad_ok);
+  m.def("stem_pool_wgrad", &stem_pool_wgrad);
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dp"), py::arg("idx"), py::arg("z"),
         py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("beta"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"),

@@ -179,6 +179,8 @@ void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: 
 // tile autotuner (igemm.hip): on by default (MPA_TUNE=0 off); the cached choices as text
 void igemm_set_tune(int on);
 std::string igemm_tuned_table();
+// adopt a table in igemm_tuned_table()'s format (replace: drop the current entries first)
+int igemm_tuned_load(const std::string& table, bool replace);
 void igemm_set_dma_uni(int on);  // LDS-DMA uniform-tap fast path (default on)
 bool igemm_stap_ok();  // super-tap forward available (engine >= 1 and fast path on)
 // conv_halo.hip: halo-staged direct 3x3 / stride-1 conv (forward and stride-1 dgrad with
@@ -194,6 +196,20 @@ void igemm_set_halo_strip(int mode);  // MPA_HALO_STRIP (0 off, 1 wide images, 2
 bool stem_wgrad_ok(const WGradArgs& a);
 int stem_wgrad(WGradArgs a, hipStream_t s);
 int64_t stem_wgrad_ws_floats();
+// the same weight gradient with the stem's BN + ReLU + 3x3/s2/p1 max-pool backward formed in
+// its operand staging (a.dy = the conv output z; dz is never written): partials into a.slab
+struct StemPoolArgs {
+  const bf16_raw* dp;    // pooled gradient [N][PP][PQ][64]
+  const uint8_t* idx;    // window argmax tap (3 i + k) [N][PP][PQ][64]
+  const float *mean, *rstd, *gamma, *beta;
+  const float* sums;     // [2][64]: sum g, sum g xhat over the batch (maxpool_bn_bwd_sums)
+  int PP, PQ;            // pooled extent (P / 2, Q / 2)
+  float invM;            // set by stem_pool_wgrad
+};
+bool stem_pool_wgrad_ok(const WGradArgs& a, const StemPoolArgs& q);
+int stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s);
+// stem_pool_wgrad + the slab reduction into a.dw
+void igemm_stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s);
 bool conv3_halo_wgrad_ok(const WGradArgs& a);
 void igemm_set_halo_wprod(int on);  // producer-wave halo weight gradients (MPA_HALO_WPROD)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
@@ -311,6 +327,10 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
                          int ph, int pw, bf16_raw* y, uint8_t* idx, float* mean, float* rstd,
                          int64_t* counter, hipStream_t s, bf16_raw* zsel = nullptr);
 int64_t maxpool_bn_ws_floats(int M, int C);
+// pooled-only backward reduction of the fused stem: sums (ws[0 .. 2C)) and dgamma / dbeta
+void maxpool_bn_bwd_sums(const bf16_raw* dp, const bf16_raw* zsel, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, float* dgamma,
+                         float* dbeta, int MP, int C, float* ws, hipStream_t s);
 void maxpool_bn_bwd(const bf16_raw* dp, const uint8_t* idx, const bf16_raw* z, const float* mean,
                     const float* rstd, const float* gamma, const float* beta, float* dgamma,
                     float* dbeta, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh,

@@ -1799,6 +1799,30 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
                      (unsigned long long*)counter, zsel);
 }
 
+__global__ void bn_sums_grad_kernel(const float* __restrict__ sums, int C,
+                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (dgamma) dgamma[c] += sums[C + c];
+  if (dbeta) dbeta[c] += sums[c];
+}
+
+// the fused stem backward's pooled-only half: (sum g, sum g xhat) into ws[0 .. 2C) and the
+// (gamma, beta) gradients; the dz pass itself runs inside the stem weight gradient
+// (stem_pool_wgrad, conv_stem.hip)
+void maxpool_bn_bwd_sums(const bf16_raw* dp, const bf16_raw* zsel, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, float* dgamma,
+                         float* dbeta, int MP, int C, float* ws, hipStream_t s) {
+  float* slab = ws + 2 * C;
+  const dim3 gr = grid_for(MP, C, stem_grid(1));
+  hipLaunchKernelGGL(maxpool_bn_bwd_sel_reduce_kernel, gr, dim3(256), 0, s, dp, zsel, mean, rstd,
+                     gamma, beta, C, MP, slab, ws);
+  slab_reduce(slab, gr.x, 2 * C, ws, false, s);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(bn_sums_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, dgamma,
+                       dbeta);
+}
+
 int64_t maxpool_bn_ws_floats(int M, int C) {
   return (int64_t)grid_for(M, C, stem_grid(1)).x * 2 * C + 2 * C;
 }

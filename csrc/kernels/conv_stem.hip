@@ -275,8 +275,22 @@ struct StemWPlan {
   int ks;                // K-steps per item: ceil(2 Q / 32) (= the kernel's KS)
 };
 
-template <int KS>
-__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h) {
+// ---------------------------------------------------------------------------------------
+// POOL form (round 6): the stem's BN + ReLU + 3x3/s2/p1 max-pool backward runs INSIDE the
+// weight gradient's staging, so the full-resolution dz is never written or read back.
+// An item (output rows 2t, 2t+1) is exactly one row of 2x2 cells; cell (t, c) is covered
+// by the pooled windows (t | t+1, c | c+1).  Per (cell, 8 channels) a thread gathers the 4
+// windows' pooled gradient dp and argmax taps plus the cell's 4 z vectors (issued under the
+// previous item's MFMAs, like the dz loads they replace), then writes
+//   dz = a g + b + cco z,  g = sum of dp over windows whose argmax is this pixel, masked
+//        by bn(z) > 0  (a = gamma rstd, b / cco from the pooled sums (sum g, sum g xhat))
+// to the dz stage - the arithmetic of maxpool_bn_bwd_cell_kernel<true> (bn.hip), so the
+// staged operand is the one the two-pass form wrote to memory.  Reference: the stem
+// conv1 -> bn1 -> relu -> maxpool of torchvision resnet / densenet (models.py:24-30, 74-80).
+// (StemPoolArgs: api.h)
+template <int KS, bool POOL>
+__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h,
+                                                            StemPoolArgs pa) {
   __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -305,19 +319,65 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
     const int v = tid + 256 * i, row = v >> 3, chunk = v & 7;
     dzoff[i] = (row >> 5) * 4096 + mn_off<64>(row & 31, chunk * 8);
   }
-  const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors]
+  const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors] (POOL: z)
   const u32x4* const cvsrc = (const u32x4*)p.x;    // [n][Hc][Wc] pair vectors
-  u32x4 pdz[KS], pcv[SW_CVPT];
+  constexpr int NDZ = POOL ? 1 : KS;
+  u32x4 pdz[NDZ], pcv[SW_CVPT];
+  // POOL: (cell, 8-channel chunk) units u = tid + 256 i (cell u >> 3 < Q / 2, chunk u & 7,
+  // the same tid & 7 for both i), their gathered windows and z vectors, and the chunk's
+  // BN-backward constants (bn_coeffs + maxpool_bn_bwd_cell_kernel<true>'s a, b, cco)
+  constexpr int PU = POOL ? 2 : 1;
+  const int pch = (tid & 7) * 8;
+  u32x4 qdp[PU][4], qz[PU][4];
+  u32x2 qix[PU][4];
+  float bsc[8], bsh[8], bb0[8], bcc[8];
+  if constexpr (POOL) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = pch + j;
+      const float mu = pa.mean[c], rs = pa.rstd[c];
+      bsc[j] = pa.gamma[c] * rs;
+      bsh[j] = pa.beta[c] - mu * bsc[j];
+      bcc[j] = -bsc[j] * rs * pa.sums[64 + c] * pa.invM;
+      bb0[j] = -bsc[j] * pa.sums[c] * pa.invM - bcc[j] * mu;
+    }
+    // K-step rows past 2 Q are never staged: zero them once in both stages
+    const int r0 = 2 * Q;
+    const int zb = (r0 >> 5) * 4096 + (r0 & 31) * 128, ze = KS * 4096;
+    for (int s2 = 0; s2 < 2; ++s2)
+      for (int b = zb + tid * 16; b < ze; b += 256 * 16)
+        *LDS_PTR(u32x4, smem + s2 * SW_STAGE + b) = u32x4{0u, 0u, 0u, 0u};
+  }
   auto fetch = [&](int it) {  // item it's vectors into registers (zeros past its end)
     const int n = it / h.items_img, oh0 = (it - n * h.items_img) * 2;
-    const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
     const size_t cv0 = ((size_t)n * Hc + 2 * oh0) * Wc;
     const int cvlim = min(SW_CROWS, Hc - 2 * oh0) * Wc;
+    if constexpr (POOL) {
+      const int t = oh0 >> 1;
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      const int v = tid + 256 * i;
-      pdz[i] = (v >> 3) < nval ? dzsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
-                               : u32x4{0u, 0u, 0u, 0u};
+      for (int i = 0; i < PU; ++i) {
+        const int u = tid + 256 * i;
+        const int cq = u < 4 * Q ? (u >> 3) : 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // out-of-range windows load a clamped one (masked)
+          const int wp = min(t + (w >> 1), pa.PP - 1), wq = min(cq + (w & 1), pa.PQ - 1);
+          const size_t o = (((size_t)n * pa.PP + wp) * pa.PQ + wq) * 64 + pch;
+          qdp[i][w] = *(const u32x4*)(pa.dp + o);
+          qix[i][w] = *(const u32x2*)(pa.idx + o);
+        }
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4)
+          qz[i][w4] = dzsrc[((size_t)(n * P + oh0 + (w4 >> 1)) * Q + 2 * cq + (w4 & 1)) * 8 +
+                            (pch >> 3)];
+      }
+    } else {
+      const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
+#pragma unroll
+      for (int i = 0; i < KS; ++i) {
+        const int v = tid + 256 * i;
+        pdz[i] = (v >> 3) < nval ? dzsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
+                                 : u32x4{0u, 0u, 0u, 0u};
+      }
     }
 #pragma unroll
     for (int i = 0; i < SW_CVPT; ++i) {
@@ -325,10 +385,53 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  auto commit = [&](int stage) {
+  auto commit = [&](int stage, int it) {
     char* st = smem + stage * SW_STAGE;
+    if constexpr (POOL) {
+      const int t = (it - (it / h.items_img) * h.items_img);  // cell row = oh0 / 2
 #pragma unroll
-    for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
+      for (int i = 0; i < PU; ++i) {
+        const int u = tid + 256 * i;
+        if (u >= 4 * Q) continue;
+        const int cq = u >> 3;
+        uint2 iv[4];
+        float d[4][8];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const bool ok = t + (w >> 1) < pa.PP && cq + (w & 1) < pa.PQ;
+          iv[w] = ok ? make_uint2(qix[i][w][0], qix[i][w][1]) : make_uint2(~0u, ~0u);
+          unpack8(make_uint4(qdp[i][w][0], qdp[i][w][1], qdp[i][w][2], qdp[i][w][3]), d[w]);
+        }
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4) {
+          const int a0 = w4 >> 1, b0 = w4 & 1;  // pixel (2t + a0, 2 cq + b0)
+          float zr[8];
+          unpack8(make_uint4(qz[i][w4][0], qz[i][w4][1], qz[i][w4][2], qz[i][w4][3]), zr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const int du = w >> 1, eu = w & 1;
+              // rows {t: tap 1 + a0} (+ {t + 1: tap 0} if a0), columns likewise
+              if ((du && !a0) || (eu && !b0)) continue;
+              const int ti = du ? 0 : 1 + a0, tk = eu ? 0 : 1 + b0;
+              const uint32_t word = j < 4 ? iv[w].x : iv[w].y;
+              if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[w][j];
+            }
+            const float gr = (zr[j] * bsc[j] + bsh[j] > 0.f) ? acc : 0.f;
+            zr[j] = bsc[j] * gr + bb0[j] + bcc[j] * zr[j];
+          }
+          const int pl = a0 * Q + 2 * cq + b0;
+          const uint4 o = pack8(zr);
+          *LDS_PTR(u32x4, st + (pl >> 5) * 4096 + mn_off<64>(pl & 31, pch)) =
+              u32x4{o.x, o.y, o.z, o.w};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
+    }
 #pragma unroll
     for (int i = 0; i < SW_CVPT; ++i) {
       const int v = tid + 256 * i;
@@ -366,7 +469,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
   int it = blockIdx.x;
   if (it < h.items) {
     fetch(it);
-    commit(0);
+    commit(0, it);
   }
   for (int k = 0; it < h.items; ++k, it += G) {
     const int st = k & 1;
@@ -389,7 +492,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
         for (int km = 0; km < 4; ++km)
           acc[km][i] = mfma16(bf[ks & 1][i], af[ks & 1][km], acc[km][i]);
     }
-    if (more) commit(st ^ 1);
+    if (more) commit(st ^ 1, it + G);
   }
   // partial of this block -> slab row blockIdx.x: dw[k][col], k = 16 km + lane % 16,
   // col = 16 j + 4 (lane / 16) .. +3
@@ -425,9 +528,38 @@ int stem_wgrad(WGradArgs a, hipStream_t s) {
   h.items = nimg * h.items_img;
   h.ks = (2 * a.Q + 31) / 32;
   const int grid = std::max(1, std::min(h.items, std::min(HALO_MAX_ROWS, active_cus())));
+  const StemPoolArgs none{};
   switch (h.ks) {
-#define SW_CASE(K) \
-  case K: hipLaunchKernelGGL(stem_wgrad_kernel<K>, dim3(grid), dim3(256), 0, s, a, h); break;
+#define SW_CASE(K)                                                                          \
+  case K:                                                                                   \
+    hipLaunchKernelGGL((stem_wgrad_kernel<K, false>), dim3(grid), dim3(256), 0, s, a, h, none); \
+    break;
+    SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
+#undef SW_CASE
+  }
+  return grid;
+}
+
+bool stem_pool_wgrad_ok(const WGradArgs& a, const StemPoolArgs& q) {
+  // 3x3 / s2 / p1 pool over an even conv output: every item is one full row of 2x2 cells
+  return stem_wgrad_ok(a) && a.P % 2 == 0 && a.Q % 2 == 0 && q.PP * 2 == a.P &&
+         q.PQ * 2 == a.Q && q.dp && q.idx && q.mean && q.rstd && q.gamma && q.beta && q.sums &&
+         ((reinterpret_cast<uintptr_t>(q.dp) | reinterpret_cast<uintptr_t>(q.idx)) & 15) == 0;
+}
+
+int stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s) {
+  StemWPlan h{};
+  const int nimg = a.Mpix / (a.P * a.Q);
+  h.items_img = a.P / 2;
+  h.items = nimg * h.items_img;
+  h.ks = (2 * a.Q + 31) / 32;
+  q.invM = 1.f / (float)a.Mpix;
+  const int grid = std::max(1, std::min(h.items, std::min(HALO_MAX_ROWS, active_cus())));
+  switch (h.ks) {
+#define SW_CASE(K)                                                                       \
+  case K:                                                                                \
+    hipLaunchKernelGGL((stem_wgrad_kernel<K, true>), dim3(grid), dim3(256), 0, s, a, h, q); \
+    break;
     SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
 #undef SW_CASE
   }

@@ -654,6 +654,29 @@ std::string igemm_tuned_table() {
   return out;
 }
 
+// load a table in igemm_tuned_table()'s format ("key -> BMxBN" lines); replace: drop every
+// entry first.  Data-parallel ranks adopt rank 0's table this way, so every rank runs the
+// same tiles (parallel/comm.py agree_tuned_tiles).  Returns the entries loaded.
+int igemm_tuned_load(const std::string& table, bool replace) {
+  std::lock_guard<std::mutex> lock(g_tune_mu);
+  if (replace) g_tuned.clear();
+  int n = 0;
+  size_t pos = 0;
+  while (pos < table.size()) {
+    size_t end = table.find('\n', pos);
+    if (end == std::string::npos) end = table.size();
+    const std::string line = table.substr(pos, end - pos);
+    pos = end + 1;
+    const size_t arrow = line.rfind(" -> ");
+    if (arrow == std::string::npos) continue;
+    int bm = 0, bn = 0;
+    if (sscanf(line.c_str() + arrow + 4, "%dx%d", &bm, &bn) != 2 || bm <= 0 || bn <= 0) continue;
+    g_tuned[line.substr(0, arrow)] = TunedTile{bm, bn};
+    ++n;
+  }
+  return n;
+}
+
 template <int BM, int BN, int WM, int WN, int VW, bool BKC, bool SPLIT>
 static void launch_rows(const IGemmArgs& a0, int splits, hipStream_t s) {
   IGemmArgs a = a0;
@@ -1153,6 +1176,14 @@ int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix) {
 }
 
 static void wgrad_run_plan(WGradArgs a, int vwa, int vwb, hipStream_t s, int tbm, int tbn);
+
+void igemm_stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s) {
+  const int z = stem_pool_wgrad(a, q, s);
+  const int64_t n = (int64_t)a.Kout * a.Ncols;
+  const int blocks = (int)std::max<int64_t>(1, (n / 4 + 63) / 64);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, a.slab, z, n, a.dw,
+                     a.overwrite);
+}
 
 static const int kWgradCands[][2] = {{64, 128}, {128, 128}, {64, 256}, {128, 256}, {256, 256}};
 

@@ -29,7 +29,7 @@ import torch.nn as nn
 from ..models import initialize_model, InceptionOutputs
 from ..ops import functional as Fn
 from ..optim import build_optimizer
-from ..parallel import ParamArena, GradBucketer, sync_params, World
+from ..parallel import ParamArena, GradBucketer, sync_params, World, agree_tuned_tiles
 
 
 def build_model(name: str, num_classes: int, feature_extract: bool, device: torch.device,
@@ -206,6 +206,7 @@ class TrainStep:
         # (rocprofv3 --marker-trace shows them beside the kernels); MPA_ROCTX=1
         self.markers = markers() if os.environ.get("MPA_ROCTX", "0") == "1" else None
         self.wgrad_stream_ddp = _WGRAD_DDP
+        self._agreed = set()  # batch shapes whose tuned tiles the ranks have agreed on
         # (an early classifier update on a side stream under the rest of the backward was
         # measured slower on one MI355X - ResNet-18 b1024 48.0k vs 48.2k, Inception 6.99k vs
         # 7.09k img/s, profiles/early_head_ab_r3.txt - and removed in round 5)
@@ -274,6 +275,11 @@ class TrainStep:
             loss = self._static_loss
         else:  # eager (also a short last batch of a graph-captured loop)
             loss = self._eager(x, y)
+            if self.world.world_size > 1 and tuple(x.shape) not in self._agreed:
+                # the first step of a batch shape tuned its GEMM tiles per rank: adopt
+                # rank 0's choices everywhere (every rank reaches this at the same step)
+                self._agreed.add(tuple(x.shape))
+                agree_tuned_tiles()
         self._accumulate(loss)
         return loss
 

@@ -781,6 +781,22 @@ class _ConvBNReLUPool(torch.autograd.Function):
         k = K(dy)
         sh, sw, ph, pw = conv.kgeom
         dy = dy.contiguous()
+        if (_STEM_POOL_WGRAD and w.requires_grad and not ctx.needs_input_grad[0]
+                and ctx.bias is None and tuple(ctx.cfg) == (3, 3, 2, 2, 1, 1, False)
+                and k.stem_pool_wgrad_ok(dy, idx, z, x, w.grad, sh, sw, ph, pw)):
+            # image stem: the BN / pool backward's dz pass runs inside the weight
+            # gradient's operand staging, so no full-resolution dz exists
+            sums = k.maxpool_bn_bwd_sums(dy, zsel, mean, rstd, gamma, beta, _sink(gamma, dy),
+                                         _sink(beta, dy))
+            _done(gamma, beta)
+
+            def wgrad():
+                k.stem_pool_wgrad(dy, idx, z, mean, rstd, gamma, beta, sums, x, w.grad,
+                                  sh, sw, ph, pw, _fresh(w))
+                conv.fix_grad(w.grad)
+                _done(w)
+            _run_wgrad(wgrad, dy, idx, z, x, mean, rstd, sums)
+            return None, None, None, None, None, None, None, None
         dz = k.maxpool_bn_bwd(dy, idx, z, mean, rstd, gamma, beta, _sink(gamma, dy),
                               _sink(beta, dy), *ctx.cfg[:6], zsel=zsel)
         _done(gamma, beta)
@@ -796,6 +812,9 @@ class _ConvBNReLUPool(torch.autograd.Function):
             dx = k.conv_dgrad(dz, weight_of(w), ctx.in_hw[0], ctx.in_hw[1], sh, sw, ph, pw,
                               weight_t_of(w))
         return dx, None, None, None, None, None, None, None
+
+
+_STEM_POOL_WGRAD = os.environ.get("MPA_STEM_POOL_WGRAD", "1") == "1"  # (A/B switch)
 
 
 def conv_bn_relu_maxpool(x, conv, bn, pool):

@@ -451,6 +451,41 @@ def maxpool_bn_bwd(dp, idx, z, mean, rstd, gamma, beta, dgamma, dbeta, kh, kw, s
     return dz
 
 
+def maxpool_bn_bwd_sums(dp, zsel, mean, rstd, gamma, beta, dgamma, dbeta):
+    """Pooled-only half of the fused stem backward: [sum g | sum g xhat] with g the pooled
+    gradient masked by bn(zsel) > 0 (zsel = raw z at each argmax); adds dgamma / dbeta."""
+    C = dp.shape[-1]
+    z = _f(zsel).reshape(-1, C)
+    g = _f(dp).reshape(-1, C) * ((z - mean) * (rstd * gamma) + beta > 0)
+    sg, sgx = g.sum(0), (g * ((z - mean) * rstd)).sum(0)
+    if _opt(dgamma) is not None:
+        dgamma.add_(sgx)
+    if _opt(dbeta) is not None:
+        dbeta.add_(sg)
+    return torch.cat([sg, sgx])
+
+
+def stem_pool_wgrad_ok(dp, idx, z, x, dw, sh, sw, ph, pw):
+    return True
+
+
+def stem_pool_wgrad(dp, idx, z, mean, rstd, gamma, beta, sums, x, dw, sh, sw, ph, pw,
+                    overwrite=False):
+    """Weight gradient of conv -> BN -> ReLU -> 3x3/s2/p1 max-pool from the pooled gradient:
+    dz = a g + b + cco z (the BN backward with the pooled ``sums``), rounded to the
+    activation dtype as the two-pass form stores it, then the conv weight gradient."""
+    N, H, W, C = z.shape
+    g = _f(maxpool_bwd(dp, idx, H, W, 3, 3, 2, 2, 1, 1, False)).reshape(-1, C)
+    zf = _f(z).reshape(-1, C)
+    g = g * ((zf - mean) * (rstd * gamma) + beta > 0)
+    M = g.shape[0]
+    a = gamma * rstd
+    cco = -a * rstd * sums[C:] / M
+    b = -a * sums[:C] / M - cco * mean
+    dz = (a * g + b + cco * zf).reshape(z.shape).to(z.dtype)
+    conv_wgrad(dz, x, dw, sh, sw, ph, pw, overwrite)
+
+
 def avgpool_fwd(x, kh, kw, sh, sw, ph, pw, ceil, count_include_pad):
     y = F.avg_pool2d(_nchw(_f(x)), (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil,
                      count_include_pad=count_include_pad)

@@ -167,3 +167,28 @@ def replica_checksum(model: nn.Module) -> bool:
     dist.all_reduce(mn, op=dist.ReduceOp.MIN)
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     return bool(torch.equal(mn.cpu(), mx.cpu()))
+
+
+def agree_tuned_tiles(get=None, load=None, root: int = 0) -> Optional[str]:
+    """Make every rank run the same GEMM tiles: the native autotuner times candidates on
+    each process's first launch of a shape and caches its own winner, so data-parallel
+    ranks could pick different tiles and step at different speeds (the job runs at the
+    slowest).  After a step that tuned new shapes, rank ``root`` broadcasts its table and
+    every rank adopts it (``_C.igemm_tuned_load``).  ``get`` / ``load`` override the native
+    table (tests).  Collective: every rank must call it at the same step.  Returns the
+    agreed table (None on one rank or without the native extension).  The reference's
+    ranks run identical code (``mpi_tools.py:30-37``); this keeps that property for a
+    timing-based kernel choice."""
+    w = get_world()
+    if w.world_size == 1:
+        return None
+    if get is None or load is None:
+        from ..ops import _ext
+        k = _ext.ext() if w.device.type == "cuda" else None
+        if k is None or not hasattr(k, "igemm_tuned_load"):
+            return None
+        get = get or k.igemm_tuned_table
+        load = load or (lambda t: k.igemm_tuned_load(t, True))
+    table = broadcast_object(get() if w.rank == root else None, root)
+    load(table)
+    return table

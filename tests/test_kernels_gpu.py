@@ -1205,6 +1205,53 @@ def test_bn_relu_maxpool_fused(gpu, case):
     assert rel(dg3, dg) < 1e-4 and rel(db3, db) < 1e-4
 
 
+@pytest.mark.parametrize("N,P,Q", [(2, 112, 112), (3, 64, 64), (2, 56, 56), (1, 32, 40)])
+def test_stem_pool_wgrad(gpu, N, P, Q):
+    """Fused stem backward (round 6): the pooled-only sums + the weight gradient that forms
+    dz = a g + b + cco z in its operand staging (conv_stem.hip, POOL form) against the
+    two-pass form (maxpool_bn_bwd writes dz, conv_wgrad reads it: the same bf16 dz, so
+    equal to fp32 summation order) and the fp32 oracle.  Channels with gamma < 0, the
+    K-step tail rows (2Q % 32 != 0) and the last window row / column are covered."""
+    torch.manual_seed(21)
+    Cc = 64
+    x = bf(N, 2 * (P - 1) + 7, Q + 3, 8, dev=gpu, scale=0.5)
+    z = (bf(N, P, Q, Cc, dev=gpu, scale=1.5) + 0.2).to(torch.bfloat16)
+    st = torch.stack([z.float().reshape(-1, Cc).mean(0),
+                      z.float().reshape(-1, Cc).var(0, unbiased=False)])
+    g = torch.rand(Cc, device=gpu) + 0.5
+    g[::3] *= -1.0                                        # gamma < 0 channels
+    b = torch.randn(Cc, device=gpu) * 0.5
+    rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+    zsel = torch.empty(N, P // 2, Q // 2, Cc, device=gpu, dtype=torch.bfloat16)
+    y, idx, mean, rstd = C().bn_relu_maxpool_fwd(z, st, g, b, rm, rv, 0.1, 1e-5, 3, 3, 2, 2, 1,
+                                                 1, False, zsel_out=zsel)
+    dp = bf(*y.shape, dev=gpu)
+    assert C().stem_pool_wgrad_ok(dp, idx, z, x, torch.zeros(64, 7, 4, 8, device=gpu),
+                                  2, 1, 0, 0)
+    # two-pass form
+    dg0, db0 = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    dz = C().maxpool_bn_bwd(dp, idx, z, mean, rstd, g, b, dg0, db0, 3, 3, 2, 2, 1, 1, zsel=zsel)
+    dw0 = torch.zeros(64, 7, 4, 8, device=gpu)
+    C().conv_wgrad(dz, x, dw0, 2, 1, 0, 0)
+    # fused form (accumulating into a non-zero gradient, and overwriting)
+    dg1, db1 = torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu)
+    sums = C().maxpool_bn_bwd_sums(dp, zsel, mean, rstd, g, b, dg1, db1)
+    dw1 = torch.full((64, 7, 4, 8), 0.25, device=gpu)
+    C().stem_pool_wgrad(dp, idx, z, mean, rstd, g, b, sums, x, dw1, 2, 1, 0, 0, False)
+    dw2 = torch.full((64, 7, 4, 8), 7.0, device=gpu)
+    C().stem_pool_wgrad(dp, idx, z, mean, rstd, g, b, sums, x, dw2, 2, 1, 0, 0, True)
+    torch.cuda.synchronize()
+    assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+    assert torch.isfinite(dw2).all()
+    assert rel(dw2, dw0) < 1e-4, rel(dw2, dw0)
+    assert rel(dw1 - 0.25, dw0) < 1e-4
+    # fp32 oracle (its own argmax convention: the native window taps as global indices)
+    gi = _global_idx(idx, P, Q, 3, 3, 2, 2, 1, 1)
+    dwr = torch.zeros(64, 7, 4, 8, device=gpu)
+    ref.stem_pool_wgrad(dp, gi, z, mean, rstd, g, b, sums, x, dwr, 2, 1, 0, 0, True)
+    assert rel(dw2, dwr) < 1e-2, rel(dw2, dwr)
+
+
 @pytest.mark.parametrize("case", POOL_CASES + [(2, 35, 35, 64, 3, 3, 1, 1, 1, 1, False),
                                                (2, 17, 17, 64, 5, 5, 3, 3, 0, 0, False)])
 @pytest.mark.parametrize("cip", [True, False])

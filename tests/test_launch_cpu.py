@@ -32,8 +32,11 @@ def test_bench_spawns_ranks_itself(tmp_path):
                        timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
-    assert len(lines) == 1, r.stdout
-    rec = json.loads(lines[0])
+    # the headline line as soon as it is measured, then the complete record with the extras
+    assert len(lines) == 2, r.stdout
+    head, rec = json.loads(lines[0]), json.loads(lines[1])
+    assert "multi_gpu" not in head
+    assert {k: v for k, v in rec.items() if k in head} == head
     assert rec["n_gpus"] == 2
     assert rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["global_batch"] == 4
@@ -80,12 +83,12 @@ def _bench_cpu(tmp_path, inject, extra=(), timeout=300):
 
 
 def test_bench_keeps_headline_when_a_variant_throws(tmp_path):
-    """Every multi-GPU decision variant raises: the headline line is still printed once,
-    each variant carries its error, and the job exits 0."""
+    """Every multi-GPU decision variant raises: the headline line is printed, the final
+    record carries each variant's error, and the job exits 0."""
     r, lines, _ = _bench_cpu(tmp_path, "variant_raise")
     assert r.returncode == 0, r.stderr[-3000:]
-    assert len(lines) == 1, r.stdout
-    rec = json.loads(lines[0])
+    assert len(lines) == 2, r.stdout
+    rec = json.loads(lines[1])
     assert rec["value"] > 0 and rec["n_gpus"] == 2
     mg = rec["multi_gpu"]
     for k in ("comm_ctas8", "comm_bf16", "wgrad_stream_on"):
@@ -94,13 +97,26 @@ def test_bench_keeps_headline_when_a_variant_throws(tmp_path):
 
 
 def test_bench_prints_headline_when_extras_hang(tmp_path):
-    """The extras after the headline never finish: the extras budget prints the headline
-    record anyway (with extras_error) and every rank exits 0."""
+    """The extras after the headline never finish: the headline line is already out, the
+    extras budget ends every rank with 0 and no final record is printed."""
     r, lines, dt = _bench_cpu(tmp_path, "extras_hang", ["--extras-budget", "5"])
     assert r.returncode == 0, r.stderr[-3000:]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
-    assert rec["value"] > 0 and "timeout" in rec["extras_error"]
+    assert rec["value"] > 0 and "multi_gpu" not in rec
+    assert "timeout: extras exceeded" in r.stderr
+
+
+def test_bench_keeps_headline_when_a_rank_aborts_in_extras(tmp_path):
+    """Rank 1 dies inside the extras (os._exit(134), what a native abort or a GPU fault in
+    a multi-GPU variant does): the headline line is on stdout, and the job exits non-zero
+    with the launcher naming the rank."""
+    r, lines, dt = _bench_cpu(tmp_path, "extras_abort=1", timeout=300)
+    assert r.returncode == 134, (r.returncode, r.stderr[-3000:])
+    assert len(lines) >= 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["n_gpus"] == 2
+    assert "launch: rank 1 exited with code 134" in r.stderr
 
 
 def test_bench_hanging_rank_exits_rank_tagged_nonzero(tmp_path):

@@ -220,3 +220,34 @@ def test_numa_pin_from_sysfs(tmp_path):
         _os.environ.pop("MPA_NUMA_PIN", None)
         _os.sched_setaffinity(0, allowed)
         torch.set_num_threads(nthr)
+
+
+def _tune_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from mpi_pytorch_amd.parallel import init_world, agree_tuned_tiles, shutdown
+    init_world("cpu")
+    # each rank "tuned" its own tiles for the same shapes (what timing noise does)
+    table = {"rows M4096 N64 K576": "%dx128" % (64 * (rank + 1)),
+             "wgrad K64 N576 P4096": "%dx256" % (128 if rank else 64)}
+    state = {"t": "".join("%s -> %s\n" % kv for kv in sorted(table.items()))}
+
+    def load(t):
+        state["t"] = t
+    agreed = agree_tuned_tiles(get=lambda: state["t"], load=load)
+    with open(os.path.join(out_dir, "tiles%d.txt" % rank), "w") as f:
+        f.write(state["t"])
+    assert agreed == state["t"]
+    shutdown()
+
+
+def test_agree_tuned_tiles_two_ranks():
+    """Data-parallel ranks adopt rank 0's autotuned GEMM tiles (parallel/comm.py
+    agree_tuned_tiles, called by TrainStep after the first step of each batch shape), so
+    every rank runs identical kernels."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_tune_worker, args=(2, _free_port(), d), nprocs=2, join=True,
+                           start_method="spawn")
+        t0 = open(os.path.join(d, "tiles0.txt")).read()
+        t1 = open(os.path.join(d, "tiles1.txt")).read()
+    assert t0 == t1 and "64x128" in t0 and "64x256" in t0

@@ -57,3 +57,23 @@ def test_capped_rccl_group_and_bucketer():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=100)
     assert r.returncode == 0 and "CAPPED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_tuned_table_roundtrip():
+    """The autotuner's table dump loads back (igemm_tuned_load): what a data-parallel rank
+    adopts from rank 0 (parallel/comm.py agree_tuned_tiles) is what its lookups then use."""
+    import torch
+    sys.path.insert(0, ROOT)
+    from mpi_pytorch_amd.ops import _ext
+    k = _ext.ext()
+    before = k.igemm_tuned_table()
+    try:
+        t = "rows test-key-A -> 64x128\nwgrad test key B -> 128x256\nbroken line\n"
+        assert k.igemm_tuned_load(t, True) == 2
+        assert k.igemm_tuned_table() == "rows test-key-A -> 64x128\nwgrad test key B -> 128x256\n"
+        assert k.igemm_tuned_load("rows test-key-A -> 256x256\n", False) == 1
+        assert "rows test-key-A -> 256x256" in k.igemm_tuned_table()
+        assert "wgrad test key B -> 128x256" in k.igemm_tuned_table()
+    finally:
+        k.igemm_tuned_load(before, True)
+    assert torch.cuda.is_available()
