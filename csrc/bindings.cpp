@@ -65,18 +65,6 @@ Tensor empty_like_shape(const Tensor& ref, at::IntArrayRef shape, torch::Dtype d
 // out (optional): a bf16 channel-window view [N, P, Q, K] of a wider NHWC buffer (DenseNet's
 // block buffer) the output is written into (row stride out.stride(2)); stats may then be a
 // [2, K] window of a wider statistics table (row stride stats.stride(0))
-// pre (optional, [2, C] fp32): x is the raw output z of a train-mode BN + ReLU whose apply
-// runs here (BN in the operand path): the 3x3/s1 halo kernel applies relu(z * pre[0] +
-// pre[1]) while staging; any other kernel gets the operand materialized first (affine_act)
-static Tensor pre_operand(const Tensor& x, const Tensor& pre) {
-  const int C = x.size(-1);
-  TORCH_CHECK(pre.numel() == 2 * C && pre.scalar_type() == torch::kFloat32 && pre.is_contiguous(),
-              "pre: [2, C] fp32 affine");
-  Tensor y = torch::empty_like(x);
-  mpa::affine_act(bp(x), pre.data_ptr<float>(), 1, (int)(x.numel() / C), C, bpm(y), cur_stream());
-  return y;
-}
-
 Tensor affine_act(Tensor x, Tensor aff, bool relu) {
   CHECK_ACT(x);
   CHECK_CUDA(aff);
@@ -92,8 +80,7 @@ Tensor affine_act(Tensor x, Tensor aff, bool relu) {
 }
 
 static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
-                            int64_t pw, bool relu, Tensor stats, Tensor shift, const Tensor* out,
-                            const Tensor* pre = nullptr) {
+                            int64_t pw, bool relu, Tensor stats, Tensor shift, const Tensor* out) {
   CHECK_ACT(x);
   CHECK_ACT(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: x NHWC, w KRSC");
@@ -170,17 +157,6 @@ static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t
   a.stats_shift = fopt(shift);
   if (a.stats_shift) TORCH_CHECK(shift.numel() == K, "conv_fwd: shift size");
   a.relu = relu ? 1 : 0;
-  Tensor xpre;
-  if (pre && has(*pre)) {
-    a.pre_aff = pre->data_ptr<float>();
-    TORCH_CHECK(pre->numel() == 2 * C && pre->scalar_type() == torch::kFloat32,
-                "conv_fwd: pre must be a [2, C] fp32 affine");
-    if (!mpa::igemm_rows_pre_ok(a, vec_width(C))) {  // materialize the operand instead
-      xpre = pre_operand(x, *pre);
-      a.A = bp(xpre);
-      a.pre_aff = nullptr;
-    }
-  }
   Tensor ws;
   // (split-K's finalize writes dense [M][N] rows: none into a window)
   float* wsp = ldc == K ? alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot)) : nullptr;
@@ -193,9 +169,8 @@ static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t
 }
 
 Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                bool relu, Tensor stats, Tensor shift, c10::optional<Tensor> pre) {
-  return conv_fwd_impl(x, w, bias, sh, sw, ph, pw, relu, stats, shift, nullptr,
-                       pre ? &*pre : nullptr);
+                bool relu, Tensor stats, Tensor shift) {
+  return conv_fwd_impl(x, w, bias, sh, sw, ph, pw, relu, stats, shift, nullptr);
 }
 
 void conv_fwd_into(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
@@ -573,7 +548,7 @@ std::vector<Tensor> bn_bwd_apply(Tensor dy, Tensor x, Tensor y, Tensor mean, Ten
 }
 
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                bool overwrite, c10::optional<Tensor> pre) {
+                bool overwrite) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   CHECK_CUDA(dw);
@@ -594,17 +569,6 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t sh, int64_t sw, int64_t 
   a.overwrite = overwrite ? 1 : 0;
   Tensor slab;
   a.slab = alloc_ws(slab, dy, mpa::igemm_wgrad_ws_floats(a.Kout, a.Ncols, a.Mpix));
-  Tensor xpre;
-  if (pre && has(*pre)) {  // BN in the operand path (see pre_operand)
-    TORCH_CHECK(pre->numel() == 2 * C && pre->scalar_type() == torch::kFloat32,
-                "conv_wgrad: pre must be a [2, C] fp32 affine");
-    a.pre_aff = pre->data_ptr<float>();
-    if (!mpa::igemm_wgrad_pre_ok(a)) {
-      xpre = pre_operand(x, *pre);
-      a.x = bp(xpre);
-      a.pre_aff = nullptr;
-    }
-  }
   mpa::igemm_wgrad(a, vec_width(K), (C % 8 == 0) ? 8 : 1, cur_stream());
 }
 
@@ -1692,6 +1656,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "adopt an igemm_tuned_table() dump (data-parallel ranks take rank 0's)");
   m.def("igemm_set_dma_uni", &mpa::igemm_set_dma_uni, "LDS-DMA uniform-tap fast path on/off");
   m.def("igemm_set_halo", &mpa::igemm_set_halo, "halo-staged direct 3x3/s1 conv on/off");
+  m.def("igemm_set_halo_mi7", &mpa::igemm_set_halo_mi7, "448-pixel halo tiles on/off");
   m.def("igemm_set_halo_strip", &mpa::igemm_set_halo_strip,
         "strip-tiled halo conv: 0 off, 1 images too wide for linear tiles, 2 also layer1");
   m.def("igemm_halo_enabled", &mpa::igemm_halo_enabled);
@@ -1707,16 +1672,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("affine_act", &affine_act, "relu?(x * aff[0] + aff[1]) per channel (aff [2, C])");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("relu"), py::arg("stats"),
-        py::arg("shift"), py::arg("pre") = py::none(),
-        "conv forward; pre: [2, C] affine of a BN + ReLU applied to x while staging");
+        py::arg("shift"), "conv forward (+ BN statistics of its output)");
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("wt") = py::none(),
         py::arg("accum") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("overwrite") = false,
-        py::arg("pre") = py::none(),
-        "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero; "
-        "pre: x is z of a BN + ReLU applied while staging)");
+        "weight gradient into dw (+=; overwrite: dw = ..., the first gradient since zero)");
   m.def("conv_bnred_ok", &conv_bnred_ok);
   m.def("conv_dgrad_bnred_gacc", &conv_dgrad_bnred_gacc);
   m.def("conv_dgrad_res", &conv_dgrad_res);

@@ -116,9 +116,6 @@ struct IGemmArgs {
   // kernels only; dense [M][N] rows)
   const bf16_raw* ep_res;
   const uint8_t* ep_rmask;
-  // BN in the operand path (3x3/s1 halo forward only, see WGradArgs::pre_aff): A is the raw
-  // z of the previous conv, staged as relu(z * pre_aff[c] + pre_aff[aC + c]) in bf16
-  const float* pre_aff;
 };
 constexpr short TAP_SRC2 = 0x2000;
 
@@ -144,10 +141,6 @@ struct WGradArgs {
   int tiles_n, tiles_total;
   int overwrite;  // 1: dw holds nothing to keep (first gradient since zero_grad): store, no
                   // read-modify-write of the fp32 arena
-  // BN in the operand path (3x3/s1 halo wgrad only): x is the raw output z of the previous
-  // conv and the operand is relu(z * pre_aff[c] + pre_aff[C + c]) rounded to bf16 (a
-  // train-mode BN + ReLU whose output is never written); padding stays zero.  null: none
-  const float* pre_aff;
 };
 
 // igemm.hip
@@ -167,10 +160,6 @@ int64_t igemm_bnred_slab_floats(int M, int N, int nphase);
 void igemm_rows_dgrad_bnred(IGemmArgs a, int vw, bool bkc, float* slab, float* sums,
                             hipStream_t s);
 void igemm_wgrad(WGradArgs a, int vwa, int vwb, hipStream_t s);
-// whether a launch with a.pre_aff set (BN in the operand path) runs on a kernel that applies
-// it while staging (else the caller materializes the operand first: affine_act)
-bool igemm_rows_pre_ok(const IGemmArgs& a, int vw);
-bool igemm_wgrad_pre_ok(const WGradArgs& a);
 int64_t igemm_ws_floats(int M, int N, int Ktot);          // split-K partials (0: no split)
 int64_t igemm_wgrad_ws_floats(int Kout, int Ncols, int Mpix);  // wgrad split slab (0: none)
 int igemm_engine();  // 0 register staging, 1 LDS-DMA rows GEMMs (default), 2 LDS-DMA all
@@ -189,6 +178,7 @@ bool conv3_halo_ok(const IGemmArgs& a);
 int conv3_halo(IGemmArgs a, hipStream_t s);  // returns the statistics-slab rows written
 constexpr int HALO_MAX_ROWS = 256;           // its slab rows (one per persistent block)
 void igemm_set_halo(int on);                 // MPA_HALO=0 disables (A/B, bitwise tests)
+void igemm_set_halo_mi7(int on);     // MPA_HALO_MI7 (448-pixel resident-weight tiles)
 void igemm_set_halo_strip(int mode);  // MPA_HALO_STRIP (0 off, 1 wide images, 2 + layer1 3-stage)
 // halo-staged 3x3/s1 weight gradient: partials into a.slab ([Z][Kout][9C]); returns Z
 // halo-staged pixel-pair stem weight gradient (conv_stem.hip): partials into a.slab

@@ -68,43 +68,19 @@ __device__ __forceinline__ bf16x8 frag16(const char* lds_byte) {
   return __builtin_bit_cast(bf16x8, *LDS_PTR(const u32x4, lds_byte));
 }
 
-// Operand BN (PRE): relu(v * sc + sh) of one staged 16-B piece (8 channels), in place, with
-// bn_fwd_train's arithmetic and rounding (fma, max, RNE to bf16), so the operand equals the
-// BN output the forward would have written
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void pre_xform(char* lds, const float (&sc)[8], const float (&sh)[8]) {
-  const u32x4 v = *LDS_PTR(const u32x4, lds);
-  u32x4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    // two channels per packed fma (v_pk_fma_f32: the same IEEE fma per element), RNE to
-    // bf16, then the ReLU as a packed signed 16-bit max with 0 (a bf16 with the sign bit set
-    // is a negative int16: every negative value and -0 become +0, as fmaxf(x, 0) followed by
-    // the rounding gives)
-    f32x2 f = {__uint_as_float(v[i] << 16), __uint_as_float(v[i] & 0xffff0000u)};
-    f = __builtin_elementwise_fma(f, f32x2{sc[2 * i], sc[2 * i + 1]},
-                                  f32x2{sh[2 * i], sh[2 * i + 1]});
-    const s16x2 h = __builtin_bit_cast(s16x2, pack2(f[0], f[1]));
-    r[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, s16x2{0, 0}));
-  }
-  *LDS_PTR(u32x4, lds) = r;
-}
-
 // Epilogue flavours (compile-time, so the fused epilogue below is one straight-line block)
-enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16,
-              // not an epilogue: the A operand is z of a BN + ReLU applied while staging
-              // (IGemmArgs::pre_aff; producer-wave blocks)
-              EP_PRE = 32 };
+enum : int { EP_RELU = 1, EP_BETA = 2, EP_BNRED = 4, EP_STATS = 8, EP_BIAS = 16 };
 
 // Per-tile operands the epilogue reads from memory (accumulate: the old output; fused
 // BN-backward reduction: z, whose ReLU mask is recomputed like bn_fwd_train rounded y, so
 // y is never read), loaded at the start of the tile's second-to-last item so they are in
 // registers long before the epilogue runs.
-struct EpiIn {
-  uint2 a[4][4];
-  uint2 mk[4];  // (accumulate from ep_res) row i's 64 ReLU mask bits of the column tile
+template <int MI = 4>
+struct EpiInT {
+  uint2 a[MI][4];
+  uint2 mk[MI];  // (accumulate from ep_res) row i's 64 ReLU mask bits of the column tile
 };
+typedef EpiInT<4> EpiIn;
 
 // the accumulate operand of element e: the old output, or the residual gradient ep_res
 // (its ReLU mask is applied at the epilogue, see masked_acc: applying it here would make the
@@ -127,19 +103,19 @@ __device__ __forceinline__ uint2 masked_acc(uint2 v, uint2 mk, int jn, int jq) {
   return v;
 }
 
-template <int EPI, int NJ>
-__device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiIn& in, int m0, int n0,
+template <int EPI, int NJ, int MI = 4>
+__device__ __forceinline__ void epi_preload(const IGemmArgs& p, EpiInT<MI>& in, int m0, int n0,
                                             int wave, int lane) {
   if constexpr (!(EPI & (EP_BETA | EP_BNRED))) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jn = 0; jn < 4; ++jn) in.a[i][jn] = make_uint2(0u, 0u);
   } else {
     const int nl = (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = min(m0 + wave * 64 + i * 16 + (lane & 15), p.M - 1);  // rows >= M: unused
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(m0 + wave * 16 * MI + i * 16 + (lane & 15), p.M - 1);  // rows >= M: unused
       const uint32_t orow = (uint32_t)m * p.ldc + n0 + nl;
       if constexpr (!(EPI & EP_BNRED)) in.mk[i] = acc_mask(p, (uint32_t)m * p.ldc + n0);
 #pragma unroll
@@ -165,8 +141,8 @@ __device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0
 // halo_stats_flush.  epi_frag handles fragment (i, jn); the fused form calls it between the
 // next tile's taps (branch-free), the MASKED form after the block's last tile.
 // (BN reduction: cb / cs = mean / rstd, mc / mh = bn_fwd_train's scale / shift)
-template <int EPI, bool FULL>
-__device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, uint2 ia, bool ok,
+template <int EPI, bool FULL, bool ST = true>
+__device__ __forceinline__ uint2 epi_frag(const IGemmArgs& p, const f32x4& acc, uint2 ia, bool ok,
                                          int jn, uint32_t orow, const f32x4& cb, const f32x4& cs,
                                          const f32x4& mc, const f32x4& mh, float (&ssj)[4],
                                          float (&sqj)[4]) {
@@ -197,7 +173,9 @@ __device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, u
     }
   }
   const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
-  if (FULL || ok) *(uint2*)(out + orow + jn * 16) = make_uint2(lo, hi);
+  if constexpr (ST) {
+    if (FULL || ok) *(uint2*)(out + orow + jn * 16) = make_uint2(lo, hi);
+  }
   if constexpr ((EPI & EP_STATS) && !(EPI & EP_BNRED)) {
     // shifted statistics of the bf16-rounded values BN will read
     float rv[4] = {lo_f(lo) - cs[0], hi_f(lo) - cs[1], lo_f(hi) - cs[2], hi_f(hi) - cs[3]};
@@ -208,6 +186,21 @@ __device__ __forceinline__ void epi_frag(const IGemmArgs& p, const f32x4& acc, u
       sqj[r] += rv[r] * rv[r];
     }
   }
+  return make_uint2(lo, hi);
+}
+
+// 16-B epilogue stores (round 6; MI300-class store-issue rule, cdna_hip_programming.md T21):
+// a lane holds 4 channels of column groups jn and jn + 1 of one pixel; v_permlane16_swap
+// trades the even lane row's jn + 1 half for the odd row's jn half, so the even lane
+// (jq = 0, 2) writes channels 16 jn + 4 jq .. + 7 and the odd lane (jq = 1, 3) channels
+// 16 (jn + 1) + 4 (jq - 1) .. + 7: one dwordx4 per lane and fragment pair instead of two
+// scattered dwordx2 (same bytes, half the store instructions).  prow = m * ldc + n0.
+__device__ __forceinline__ void store_pair16(bf16_t* out, uint32_t prow, int jn, int jq,
+                                             uint2 x, uint2 y, bool ok) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+  const uint32_t off = prow + jn * 16 + jq * 4 + ((jq & 1) ? 12 : 0);
+  if (ok) *(uint4*)(out + off) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
 }
 
 // Sum over the 16 lanes of a DPP row (the 16 pixel lanes of one column group), result in
@@ -228,14 +221,14 @@ __device__ __forceinline__ float row16_sum(float v) {
 // Block-level statistics: reduce the per-lane sums of the block's tiles and write slab row
 // blockIdx.x ([2][N]: the block's 64 columns, zeros elsewhere, so every row is complete);
 // block 0 zeroes the final-sum vector the slab reduction accumulates into.
-// PRE: the per-wave sums are already in `red` (per-tile LDS accumulation, see TRED).
-template <bool PRE = false>
+// TRED: the per-wave sums are already in `red` (per-tile LDS accumulation).
+template <bool TRED = false>
 __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)[4][4],
                                                  float (&sq)[4][4], char* red, int n0, int wave,
                                                  int tid) {
   const int lane = tid & 63, nl = (lane >> 4) * 4;
   float* rd = (float*)red;
-  if constexpr (!PRE) {
+  if constexpr (!TRED) {
 #pragma unroll
   for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
@@ -281,12 +274,31 @@ __device__ __forceinline__ void halo_stats_flush(const IGemmArgs& p, float (&ss)
 
 // NJ: 16-column fragment groups per wave (4: 64-wide column tiles; 2: N == 32 - the weight
 // image's upper 32 columns are zero-filled DMAs and never read, no MFMA touches them)
-template <bool WRES, int EPI, bool FULL, int NJ>
-__global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPlan h) {
-  __shared__ __attribute__((aligned(16))) char smem[HB_LDS];
+// MI: 16-pixel row fragments per MFMA wave.  4: 256-pixel linear tiles (576-pixel halo
+// stages, 9 DMAs per producer wave).  7 (round 6, resident weights): 448-pixel tiles of 8
+// whole image rows (ResNet layer1, W = 56): the 10-slot halo stage (640 pixels, 10 DMAs per
+// producer wave) feeds 1.75x the MFMA work of a 576-pixel stage, so the layer's staging -
+// HBM-latency-bound at one item in flight per CU (tools/dma_probe.hip) - is paid per 448
+// output pixels instead of per 256; A fragments stream one row fragment behind its MFMAs.
+template <bool WRES, int EPI, bool FULL, int NJ, int MI = 4>
+__global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void conv3_halo_kernel(IGemmArgs p,
+                                                                          HaloPlan h) {
+  // SELF (MI = 7): 4-wave blocks whose MFMA waves issue their own DMAs.  The 448-pixel
+  // tile's 112 accumulator registers do not fit the 256 registers per wave of an 8-wave
+  // block (92-158 B/lane of scratch, 1.8x slower); alone on its SIMD a wave has 512.
+  constexpr bool SELF = MI != 4;
+  // 16-B epilogue stores (store_pair16) in the 448-pixel flavours; the 256-pixel ones keep
+  // 8-B stores (their pair form spills 1-18 B/lane at 256 registers)
+  constexpr bool WIDE = SELF;
+  constexpr int BM = 64 * MI;                        // tile pixels: 16 MI per MFMA wave
+  constexpr int HIW = MI == 4 ? HB_HIW : 10;         // halo DMAs per producer wave per item
+  constexpr int HBYTES = 16 * HB_NW * HIW * 64;      // halo stage bytes
+  static_assert(MI == 4 || (MI == 7 && WRES), "448-pixel tiles: resident weights only");
+  static_assert(2 * HBYTES + 2 * HB_WBYTES + HB_RED + HB_COLS <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[2 * HBYTES + 2 * HB_WBYTES + HB_RED + HB_COLS];
   char* const hal = smem;
-  char* const wst = smem + 2 * HB_HBYTES;
-  char* const red = smem + 2 * HB_HBYTES + 2 * HB_WBYTES;
+  char* const wst = smem + 2 * HBYTES;
+  char* const red = smem + 2 * HBYTES + 2 * HB_WBYTES;
   float* const cst = (float*)(red + HB_RED);  // [4][64] per-column epilogue operands
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -307,15 +319,15 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   const int nt = (tbeg + loc) % p.tiles_n;
   const int n0 = nt * HB_BN;
   auto tile_of = [&](int tk) { return tbeg + loc + tk * G8; };
-  auto m0_of = [&](int tk) { return (tile_of(tk) / p.tiles_n) * HB_BM; };
+  auto m0_of = [&](int tk) { return (tile_of(tk) / p.tiles_n) * BM; };
 
   // ---- staging: the DMA lanes of lane group `wave` and the instructions of one item
   auto stager = [&](auto body) {
     // halo lanes: tile-independent (slot, column, logical chunk) of each DMA lane
-    uint32_t hsc[HB_HIW];  // slot | (col + 1) << 10 | chunk << 18
+    uint32_t hsc[HIW];  // slot | (col + 1) << 10 | chunk << 18
 #pragma unroll
-    for (int j = 0; j < HB_HIW; ++j) {
-      const uint32_t hp = 16 * (wave * HB_HIW + j) + (lane >> 2);
+    for (int j = 0; j < HIW; ++j) {
+      const uint32_t hp = 16 * (wave * HIW + j) + (lane >> 2);
       const uint32_t s = udiv(hp, h.mag_w2);
       const uint32_t colp = hp - s * W2;
       const uint32_t lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
@@ -333,13 +345,13 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       wv[j] = (n0 + n < p.N) ? (uint32_t)(n0 + n) * p.ldb * 2 + h.btoff[q >> 2] + lc * 16
                              : 0x80000000u;
     }
-    uint32_t hv[HB_HIW];
+    uint32_t hv[HIW];
     auto prep_tile = [&](int tk) {  // DMA source offsets of a tile's halo
       const int m0 = m0_of(tk);
       const int img0 = m0 / HW;
       const int oh0 = (m0 - img0 * HW) / W;
 #pragma unroll
-      for (int j = 0; j < HB_HIW; ++j) {
+      for (int j = 0; j < HIW; ++j) {
         const int s = hsc[j] & 1023, col = (int)((hsc[j] >> 10) & 255) - 1;
         const int v = s + oh0 - 1;                                     // >= -1
         const int d = (int)udiv((uint32_t)(v + H + 1), h.mag_h1) - 1;  // floor(v / (H+1))
@@ -352,42 +364,21 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     };
     // DMA instruction j (halo 0..8, then weights 9..17 unless resident) of item (cc, stage)
     auto dma = [&](int cc, int stage, int j) {
-      if (j < HB_HIW) {
+      if (j < HIW) {
         const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)p.A + cc * 64, h.a_bytes);
-        buf_lds16(ra, hal + stage * HB_HBYTES + (wave * HB_HIW + j) * 1024, hv[j]);
-      } else if (!WRES && j < HB_HIW + HB_WIW) {
+        // (SELF: as asm, invisible to the compiler, which would otherwise wait for these
+        // DMAs before the MFMA waves' next ds_read of the other stage)
+        if constexpr (SELF) buf_lds16_asm(ra, hal + stage * HBYTES + (wave * HIW + j) * 1024, hv[j]);
+        else buf_lds16(ra, hal + stage * HBYTES + (wave * HIW + j) * 1024, hv[j]);
+      } else if (!WRES && j < HIW + HB_WIW) {
         const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.B + cc * 64, h.b_bytes);
-        buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j - HB_HIW) * 1024,
-                  wv[j - HB_HIW]);
-      }
-    };
-    // operand BN (EP_PRE): this lane's 16-B halo pieces hold channels 32 cc + 8 lc .. +7 (lc
-    // fixed per lane); the chunk's scale / shift are loaded with its DMAs (the vmcnt wait
-    // that covers the DMAs covers them) and applied to the landed pieces in place
-    float psc[8], psh[8];
-    const int plc = (lane & 3) ^ (((lane >> 4) & 1) << 1);
-    auto pre_coef = [&](int cc) {
-      if constexpr (EPI & EP_PRE) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          psc[e] = p.pre_aff[cc * 32 + plc * 8 + e];
-          psh[e] = p.pre_aff[aC + cc * 32 + plc * 8 + e];
-        }
-      }
-    };
-    auto xform = [&](int stage) {
-      if constexpr (EPI & EP_PRE) {
-        char* hb = hal + stage * HB_HBYTES + wave * HB_HIW * 1024 + lane * 16;
-#pragma unroll
-        for (int j = 0; j < HB_HIW; ++j)
-          if (hv[j] != 0x80000000u) pre_xform(hb + j * 1024, psc, psh);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        buf_lds16(rb, wst + stage * HB_WBYTES + (wave * HB_WIW + j - HIW) * 1024,
+                  wv[j - HIW]);
       }
     };
     auto issue = [&](int cc, int stage) {
-      pre_coef(cc);
 #pragma unroll
-      for (int j = 0; j < HB_HIW + HB_WIW; ++j) dma(cc, stage, j);
+      for (int j = 0; j < HIW + HB_WIW; ++j) dma(cc, stage, j);
     };
     if (nitems > 0) {
       if constexpr (WRES) {  // whole weight tile (tiles_n == 1, CC <= 2) once per block
@@ -401,7 +392,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
       prep_tile(0);
       issue(0, 0);
     }
-    body(prep_tile, dma, issue, xform);
+    body(prep_tile, dma, issue);
   };
 
   {
@@ -412,17 +403,10 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     // issuing the 18 per item between the MFMAs cost those waves ~10 % (round-2 A/B,
     // docs/KERNELS.md), waiting for them nothing measurable.  Barrier count per wave:
     // nitems (+1 for the statistics flush) on both sides.
-    if (wave_all >= HB_NW) {
-      stager([&](auto& prep_tile, auto&, auto& issue, auto& xform) {
+    if (!SELF && wave_all >= HB_NW) {
+      stager([&](auto& prep_tile, auto&, auto& issue) {
         int cc1 = 0;
         for (int k = 0; k < nitems; ++k) {
-          if constexpr (EPI & EP_PRE) {
-            // item k's halo landed (its weight DMAs, issued after it, may still be in
-            // flight: the transform overlaps their landing); transform before publishing
-            if constexpr (WRES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HB_WIW) : "memory");
-            xform(k & 1);
-          }
           wait_all_barrier();
           if (++cc1 == CC) cc1 = 0;
           if (k + 1 < nitems) {
@@ -457,7 +441,9 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // Holding them for the block's life (as the statistics flavours do) put this flavour at
   // 256 VGPRs with 344-556 B/lane of scratch spills - the round-2/3 "BN link is slower"
   // measurements were those spills.
-  constexpr bool TRED = (EPI & EP_BNRED) != 0;
+  // (SELF, statistics epilogue: the same per-tile reduction - 32 sums held for the block's
+  // life beside 112 accumulators put the 448-pixel flavour at ~600 registers)
+  constexpr bool TRED = (EPI & EP_BNRED) != 0 || (SELF && (EPI & EP_STATS) != 0);
   if constexpr (TRED) ((float2*)red)[tid] = make_float2(0.f, 0.f);  // own wave's slot
   float ss[4][4], sq[4][4];
 #pragma unroll
@@ -471,14 +457,14 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // dw = d - 1: X = 64 * (pixel + dw) + 16 * chunk, chunk position flipped by pixel bit 2
   // (X bit 8).  The pitch is a multiple of 8 pixels, so a row tap dh adds dh*P*64 without
   // touching bits 0..8: a tap's address is xbw[i][dw + 1] + dh*P*64 (+ stage) - 1 VALU.
-  int xbw[4][3];
-  EpiIn ein;
-  f32x4 acc[4][4];
+  int xbw[MI][3];
+  EpiInT<MI> ein;
+  f32x4 acc[MI][4];
 
   // Epilogue of fragment (i, jn) of the tile at m0e (operands from epi_preload).
   auto epi_fr = [&](int i, int jn, int m0e, auto full, float (&es)[4][4], float (&eq)[4][4]) {
     constexpr bool F = decltype(full)::value;
-    const int m = m0e + wave * 64 + i * 16 + l15;
+    const int m = m0e + wave * 16 * MI + i * 16 + l15;
     const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
     // (BN reduction: volatile, read where used - hoisted out of the tile loop, its four
     // vectors would hold 64 VGPRs through every MFMA.  Volatile reads in the other
@@ -499,14 +485,67 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     if constexpr ((EPI & EP_BETA) != 0) {
       if (p.ep_rmask) av = masked_acc(av, ein.mk[i], jn, jq);
     }
-    epi_frag<EPI, F>(p, acc[i][jn], av, m < p.M, jn, orow, colb, cols, mc, mh, es[jn],
-                     eq[jn]);
+    return epi_frag<EPI, F, false>(p, acc[i][jn], av, m < p.M, jn, orow, colb, cols, mc, mh,
+                                   es[jn], eq[jn]);
   };
   // Epilogue of a whole tile (see TRED)
   auto epi_tile = [&](int m0e, auto full) {
     if constexpr (TRED) {
       constexpr bool F = decltype(full)::value;
       float* rd = (float*)red;
+      if constexpr (WIDE) {
+#pragma unroll
+      for (int jp = 0; jp < NJ; jp += 2) {
+        // this column-group pair's mean / rstd / mask affine, read from LDS per tile (an
+        // empty asm memory clobber keeps the compiler from hoisting 64 VGPRs of them out of
+        // the tile loop); its sums live only across its row fragments (32 live sums spilled)
+        asm volatile("" ::: "memory");
+        f32x4 colb[2], cols[2], mc[2], mh[2];
+        float ts[2][4], tq[2][4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = (jp + e) * 16 + jq * 4;
+          colb[e] = *LDS_PTR(const f32x4, cst + c);
+          cols[e] = *LDS_PTR(const f32x4, cst + HB_BN + c);
+          mc[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+          mh[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr ((EPI & EP_BNRED) != 0) {
+            mc[e] = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
+            mh[e] = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { ts[e][r] = 0.f; tq[e][r] = 0.f; }
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int m = m0e + wave * 16 * MI + i * 16 + l15;
+          const uint32_t prow = (uint32_t)m * p.ldc + n0;
+          const uint32_t orow = prow + jq * 4;
+          uint2 v[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            v[e] = epi_frag<EPI, F, false>(p, acc[i][jp + e], ein.a[i][jp + e], m < p.M, jp + e,
+                                           orow, colb[e], cols[e], mc[e], mh[e], ts[e], tq[e]);
+          store_pair16((bf16_t*)p.C, prow, jp, jq, v[0], v[1], F || m < p.M);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ts[e][r] = row16_sum(ts[e][r]);
+            tq[e][r] = row16_sum(tq[e][r]);
+          }
+          if (l15 == 0) {  // columns (jp+e)*16 + 4 jq .. +3 of this wave: [sum, sum2] pairs
+            f32x4* q = (f32x4*)(rd + (wave * 64 + (jp + e) * 16 + jq * 4) * 2);
+            f32x4 q0 = q[0], q1 = q[1];
+            q0[0] += ts[e][0]; q0[1] += tq[e][0]; q0[2] += ts[e][1]; q0[3] += tq[e][1];
+            q1[0] += ts[e][2]; q1[1] += tq[e][2]; q1[2] += ts[e][3]; q1[3] += tq[e][3];
+            q[0] = q0;
+            q[1] = q1;
+          }
+        }
+      }
+      } else {
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) {
         // this column group's mean / rstd / mask affine, read from LDS per tile (an empty
@@ -516,14 +555,17 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
         const int c = jn * 16 + jq * 4;
         const f32x4 colb = *LDS_PTR(const f32x4, cst + c);
         const f32x4 cols = *LDS_PTR(const f32x4, cst + HB_BN + c);
-        const f32x4 mc = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
-        const f32x4 mh = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+        f32x4 mc = {0.f, 0.f, 0.f, 0.f}, mh = {0.f, 0.f, 0.f, 0.f};
+        if constexpr ((EPI & EP_BNRED) != 0) {
+          mc = *LDS_PTR(const f32x4, cst + 2 * HB_BN + c);
+          mh = *LDS_PTR(const f32x4, cst + 3 * HB_BN + c);
+        }
         float ts[4][4], tq[4][4];  // (only row jn is used)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { ts[jn][r] = 0.f; tq[jn][r] = 0.f; }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0e + wave * 64 + i * 16 + l15;
+        for (int i = 0; i < MI; ++i) {
+          const int m = m0e + wave * 16 * MI + i * 16 + l15;
           const uint32_t orow = (uint32_t)m * p.ldc + n0 + jq * 4;
           epi_frag<EPI, F>(p, acc[i][jn], ein.a[i][jn], m < p.M, jn, orow, colb, cols, mc, mh,
                            ts[jn], tq[jn]);
@@ -542,14 +584,34 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
           q[1] = q1;
         }
       }
+      }
     } else {
       // (the per-column operands are re-read from LDS per tile: an empty asm memory clobber
       // keeps the compiler from hoisting 32 VGPRs of them out of the tile loop)
       asm volatile("" ::: "memory");
+      if constexpr (WIDE) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0e + wave * 16 * MI + i * 16 + l15;
 #pragma unroll
-        for (int jn = 0; jn < NJ; ++jn) epi_fr(i, jn, m0e, full, ss, sq);
+        for (int jn = 0; jn < NJ; jn += 2) {
+          const uint2 v0 = epi_fr(i, jn, m0e, full, ss, sq);
+          const uint2 v1 = epi_fr(i, jn + 1, m0e, full, ss, sq);
+          store_pair16((bf16_t*)p.C, (uint32_t)m * p.ldc + n0, jn, jq, v0, v1,
+                       decltype(full)::value || m < p.M);
+        }
+      }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int jn = 0; jn < NJ; ++jn) {
+            const int m = m0e + wave * 16 * MI + i * 16 + l15;
+            const uint2 v = epi_fr(i, jn, m0e, full, ss, sq);
+            if (decltype(full)::value || m < p.M)
+              *(uint2*)((bf16_t*)p.C + (uint32_t)m * p.ldc + n0 + jq * 4 + jn * 16) = v;
+          }
+      }
     }
   };
 
@@ -563,8 +625,39 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // tile's MFMAs was 10-15 % slower.)
   auto mma_chunk = [&](int st, int cc, auto first) {
     constexpr bool FIRST = decltype(first)::value;
-    const int hbase = st * HB_HBYTES;
+    const int hbase = st * HBYTES;
     const char* wimg = (WRES ? wst + cc * HB_WBYTES : wst + st * HB_WBYTES) + boff;
+    if constexpr (MI != 4) {
+      // (MI = 7: row fragment i of tap t + 1 is read into its register right after tap t's
+      // MFMAs on row i consumed it - one A set instead of a double buffer - and a
+      // scheduling fence per row group keeps the compiler from hoisting those reads, which
+      // would need the double buffer's registers: the 8-wave block has 256 per wave)
+      bf16x8 a1[MI], b2[2][4];
+      auto lda = [&](int t, int i) {
+        a1[i] = frag16(hal + hbase + (t / 3 - 1) * W2 * 64 + xbw[i][t % 3]);
+      };
+      auto ldb = [&](int t, int b) {
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) b2[b][jn] = frag16(wimg + t * (HB_BN * 64) + jn * 1024);
+      };
+#pragma unroll
+      for (int i = 0; i < MI; ++i) lda(0, i);
+      ldb(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) ldb(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+          for (int jn = 0; jn < NJ; ++jn)
+            acc[i][jn] = mfma16(b2[t & 1][jn], a1[i],
+                                (FIRST && t == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jn]);
+          if (t + 1 < 9) lda(t + 1, i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      return;
+    }
     bf16x8 a2[2][4], b2[2][4];
     auto ld = [&](int t, int b) {
 #pragma unroll
@@ -590,24 +683,35 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
   // (accumulate: old output; fused BN reduction: z, y) are loaded right after the top wait
   // of the tile's second-to-last item, so they are in flight under its MFMAs (a load issued
   // in front of a wait would be waited for with the DMAs).
-  auto run_tile = [&](int tk) {
+  auto run_tile = [&](int tk, auto hook) {
     const int m0 = m0_of(tk);
     for (int cc = 0; cc < CC; ++cc) {
       const int k = tk * CC + cc;
       const int st = k & 1;
       // this item's DMAs were issued by the producers during the previous item (stage st ^ 1
       // was freed by this barrier); the MFMA waves have no DMA of their own to wait for
+      // (SELF: this wave's own DMAs of item k - issued at item k - 1's top - have landed;
+      // the previous tile's epilogue stores, issued after them, may stay in flight)
+      if constexpr (SELF) {
+        if (cc == 0 && tk > 0) {
+          static_assert(MI * NJ == 28, "vmcnt below counts one store per epilogue fragment");
+          asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+        } else {
+          __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+        }
+      }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
-      if (cc == max(CC - 2, 0)) epi_preload<EPI, NJ>(p, ein, m0, n0, wave, lane);
+      hook(k);  // (SELF: item k + 1's DMAs into the stage this barrier freed)
+      if (cc == max(CC - 2, 0)) epi_preload<EPI, NJ, MI>(p, ein, m0, n0, wave, lane);
       if (cc == 0) {
         const int img0 = m0 / HW;
         const int r0 = m0 - img0 * HW;
         const int oh0 = r0 / W;
         const int mlast = p.M - 1 - img0 * HW;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t n = (uint32_t)min(r0 + wave * 64 + i * 16 + l15, mlast);
+        for (int i = 0; i < MI; ++i) {
+          const uint32_t n = (uint32_t)min(r0 + wave * 16 * MI + i * 16 + l15, mlast);
           const uint32_t di = udiv(n, h.mag_hw);
           const uint32_t rem = n - di * HW;
           const uint32_t oh = udiv(rem, h.mag_w);
@@ -630,7 +734,21 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(IGemmArgs p, HaloPla
     }
   };
 
-  for (int tk = 0; tk < ntiles; ++tk) run_tile(tk);
+  if constexpr (SELF) {
+    stager([&](auto& prep_tile, auto&, auto& issue) {
+      int cc1 = 0;
+      auto next = [&](int k) {
+        if (++cc1 == CC) cc1 = 0;
+        if (k + 1 < nitems) {
+          if (cc1 == 0) prep_tile((k + 1) / CC);
+          issue(cc1, (k + 1) & 1);
+        }
+      };
+      for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, next);
+    });
+  } else {
+    for (int tk = 0; tk < ntiles; ++tk) run_tile(tk, [](int) {});
+  }
   if (ntiles > 0) epi_tile(m0_of(ntiles - 1), std::integral_constant<bool, FULL>{});
   if constexpr (EPI & (EP_STATS | EP_BNRED)) halo_stats_flush<TRED>(p, ss, sq, red, n0, wave, tid);
 }
@@ -1002,18 +1120,13 @@ struct HaloWPlan {
 // of a stage hold ONE 896-pixel halo image of the first chunk (14 DMA instructions per
 // wave instead of 2 x 7).  Waves 2 and 3 then read chunk 0 as well; their partials are
 // duplicates of waves 0 / 1 and are not stored.
-// PROD: 8-wave blocks; waves 4..7 are producers (every tile's index math, LDS-DMAs and - PRE -
-// the operand BN transform of the landed halo), waves 0..3 run only fragment reads and
-// MFMAs.  One barrier per tile on both sides: tile k's barrier publishes stage k & 1 and
-// frees stage (k + 1) & 1.  PRE (BN in the operand path, WGradArgs::pre_aff): each producer
-// lane transforms the halo pieces its own DMAs wrote, after its vmcnt wait and before the
-// barrier; out-of-image pieces (DMA offset past num_records, zeros) stay zero.
+// PROD: 8-wave blocks; waves 4..7 are producers (every tile's index math and LDS-DMAs),
+// waves 0..3 run only fragment reads and MFMAs.  One barrier per tile on both sides: tile
+// k's barrier publishes stage k & 1 and frees stage (k + 1) & 1.
 // KM: 16-row k fragments per partition (4; 2 when Kout == 32 - DenseNet's growth-rate
 // convs - so the partition's zero upper half costs no MFMA and no fragment read)
-template <int W2T, bool ONECH = false, bool STRIP = false, bool PROD = false, bool PRE = false,
-          int KM = 4>
+template <int W2T, bool ONECH = false, bool STRIP = false, bool PROD = false, int KM = 4>
 __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(WGradArgs p, HaloWPlan h) {
-  static_assert(PROD || !PRE, "the operand transform runs on producer waves");
   constexpr int HIW = ONECH ? 2 * HW_HIW : HW_HIW;  // halo DMA instructions per wave (chunk)
   __shared__ __attribute__((aligned(16))) char smem[HW_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1193,41 +1306,12 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
   if constexpr (PROD) {
     if (wave_all >= 4) {
       // ---- producers
-      float psc[2][8], psh[2][8];
-      if constexpr (PRE) {
-        // this lane's 16-B pieces hold channels c0 + 32 ch + 8 lc .. +7 (lc fixed per lane)
-        const int lc = (lane & 3) ^ (((lane >> 5) & 1) << 1);
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int c = c0 + 32 * ch + 8 * lc + e;
-            psc[ch][e] = c < C ? p.pre_aff[c] : 0.f;
-            psh[ch][e] = c < C ? p.pre_aff[C + c] : 0.f;
-          }
-      }
       if (ntiles > 0) {
         prep_dma(z);
         issue(0);
       }
       for (int k = 0; k < ntiles; ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k landed (this wave's part)
-        if constexpr (PRE) {
-          char* hb = smem + (k & 1) * HW_STAGE + HW_DBYTES + lane * 16;
-          if constexpr (ONECH) {
-#pragma unroll
-            for (int jj = 0; jj < HIW; ++jj)
-              if (hv[jj] != 0x80000000u) pre_xform(hb + (wave * HIW + jj) * 1024, psc[0], psh[0]);
-          } else {
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-              for (int jj = 0; jj < HW_HIW; ++jj)
-                if (hv[jj] != 0x80000000u)
-                  pre_xform(hb + ch * HW_HBYTES + (wave * HW_HIW + jj) * 1024, psc[ch], psh[ch]);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
         __builtin_amdgcn_s_barrier();  // publishes stage k & 1, frees stage (k + 1) & 1
         if (k + 1 < ntiles) {
           prep_dma(z + (k + 1) * h.Z);
@@ -1588,8 +1672,6 @@ static bool use_strip(const IGemmArgs& a, bool linear) {
 bool conv3_halo_ok(const IGemmArgs& a) {
   bool linear;
   if (!halo_ok_impl(a, linear)) return false;
-  if (a.pre_aff)  // operand BN: linear tiles, statistics epilogue, 64-wide column tiles
-    return linear && !use_strip(a, linear) && halo_epi(a) == EP_STATS && a.N % HB_BN == 0;
   return linear || use_strip(a, linear);
 }
 
@@ -1600,7 +1682,14 @@ bool conv3_halo_ok(const IGemmArgs& a) {
 
 template <int EPI, int NJ>
 static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
-                          hipStream_t s) {
+                          hipStream_t s, bool mi7 = false) {
+  if constexpr (NJ == 4 && (EPI == 0 || EPI == EP_STATS)) {
+    if (mi7) {  // (halo_mi7_ok: resident weights, whole 448-pixel tiles)
+      hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, 4, 7>), dim3(grid), dim3(256), 0, s,
+                         a, h);
+      return;
+    }
+  }
   const bool full = a.M % HB_BM == 0;  // no tile ends past M: branch-free epilogue everywhere
   if (wres && full)
     hipLaunchKernelGGL((conv3_halo_kernel<true, EPI, true, NJ>), dim3(grid), dim3(512), 0, s, a, h);
@@ -1614,8 +1703,30 @@ static void launch_halo_k(bool wres, int grid, const IGemmArgs& a, const HaloPla
 
 template <int EPI>
 static void launch_halo(bool wres, int grid, const IGemmArgs& a, const HaloPlan& h,
-                        hipStream_t s) {
-  launch_halo_k<EPI, 4>(wres, grid, a, h, s);
+                        hipStream_t s, bool mi7 = false) {
+  launch_halo_k<EPI, 4>(wres, grid, a, h, s, mi7);
+}
+
+// MPA_HALO_MI7=0: keep the 256-pixel tiles for the resident-weight layers (A/B)
+static int g_halo_mi7 = [] {
+  const char* e = getenv("MPA_HALO_MI7");
+  return e ? atoi(e) : 1;
+}();
+void igemm_set_halo_mi7(int on) { g_halo_mi7 = on; }
+
+// 448-pixel tiles (MI = 7): same-conv tap set, one resident 64-wide weight tile, tiles of
+// whole image rows that never cross an image (HW % 448 == 0, 448 % W == 0) and whose
+// (448 / W + 2)-slot halo fits the 640-pixel stage
+static bool halo_mi7_ok(const IGemmArgs& a, int epi, bool wres) {
+  if (!g_halo_mi7 || !wres || a.N != HB_BN) return false;
+  // (the accumulate / BN-link dgrad flavours spill 92-102 B/lane at 448 pixels: not yet)
+  if (epi != 0 && epi != EP_STATS) return false;
+  int ch, cw;
+  if (!tap_shift(a, ch, cw) || ch != 0 || cw != 0) return false;
+  const int64_t HW = (int64_t)a.aH * a.aW;
+  constexpr int BM7 = 448;
+  if (HW % BM7 != 0 || BM7 % a.aW != 0 || a.M % BM7 != 0) return false;
+  return (BM7 / a.aW + 2) * halo_pitch(a.aW) <= 640;
 }
 
 // N == 32 (plain and statistics epilogues only; producer-wave blocks)
@@ -1645,7 +1756,9 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   h.mag_h1 = magic(a.aH + 1);
   h.mag_hw = magic(a.aH * a.aW);
   h.cc = a.aC / 32;
-  h.tiles_m = (a.M + HB_BM - 1) / HB_BM;
+  const bool wres = g_halo_wres && (a.N + HB_BN - 1) / HB_BN == 1 && h.cc <= 2;
+  const bool mi7 = halo_mi7_ok(a, halo_epi(a), wres);
+  h.tiles_m = mi7 ? a.M / 448 : (a.M + HB_BM - 1) / HB_BM;
   a.tiles_n = (a.N + HB_BN - 1) / HB_BN;
   h.tiles_total = h.tiles_m * a.tiles_n;
   a.tiles_total = h.tiles_total;
@@ -1655,20 +1768,15 @@ int conv3_halo(IGemmArgs a, hipStream_t s) {
   int g8 = std::min(std::min(active_cus(), HALO_MAX_ROWS) / 8, (h.tiles_total + 7) / 8);
   g8 = std::max(a.tiles_n, g8 / a.tiles_n * a.tiles_n);
   const int grid = 8 * g8;
-  const bool wres = g_halo_wres && a.tiles_n == 1 && h.cc <= 2;
-  if (a.pre_aff) {  // (conv3_halo_ok: statistics epilogue, N % 64 == 0)
-    launch_halo_k<EP_STATS | EP_PRE, 4>(wres, grid, a, h, s);
-    return grid;
-  }
   if (a.N == 32) {
     if (halo_epi(a) == EP_STATS) launch_halo32<EP_STATS>(wres, grid, a, h, s);
     else launch_halo32<0>(wres, grid, a, h, s);
     return grid;
   }
   switch (halo_epi(a)) {
-    case 0: launch_halo<0>(wres, grid, a, h, s); break;
+    case 0: launch_halo<0>(wres, grid, a, h, s, mi7); break;
     case EP_BETA: launch_halo<EP_BETA>(wres, grid, a, h, s); break;
-    case EP_STATS: launch_halo<EP_STATS>(wres, grid, a, h, s); break;
+    case EP_STATS: launch_halo<EP_STATS>(wres, grid, a, h, s, mi7); break;
     case EP_BIAS | EP_RELU: launch_halo<EP_BIAS | EP_RELU>(wres, grid, a, h, s); break;
     case EP_BIAS | EP_STATS: launch_halo<EP_BIAS | EP_STATS>(wres, grid, a, h, s); break;
     default: launch_halo<EP_BNRED>(wres, grid, a, h, s); break;
@@ -1760,7 +1868,7 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
 // Producer-wave weight-gradient kernels (PROD) for the linear tiles: the 13 ResNet-18 halo
 // weight gradients take 3.14 ms instead of 3.63 ms per b1024 step, +2.4 % single-stream
 // (round-5 A/B, profiles/wprod_pre_ab_r5.txt).  MPA_HALO_WPROD=0: the 4-wave form (the
-// MFMA waves issue the DMAs).  The operand-BN form (a.pre_aff) always runs on them.
+// MFMA waves issue the DMAs).
 static bool g_wprod = [] {
   const char* e = getenv("MPA_HALO_WPROD");
   return !(e && e[0] == '0');
@@ -1771,18 +1879,13 @@ void igemm_set_halo_wprod(int on) { g_wprod = on != 0; }
 // tap addresses spill past their 256 registers)
 template <int W2T, bool ONECH = false, bool STRIP = false>
 static void launch_halo_wgrad(const WGradArgs& a, const HaloWPlan& h, dim3 grid, hipStream_t s) {
-  if (a.pre_aff) {
-    hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, STRIP, true, true>), grid, dim3(512),
-                       0, s, a, h);
-    return;
-  }
   if constexpr (!STRIP) {
     if (g_wprod) {
       if (a.Kout == 32)
-        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false, 2>), grid,
+        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, 2>), grid,
                            dim3(512), 0, s, a, h);
       else
-        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true, false>), grid,
+        hipLaunchKernelGGL((conv3_halo_wgrad_kernel<0, ONECH, false, true>), grid,
                            dim3(512), 0, s, a, h);
       return;
     }

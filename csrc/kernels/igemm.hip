@@ -949,14 +949,6 @@ void igemm_rows(IGemmArgs a, int vw, float* ws, float* slab, hipStream_t s) {
   run_rows(a, true, vw, ws, slab, s);
 }
 
-bool igemm_rows_pre_ok(const IGemmArgs& a, int vw) {
-  return use_dma(vw) && conv3_halo_ok(a);
-}
-
-bool igemm_wgrad_pre_ok(const WGradArgs& a) {
-  return igemm_engine() >= 1 && conv3_halo_wgrad_ok(a);
-}
-
 void igemm_rows_dgrad(IGemmArgs a, int vw, float* ws, hipStream_t s, bool bkc) {
   a.stats = nullptr;
   a.nphase = 0;

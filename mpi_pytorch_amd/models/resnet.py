@@ -26,17 +26,6 @@ _LINK = os.environ.get("MPA_BN_LINK", "1") == "1"
 _JOIN = os.environ.get("MPA_GRAD_JOIN", "1") == "1"
 # MPA_DS_DEFER=0: the downsample BN writes its output (instead of bn2 applying it on read)
 _DS_DEFER = os.environ.get("MPA_DS_DEFER", "1") == "1"
-# BN in the operand path (Fn.BNLink.want_pre): bn1 + ReLU applied by conv2's forward and
-# weight-gradient kernels while they stage conv1's raw output, so y1 is never written.
-# Opt-in (MPA_BN_PRE=1): bitwise equal to the written y1 (tests/test_pre_bn_gpu.py) but
-# measured SLOWER - 47.4k vs 49.2k img/s single-stream, b1024 (profiles/wprod_pre_ab_r5.txt):
-# the producer waves' transform of each landed halo sits on the critical path between the
-# DMAs landing and the barrier that publishes them (+50-95 us per forward, +60 % per weight
-# gradient) and costs more than the 8 bn1 apply passes (645 us) it removes.
-_PRE = os.environ.get("MPA_BN_PRE", "0") == "1"
-_PRE_CPU = False  # (tests: the same op sequence on the CPU reference ops)
-
-
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -54,10 +43,7 @@ class BasicBlock(nn.Module):
         # conv1's output feeds only conv2: conv2's dgrad performs bn1's backward reduction
         link = None
         if self.bn1.training and _LINK:
-            c2 = self.conv2
-            link = Fn.BNLink(want_pre=_PRE and (x.is_cuda or _PRE_CPU) and c2.kgeom == (1, 1, 1, 1)
-                             and tuple(c2.weight.shape[1:3]) == (3, 3)
-                             and c2.weight.shape[3] % 32 == 0 and c2.weight.shape[0] % 64 == 0)
+            link = Fn.BNLink()
         # x's gradient = conv1's dgrad + the shortcut's: summed inside the second dgrad
         join = Fn.GradJoin() if (self.bn1.training and _JOIN and x.requires_grad) else None
         out = Fn.conv_bn_act(x, self.conv1, self.bn1, relu=True, link_out=link, join_x=join)

@@ -217,17 +217,12 @@ class BNLink:
     mask and sums (g, g * x_hat) while the gradient is still in registers - and the
     producer's backward runs only the BN apply pass (no reduce pass, no re-read of dy/y).
 
-    ``want_pre`` (set by the block when the consumer is a 3x3/s1 conv): BN in the operand
-    path.  The producer then runs only the statistics half of its BN (``bn_stats_affine``)
-    and returns z standing for relu(bn(z)); ``pre`` is the [2, C] scale | shift the
-    consumer's forward and weight-gradient kernels apply while staging z (padding stays
-    zero), so the BN output is never written and never read."""
+    (Round 5 also built the producer's BN + ReLU into the consumer's operand staging; it
+    measured 3.9 % slower - profiles/wprod_pre_ab_r5.txt - and was removed in round 6.)"""
 
-    __slots__ = ("z", "y", "mean", "rstd", "gamma", "beta", "sums", "gacc", "want_pre", "pre")
+    __slots__ = ("z", "y", "mean", "rstd", "gamma", "beta", "sums", "gacc")
 
-    def __init__(self, want_pre: bool = False):
-        self.want_pre = bool(want_pre)
-        self.pre = None
+    def __init__(self):
         self.z = self.y = self.mean = self.rstd = self.gamma = self.beta = self.sums = None
         # gacc: a DenseNet block gradient.  The consumer's (1x1) dgrad then ADDS gamma*rstd *
         # g into its first Ci channels instead of returning dx, and the producer side
@@ -439,24 +434,15 @@ class _ConvBNAct(torch.autograd.Function):
         sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
-        # x may be z of the previous op's BN + ReLU, applied here while staging (BNLink.pre)
-        pre = link_in.pre if link_in is not None else None
         # BN statistics come out of the conv epilogue, shifted by the running mean
         z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
-                       _empty(x) if _NO_SHIFT else bn.running_mean, pre=pre)
+                       _empty(x) if _NO_SHIFT else bn.running_mean)
         # relu(bn(z) + residual): the backward's ReLU mask as one bit per element, written by
         # the forward, so neither backward pass reads y (two activation-sized reads less)
         ymask = None
         if relu and residual is not None:
             ymask = torch.empty(z.numel() // 8, device=z.device, dtype=torch.uint8)
-        pre_out = (link_out is not None and link_out.want_pre and relu and residual is None
-                   and defer is None and out is None and gamma is not None and beta is not None)
-        if pre_out:  # statistics only; the consumer's kernels apply relu(bn(z)) (BNLink.pre)
-            mean, rstd, link_out.pre = k.bn_stats_affine(z, stats, gamma, beta, bn.running_mean,
-                                                         bn.running_var, bn.momentum_value(),
-                                                         bn.eps, bn.num_batches_tracked)
-            y = z
-        elif defer is not None:  # statistics only; the consumer applies this BN (BNDefer)
+        if defer is not None:  # statistics only; the consumer applies this BN (BNDefer)
             mean, rstd, defer.aff = k.bn_stats_affine(z, stats, gamma, beta, bn.running_mean,
                                                       bn.running_var, bn.momentum_value(),
                                                       bn.eps, bn.num_batches_tracked)
@@ -476,7 +462,6 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.bias = b
         ctx.params = (w, gamma, beta)
         ctx.in_hw = (x.shape[1], x.shape[2])
-        ctx.pre = pre  # (the weight gradient applies it to x as well)
         # (relu(bn(z)) without a residual recomputes its mask from z: y is not kept)
         keep_y = relu and ymask is None and not (residual is None and beta is not None)
         ctx.save_for_backward(x, z, y if keep_y else None, mean, rstd, ymask)
@@ -492,7 +477,7 @@ class _ConvBNAct(torch.autograd.Function):
             # (as the forward rounded y) when the BN is affine and never reads y (the
             # implicit-GEMM fallback does)
             zmask = relu and residual is None and gamma is not None and beta is not None
-            link_out.y = y if (relu and not pre_out) else None
+            link_out.y = y if relu else None
             link_out.gamma, link_out.beta = (gamma, beta) if zmask else (None, None)
             link_out.sums = None
         return y
@@ -544,10 +529,8 @@ class _ConvBNAct(torch.autograd.Function):
             _done(gamma, beta)
         sh, sw, ph, pw = conv.kgeom
         if w.requires_grad:
-            pre = ctx.pre
-
             def wgrad():
-                k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w), pre=pre)
+                k.conv_wgrad(dz, x, w.grad, sh, sw, ph, pw, overwrite=_fresh(w))
                 conv.fix_grad(w.grad)
                 _done(w)
             _run_wgrad(wgrad, dz, x)

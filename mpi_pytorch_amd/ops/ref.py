@@ -55,9 +55,7 @@ def affine_act(x, aff, relu):
     return y.to(x.dtype)
 
 
-def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None, pre=None):
-    if _opt(pre) is not None:  # x is z of a BN + ReLU applied here (operand-path BN)
-        x = affine_act(x, pre, True)
+def conv_fwd(x, w, bias, sh, sw, ph, pw, relu, stats, shift=None):
     y = F.conv2d(_nchw(_f(x)), _f(w).permute(0, 3, 1, 2), None if _opt(bias) is None else _f(bias),
                  (sh, sw), (ph, pw))
     y = _nhwc(y)
@@ -120,9 +118,7 @@ def conv_dgrad_pair(dy, w, wt, H, W, sh, sw, ph, pw, dy2, w2, wt2, ph2, pw2, acc
     return tot.to(dy.dtype)
 
 
-def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False, pre=None):
-    if _opt(pre) is not None:
-        x = affine_act(x, pre, True)
+def conv_wgrad(dy, x, dw, sh, sw, ph, pw, overwrite=False):
     K, R, S, C = dw.shape
     gw = torch.ops.aten.convolution_backward(
         _nchw(_f(dy)).contiguous(), _nchw(_f(x)).contiguous(),

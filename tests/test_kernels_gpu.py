@@ -1603,3 +1603,35 @@ def test_wgrad_overwrite(gpu, kind):
     assert rel(acc - junk, zero) < 1e-3
 
 
+
+
+@pytest.mark.parametrize("N", [4, 2])
+def test_halo_mi7_tiles_bitwise(gpu, N):
+    """448-pixel halo tiles (8 whole 56-wide rows per tile, MI = 7, round 6) vs the 256-pixel
+    tiles on ResNet layer1's shape: every output accumulates its taps and chunks in the same
+    order, so forward, dgrad and accumulating dgrad are bitwise equal; the BN statistics
+    (different summation order) agree to fp32 rounding; and the fp32 oracle."""
+    torch.manual_seed(17)
+    H, Ci, Co = 56, 64, 64
+    x = bf(N, H, H, Ci, dev=gpu)
+    w = bf(Co, 3, 3, Ci, dev=gpu, scale=0.05)
+    dy = bf(N, H, H, Co, dev=gpu)
+    e = torch.empty(0, device=gpu)
+    shift = torch.randn(Co, device=gpu) * 0.1
+    out = {}
+    try:
+        for on in (0, 1):
+            C().igemm_set_halo_mi7(on)
+            st = torch.empty(2, Co, device=gpu)
+            y = C().conv_fwd(x, w, e, 1, 1, 1, 1, False, st, shift)
+            dx = C().conv_dgrad(dy, w, H, H, 1, 1, 1, 1)
+            acc = x.clone()
+            dxa = C().conv_dgrad(dy, w, H, H, 1, 1, 1, 1, None, acc)
+            out[on] = (y, st, dx, dxa)
+    finally:
+        C().igemm_set_halo_mi7(1)
+    (y0, s0, d0, a0), (y1, s1, d1, a1) = out[0], out[1]
+    assert torch.equal(y0, y1) and torch.equal(d0, d1) and torch.equal(a0, a1)
+    assert rel(s1, s0) < 1e-5
+    assert rel(y1, ref.conv_fwd(x, w, e, 1, 1, 1, 1, False, None, None)) < 1e-2
+    assert rel(d1, ref.conv_dgrad(dy, w, H, H, 1, 1, 1, 1)) < 1e-2

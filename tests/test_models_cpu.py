@@ -470,35 +470,6 @@ def test_resnet_deferred_downsample_bn_equals_materialized(monkeypatch):
     assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
 
 
-def test_resnet_operand_path_bn_equals_materialized(monkeypatch):
-    """bn1 + ReLU applied by conv2's forward and weight gradient to conv1's raw output
-    (Fn.BNLink.want_pre: statistics half only in conv1's op, y1 never written) == the
-    materialized y1: logits, gradients, running statistics (fp32, CPU reference ops)."""
-    from mpi_pytorch_amd.models import resnet as rn
-    torch.manual_seed(0)
-    model, _o, _s, _ = build_training("resnet18", 10, torch.device("cpu"), World(), 1e-3)
-    a = model._mpa_arena
-    x = torch.randn(2, 64, 64, 3)
-    y = torch.randint(0, 10, (2,))
-    sd = {k: v.clone() for k, v in model.state_dict().items()}
-    res = []
-    monkeypatch.setattr(rn, "_PRE_CPU", True)
-    for pre in (True, False):
-        monkeypatch.setattr(rn, "_PRE", pre)
-        model.load_state_dict(sd)
-        model.train()
-        a.zero_grad()
-        out = model(x)
-        loss_fn(out, y).backward()
-        res.append((out.detach(), a.grad.clone(),
-                    [v.clone() for k, v in model.state_dict().items()
-                     if "running" in k or "num_batches" in k]))
-    (o1, g1, r1), (o2, g2, r2) = res
-    assert torch.allclose(o1, o2, atol=1e-5)
-    assert all(torch.allclose(u.float(), v.float(), atol=1e-5) for u, v in zip(r1, r2))
-    assert float((g1 - g2).abs().max()) < 1e-5 * float(g2.abs().max())
-
-
 def test_resnet_dgrad_pair_equals_two_dgrads(monkeypatch):
     """Each residual stage's conv1 (3x3/s2) and 1x1/s2 shortcut dgrads merged into one
     launch (Fn._dgrad_pair -> conv_dgrad_pair; 3 per ResNet-18 step) == the two separate
