@@ -79,8 +79,16 @@ Tensor affine_act(Tensor x, Tensor aff, bool relu) {
   return y;
 }
 
+// pooled outputs of the fused stem forward (conv_stem_pool_fwd): when set, conv_fwd_impl
+// returns an undefined tensor unless the pixel-pair stem kernel takes the launch
+struct StemPoolOut {
+  Tensor zsel, idx, bz, bidx;
+  const float* gamma;
+};
+
 static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
-                            int64_t pw, bool relu, Tensor stats, Tensor shift, const Tensor* out) {
+                            int64_t pw, bool relu, Tensor stats, Tensor shift, const Tensor* out,
+                            StemPoolOut* spo = nullptr, mpa::IGemmArgs* args_out = nullptr) {
   CHECK_ACT(x);
   CHECK_ACT(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: x NHWC, w KRSC");
@@ -157,6 +165,21 @@ static Tensor conv_fwd_impl(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t
   a.stats_shift = fopt(shift);
   if (a.stats_shift) TORCH_CHECK(shift.numel() == K, "conv_fwd: shift size");
   a.relu = relu ? 1 : 0;
+  if (spo) {
+    const int PP = P / 2, PQ = Q / 2, P8 = std::max(1, P / 8);
+    spo->zsel = empty_like_shape(x, {N, PP, PQ, K}, torch::kBFloat16);
+    spo->idx = empty_like_shape(x, {N, PP, PQ, K}, torch::kUInt8);
+    spo->bz = empty_like_shape(x, {N, P8, PQ, K}, torch::kBFloat16);
+    spo->bidx = empty_like_shape(x, {N, P8, PQ, K}, torch::kUInt8);
+    a.sp_zsel = bpm(spo->zsel);
+    a.sp_idx = spo->idx.data_ptr<uint8_t>();
+    a.sp_bz = bpm(spo->bz);
+    a.sp_bidx = spo->bidx.data_ptr<uint8_t>();
+    a.sp_gamma = spo->gamma;
+    if (!(vec_width(C) == 8 && mpa::igemm_engine() >= 1 && a.stats && mpa::conv_stem_ok(a)))
+      return Tensor();
+  }
+  if (args_out) *args_out = a;
   Tensor ws;
   // (split-K's finalize writes dense [M][N] rows: none into a window)
   float* wsp = ldc == K ? alloc_ws(ws, x, mpa::igemm_ws_floats(a.M, a.N, a.Ktot)) : nullptr;
@@ -176,6 +199,37 @@ Tensor conv_fwd(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t
 void conv_fwd_into(Tensor x, Tensor w, Tensor bias, int64_t sh, int64_t sw, int64_t ph,
                    int64_t pw, bool relu, Tensor stats, Tensor shift, Tensor out) {
   conv_fwd_impl(x, w, bias, sh, sw, ph, pw, relu, stats, shift, &out);
+}
+
+// The ResNet / DenseNet stem forward, conv -> BN(train) -> ReLU -> 3x3/s2/p1 max-pool, with
+// the pool taken inside the conv kernel (conv_stem.hip, PF) and the BN + ReLU applied to the
+// pooled extremes only (stem_pool_apply).  Returns [y, idx, mean, rstd, z, zsel] like
+// bn_relu_maxpool_fwd (+ conv_fwd's z), or None when the stem kernel cannot take the launch.
+c10::optional<std::vector<Tensor>> conv_stem_pool_fwd(Tensor x, Tensor w, int64_t sh, int64_t sw,
+                                                      int64_t ph, int64_t pw, Tensor stats,
+                                                      Tensor shift, Tensor gamma, Tensor beta,
+                                                      Tensor rmean, Tensor rvar,
+                                                      double momentum, double eps,
+                                                      c10::optional<Tensor> counter) {
+  CHECK_CUDA(gamma);
+  CHECK_F32(gamma);
+  TORCH_CHECK(gamma.numel() == w.size(0) && beta.numel() == w.size(0), "conv_stem_pool_fwd: BN size");
+  StemPoolOut spo;
+  spo.gamma = gamma.data_ptr<float>();
+  mpa::IGemmArgs a{};
+  Tensor z = conv_fwd_impl(x, w, Tensor(), sh, sw, ph, pw, false, stats, shift, nullptr, &spo, &a);
+  if (!z.defined()) return c10::nullopt;
+  const int K = w.size(0);
+  Tensor y = torch::empty_like(spo.zsel);
+  Tensor mean = torch::empty({K}, gamma.options());
+  Tensor rstd = torch::empty({K}, gamma.options());
+  mpa::stem_pool_apply(a, stats.data_ptr<float>(), gamma.data_ptr<float>(), fopt(beta),
+                       fopt_mut(rmean), fopt_mut(rvar), (float)momentum, (float)eps, bpm(y),
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                       (counter && counter->defined() && counter->numel() == 1)
+                           ? counter->data_ptr<int64_t>() : nullptr,
+                       cur_stream());
+  return std::vector<Tensor>{y, spo.idx, mean, rstd, z, spo.zsel};
 }
 
 // wt (optional): the transposed weight [C][R*S][K] (arena shadow_t) - the dgrad GEMM then
@@ -1727,6 +1781,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pw"), py::arg("ceil"), py::arg("counter") = py::none(),
         py::arg("zsel_out") = py::none());
   m.def("maxpool_bn_bwd_sums", &maxpool_bn_bwd_sums);
+  m.def("conv_stem_pool_fwd", &conv_stem_pool_fwd, py::arg("x"), py::arg("w"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("stats"),
+        py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("momentum"), py::arg("eps"), py::arg("counter") = py::none());
   m.def("stem_pool_wgrad_ok", &stem_pool_wgrad_ok);
   m.def("stem_pool_wgrad", &stem_pool_wgrad);
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dp"), py::arg("idx"), py::arg("z"),

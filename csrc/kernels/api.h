@@ -116,6 +116,17 @@ struct IGemmArgs {
   // kernels only; dense [M][N] rows)
   const bf16_raw* ep_res;
   const uint8_t* ep_rmask;
+  // the stem's 3x3/s2/p1 max-pool fused into the pixel-pair stem forward (conv_stem.hip;
+  // sp_zsel set): per pooled window and channel the extreme z of the window rows inside the
+  // kernel's 8-row item - the max where gamma >= 0, the min where gamma < 0, which is where
+  // relu(bn(z)) is largest - and its tap 3 i + k ([N][P/2][Q/2][N] each).  An item's first
+  // pooled row lacks its top window row: the previous item leaves that row's horizontal
+  // extreme in sp_bz / sp_bidx ([N][P/8][Q/2][N]) and stem_pool_apply merges the two.
+  bf16_raw* sp_zsel;
+  uint8_t* sp_idx;
+  bf16_raw* sp_bz;
+  uint8_t* sp_bidx;
+  const float* sp_gamma;
 };
 constexpr short TAP_SRC2 = 0x2000;
 
@@ -218,6 +229,13 @@ int active_cus();
 // 64 output channels); run_rows takes it when conv_stem_ok.  Returns the slab rows written.
 bool conv_stem_ok(const IGemmArgs& a);
 int conv_stem(IGemmArgs a, hipStream_t s);
+// the pooled half of the fused stem forward: merges each item's first pooled row with the
+// previous item's bottom row (a.sp_bz), then y = relu(bn(zsel)) with the batch statistics
+// `stats` ([2][C] mean, biased var); mean / rstd out, running stats (momentum) and the
+// batch counter updated like bn_relu_maxpool_fwd
+void stem_pool_apply(const IGemmArgs& a, const float* stats, const float* gamma,
+                     const float* beta, float* rmean, float* rvar, float momentum, float eps,
+                     bf16_raw* y, float* mean, float* rstd, int64_t* counter, hipStream_t s);
 void igemm_set_stem(int on);  // MPA_STEM_DIRECT=0 disables (A/B, tests)
 
 // bn.hip  (x/y/res/dy/dx: [M][C] bf16 rows; per-channel fp32 vectors)

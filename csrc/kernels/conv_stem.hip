@@ -44,8 +44,101 @@ struct StemPlan {
   int qsub;         // 16-pixel subtiles per output row: ceil(Q / 16)
 };
 
-// STEM_NW waves per block, STEM_ROWS output rows per item, STEM_OCC waves per SIMD
-template <int STEM_NW, int STEM_ROWS, int STEM_OCC>
+constexpr int SP_MAXQ = 112;  // PF: output width the z image holds
+
+// PF pooling of one item (output rows p0 .. p0 + 7 of image img) from its LDS z image:
+// thread = (pooled pixel, 8-channel chunk).  Window (pp, qq) covers output rows 2 pp - 1 ..
+// 2 pp + 1 and columns 2 qq - 1 .. 2 qq + 1 (tap 3 i + k); taps are scanned in order with a
+// strict comparison, so the first extreme wins, as in bn_relu_maxpool_fwd_kernel.  gamma < 0
+// channels take the minimum (relu(bn(z)) decreases in z there).
+__device__ __forceinline__ void stem_pool_item(const IGemmArgs& p, const StemPlan& h,
+                                               const char* zimg, int img, int p0) {
+  const int Q = p.oW, PQ = Q >> 1, PP = p.oH >> 1;
+  const int pp0 = p0 >> 1, item = p0 >> 3, nthr = blockDim.x;
+  auto chunk = [&](int r, int q, int c8) -> uint4 {
+    const u32x4 v = *LDS_PTR(const u32x4, zimg + (r * SP_MAXQ + q) * 128 + ((c8 ^ (q & 7)) << 4));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
+  // main records: pooled rows pp0 .. pp0 + 3, window rows inside the item
+  for (int u = threadIdx.x; u < 4 * PQ * 8; u += nthr) {
+    const int c8 = u & 7, t = u >> 3, qq = t % PQ, pr = t / PQ;
+    float sg[8], best[8], bz[8];
+    int bt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sg[j] = p.sp_gamma[c8 * 8 + j] < 0.f ? -1.f : 1.f;
+      best[j] = -INFINITY;
+      bz[j] = 0.f;
+      bt[j] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int r = 2 * pr - 1 + i;  // (>= -1, <= 7)
+      if (r < 0) continue;            // the previous item's bottom row (stem_pool_apply)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = 2 * qq - 1 + k;
+        if (q < 0) continue;          // left padding
+        float f[8];
+        const uint4 cv = chunk(r, q, c8);
+        unpack8(cv, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = sg[j] * f[j];
+          if (v > best[j]) { best[j] = v; bz[j] = f[j]; bt[j] = 3 * i + k; }
+        }
+      }
+    }
+    const size_t o = (((size_t)img * PP + pp0 + pr) * PQ + qq) * 64 + c8 * 8;
+    *(uint4*)((bf16_t*)p.sp_zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
+    uint2 ib;
+    ib.x = (uint32_t)bt[0] | ((uint32_t)bt[1] << 8) | ((uint32_t)bt[2] << 16) | ((uint32_t)bt[3] << 24);
+    ib.y = (uint32_t)bt[4] | ((uint32_t)bt[5] << 8) | ((uint32_t)bt[6] << 16) | ((uint32_t)bt[7] << 24);
+    *(uint2*)(p.sp_idx + o) = ib;
+  }
+  // bottom record: output row p0 + 7 is window row 0 (taps 0..2) of the next item's first
+  // pooled row pp0 + 4
+  if (item + 1 < h.items_img) {
+    for (int u = threadIdx.x; u < PQ * 8; u += nthr) {
+      const int c8 = u & 7, qq = u >> 3;
+      float sg[8], best[8], bz[8];
+      int bt[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[j] = p.sp_gamma[c8 * 8 + j] < 0.f ? -1.f : 1.f;
+        best[j] = -INFINITY;
+        bz[j] = 0.f;
+        bt[j] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int q = 2 * qq - 1 + k;
+        if (q < 0) continue;
+        float f[8];
+        const uint4 cv = chunk(7, q, c8);
+        unpack8(cv, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = sg[j] * f[j];
+          if (v > best[j]) { best[j] = v; bz[j] = f[j]; bt[j] = k; }
+        }
+      }
+      const size_t o = (((size_t)img * h.items_img + item + 1) * PQ + qq) * 64 + c8 * 8;
+      *(uint4*)((bf16_t*)p.sp_bz + o) = pack8(bz);
+      uint2 ib;
+      ib.x = (uint32_t)bt[0] | ((uint32_t)bt[1] << 8) | ((uint32_t)bt[2] << 16) | ((uint32_t)bt[3] << 24);
+      ib.y = (uint32_t)bt[4] | ((uint32_t)bt[5] << 8) | ((uint32_t)bt[6] << 16) | ((uint32_t)bt[7] << 24);
+      *(uint2*)(p.sp_bidx + o) = ib;
+    }
+  }
+}
+
+// STEM_NW waves per block, STEM_ROWS output rows per item, STEM_OCC waves per SIMD.
+// PF (round 6): the stem max-pool fused in (IGemmArgs::sp_zsel).  Every subtile's bf16 z also
+// goes to an LDS image of the item's 8 x Q outputs (16-B chunks swizzled by pixel), and
+// after the item's MFMAs the block takes each pooled window's extreme from it: the
+// separate pool pass no longer reads z back from memory.
+template <int STEM_NW, int STEM_ROWS, int STEM_OCC, bool PF = false>
 __global__ __launch_bounds__(STEM_NW * 64, STEM_OCC) void conv_stem_kernel(IGemmArgs p,
                                                                            StemPlan h) {
   constexpr int STEM_MAX_CROWS = (STEM_ROWS - 1) * 2 + STEM_R;  // canvas rows, sh <= 2
@@ -53,6 +146,8 @@ __global__ __launch_bounds__(STEM_NW * 64, STEM_OCC) void conv_stem_kernel(IGemm
   constexpr int STEM_PREF = (STEM_LDS / 16 + STEM_NW * 64 - 1) / (STEM_NW * 64);  // vec/thread
   __shared__ __attribute__((aligned(16))) char canvas[STEM_LDS];
   __shared__ float red[STEM_NW][2][64];
+  __shared__ __attribute__((aligned(16))) char zimg[PF ? STEM_ROWS * SP_MAXQ * 128 : 16];
+  static_assert(!PF || STEM_ROWS == 8, "fused pool: 8-row items (4 pooled rows)");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kc = lane >> 4, li = lane & 15;
   const int Wp = p.aW, P = p.oH, Q = p.oW, sh = p.Uh;
@@ -152,6 +247,11 @@ __global__ __launch_bounds__(STEM_NW * 64, STEM_OCC) void conv_stem_kernel(IGemm
           }
           const uint32_t lo = pack2(v[0], v[1]), hi = pack2(v[2], v[3]);
           *(uint2*)(orow + 16 * nb) = make_uint2(lo, hi);
+          if constexpr (PF) {  // channels 16 nb + 4 kc .. +3: half of 16-B chunk 2 nb + kc / 2
+            const int q = q0 + li, ch = 2 * nb + (kc >> 1);
+            *LDS_PTR(u32x2, zimg + (pr * SP_MAXQ + q) * 128 + ((ch ^ (q & 7)) << 4) +
+                                ((kc & 1) << 3)) = u32x2{lo, hi};
+          }
           // statistics of the stored (bf16-rounded) values, shifted
           const float r0 = bf2f(lo & 0xffff) - shift[nb][0], r1 = bf2f(lo >> 16) - shift[nb][1];
           const float r2 = bf2f(hi & 0xffff) - shift[nb][2], r3 = bf2f(hi >> 16) - shift[nb][3];
@@ -164,6 +264,9 @@ __global__ __launch_bounds__(STEM_NW * 64, STEM_OCC) void conv_stem_kernel(IGemm
     }
     __syncthreads();  // every wave is done reading this item's canvas rows
     if (nxt < h.items) commit();
+    // (PF: after the commit, whose prefetch registers are then dead; the z image is not
+    // rewritten before the next item's MFMAs, behind the barrier below)
+    if constexpr (PF) stem_pool_item(p, h, zimg, img, p0);
     __syncthreads();
   }
 
@@ -209,6 +312,12 @@ bool conv_stem_ok(const IGemmArgs& a) {
        reinterpret_cast<uintptr_t>(a.C)) & 15)
     return false;
   if (a.aH < (a.oH - 1) * a.Uh + STEM_R || a.M % (a.oH * a.oW) != 0) return false;
+  if (a.sp_zsel &&  // fused pool: whole 8-row items, an even width the z image holds
+      (a.oH % 8 != 0 || a.oW % 2 != 0 || a.oW > SP_MAXQ || !a.sp_idx || !a.sp_bz ||
+       !a.sp_bidx || !a.sp_gamma || a.relu || a.bias ||
+       ((reinterpret_cast<uintptr_t>(a.sp_zsel) | reinterpret_cast<uintptr_t>(a.sp_bz)) & 15) ||
+       ((reinterpret_cast<uintptr_t>(a.sp_idx) | reinterpret_cast<uintptr_t>(a.sp_bidx)) & 7)))
+    return false;
   for (int t = 0; t < STEM_R; ++t)  // one super-tap per kernel row: dh = t, dw = 0, 4 columns
     if (a.taps.dh[t] != t || a.taps.dw[t] != 0 || a.taps.bt[t] != ((t * 4) | (4 << 12)))
       return false;
@@ -218,7 +327,7 @@ bool conv_stem_ok(const IGemmArgs& a) {
 // block shape: 8 waves x 8-row items, one block per CU (4 waves x 4-row items, two blocks
 // per CU, measured equal at batch 512 - 37.96k vs 38.01k img/s - and was removed)
 
-template <int NW, int ROWS, int OCC>
+template <int NW, int ROWS, int OCC, bool PF = false>
 static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
   StemPlan h{};
   h.items_img = (a.oH + ROWS - 1) / ROWS;
@@ -227,13 +336,93 @@ static int launch_stem(IGemmArgs a, int max_blocks, hipStream_t s) {
   h.crows = (ROWS - 1) * a.Uh + STEM_R;
   h.qsub = (a.oW + 15) / 16;
   const int grid = std::max(1, std::min(h.items, max_blocks));
-  hipLaunchKernelGGL((conv_stem_kernel<NW, ROWS, OCC>), dim3(grid), dim3(NW * 64), 0, s, a, h);
+  hipLaunchKernelGGL((conv_stem_kernel<NW, ROWS, OCC, PF>), dim3(grid), dim3(NW * 64), 0, s, a, h);
   return grid;
 }
 
 int conv_stem(IGemmArgs a, hipStream_t s) {
   // one statistics-slab row per block: the caller's slab holds >= slab_rows_max(M) rows
+  // (PF: 4-wave blocks, one wave per SIMD with 512 registers: the 112 weight registers held
+  // for the kernel's life plus the pooling pass spill at the 256 of an 8-wave block)
+  if (a.sp_zsel) return launch_stem<4, 8, 1, true>(a, std::min(HALO_MAX_ROWS, active_cus()), s);
   return launch_stem<8, 8, 1>(a, std::min(HALO_MAX_ROWS, active_cus()), s);
+}
+
+// stem_pool_apply: thread = (pooled pixel, 8-channel chunk); the BN affine as
+// bn_relu_maxpool_fwd_kernel computes it (rsqrt of the batch variance, fma shift)
+__global__ __launch_bounds__(256) void stem_pool_apply_kernel(
+    IGemmArgs p, int items_img, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, bf16_t* __restrict__ y, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, unsigned long long* __restrict__ counter) {
+  const int C = 64, PQ = p.oW >> 1, PP = p.oH >> 1;
+  const int nimg = p.M / (p.oH * p.oW);
+  const int64_t rows = (int64_t)nimg * PP * PQ;
+  if (blockIdx.x == 0 && threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const float mu = stats[c], var = stats[C + c];
+    const int64_t M = p.M;
+    mean_out[c] = mu;
+    rstd_out[c] = rsqrtf(var + eps);
+    const float unb = var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    if (counter && c == 0) atomicAdd(counter, 1ull);
+  }
+  const int c8 = threadIdx.x & 7;
+  float sc[8], sh[8], sg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c8 * 8 + j;
+    const float rs = rsqrtf(stats[C + c] + eps);
+    sc[j] = gamma[c] * rs;
+    sh[j] = __builtin_fmaf(-stats[c], sc[j], beta[c]);
+    sg[j] = gamma[c] < 0.f ? -1.f : 1.f;
+  }
+  bf16_t* const zsel = (bf16_t*)p.sp_zsel;
+  for (int64_t r = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3); r < rows;
+       r += (int64_t)gridDim.x * 32) {
+    const int qq = (int)(r % PQ);
+    const int64_t t = r / PQ;
+    const int pp = (int)(t % PP), img = (int)(t / PP);
+    const size_t o = (size_t)r * C + c8 * 8;
+    float z[8];
+    unpack8(*(const uint4*)(zsel + o), z);
+    if ((pp & 3) == 0 && pp > 0) {  // merge the previous item's bottom row (taps 0..2 first)
+      const size_t ob = (((size_t)img * items_img + (pp >> 2)) * PQ + qq) * C + c8 * 8;
+      float zb[8];
+      unpack8(*(const uint4*)((const bf16_t*)p.sp_bz + ob), zb);
+      const uint2 ib = *(const uint2*)(p.sp_bidx + ob);
+      uint2 im = *(const uint2*)(p.sp_idx + o);
+      uint32_t w[2] = {im.x, im.y};
+      const uint32_t wb[2] = {ib.x, ib.y};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (sg[j] * zb[j] >= sg[j] * z[j]) {  // (a tie keeps the earlier tap: the bottom row)
+          z[j] = zb[j];
+          const int sft = 8 * (j & 3);
+          w[j >> 2] = (w[j >> 2] & ~(0xffu << sft)) | (((wb[j >> 2] >> sft) & 0xffu) << sft);
+        }
+      }
+      *(uint4*)(zsel + o) = pack8(z);
+      *(uint2*)(p.sp_idx + o) = make_uint2(w[0], w[1]);
+    }
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(z[j] * sc[j] + sh[j], 0.f);
+    *(uint4*)(y + o) = pack8(v);
+  }
+}
+
+void stem_pool_apply(const IGemmArgs& a, const float* stats, const float* gamma,
+                     const float* beta, float* rmean, float* rvar, float momentum, float eps,
+                     bf16_raw* y, float* mean, float* rstd, int64_t* counter, hipStream_t s) {
+  const int items_img = a.oH / 8;
+  const int64_t rows = (int64_t)(a.M / (a.oH * a.oW)) * (a.oH / 2) * (a.oW / 2);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 31) / 32, 4096));
+  hipLaunchKernelGGL(stem_pool_apply_kernel, dim3(grid), dim3(256), 0, s, a, items_img, stats,
+                     gamma, beta, rmean, rvar, momentum, eps, (bf16_t*)y, mean, rstd,
+                     (unsigned long long*)counter);
 }
 
 // ======================================================================================
@@ -288,12 +477,25 @@ struct StemWPlan {
 // staged operand is the one the two-pass form wrote to memory.  Reference: the stem
 // conv1 -> bn1 -> relu -> maxpool of torchvision resnet / densenet (models.py:24-30, 74-80).
 // (StemPoolArgs: api.h)
+// POOL: 8-wave blocks.  Waves 4..7 are producers - the gathers and the VALU-heavy dz
+// formation of item k + 1 (~1,000 VALU per thread per item) run beside item k's MFMAs on
+// the CU's other wave slots - and waves 0..3 only read fragments and multiply: 0.88 ms per
+// b1024 step (as one 4-wave block, with the dz formation between the items' MFMA loops,
+// 1.0 ms).  Measured slower: issuing item k + 2's gathers right after forming item k + 1
+// (12 B/lane of spills: 1.22 ms), and 12-wave blocks with one unit per producer thread
+// (168 registers per wave spill the MFMA waves).
 template <int KS, bool POOL>
-__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h,
-                                                            StemPoolArgs pa) {
+__global__ __launch_bounds__(POOL ? 512 : 256, 1) void stem_wgrad_kernel(WGradArgs p,
+                                                                          StemWPlan h,
+                                                                          StemPoolArgs pa) {
   __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NPT = 256;  // staging threads (POOL: the producers)
+  constexpr int CVPT = (SW_CVV + NPT - 1) / NPT;  // canvas vectors per staging thread
+  const int lane = threadIdx.x & 63;
+  const int wave_all = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = wave_all & 3;
+  // staging-thread id (POOL: producer-local; negative on the MFMA waves, which never stage)
+  const int tid = POOL ? (int)threadIdx.x - 256 : (int)threadIdx.x;
   const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W;
   const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
   const int nfr = wave < 2 ? 4 : 3;  // column fragments j = wave + 4 i < 14
@@ -322,11 +524,12 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
   const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors] (POOL: z)
   const u32x4* const cvsrc = (const u32x4*)p.x;    // [n][Hc][Wc] pair vectors
   constexpr int NDZ = POOL ? 1 : KS;
-  u32x4 pdz[NDZ], pcv[SW_CVPT];
+  u32x4 pdz[NDZ], pcv[CVPT];
   // POOL: (cell, 8-channel chunk) units u = tid + 256 i (cell u >> 3 < Q / 2, chunk u & 7,
   // the same tid & 7 for both i), their gathered windows and z vectors, and the chunk's
   // BN-backward constants (bn_coeffs + maxpool_bn_bwd_cell_kernel<true>'s a, b, cco)
   constexpr int PU = POOL ? 2 : 1;
+  static_assert(!POOL || 4 * 128 <= NPT * PU, "one unit per producer thread (Q <= 128)");
   const int pch = (tid & 7) * 8;
   u32x4 qdp[PU][4], qz[PU][4];
   u32x2 qix[PU][4];
@@ -345,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
     const int r0 = 2 * Q;
     const int zb = (r0 >> 5) * 4096 + (r0 & 31) * 128, ze = KS * 4096;
     for (int s2 = 0; s2 < 2; ++s2)
-      for (int b = zb + tid * 16; b < ze; b += 256 * 16)
+      for (int b = zb + (int)threadIdx.x * 16; b < ze; b += (POOL ? 512 : 256) * 16)
         *LDS_PTR(u32x4, smem + s2 * SW_STAGE + b) = u32x4{0u, 0u, 0u, 0u};
   }
   auto fetch = [&](int it) {  // item it's vectors into registers (zeros past its end)
@@ -356,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       const int t = oh0 >> 1;
 #pragma unroll
       for (int i = 0; i < PU; ++i) {
-        const int u = tid + 256 * i;
+        const int u = tid + NPT * i;
         const int cq = u < 4 * Q ? (u >> 3) : 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {  // out-of-range windows load a clamped one (masked)
@@ -380,8 +583,8 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       }
     }
 #pragma unroll
-    for (int i = 0; i < SW_CVPT; ++i) {
-      const int v = tid + 256 * i;
+    for (int i = 0; i < CVPT; ++i) {
+      const int v = tid + NPT * i;
       pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
     }
   };
@@ -391,7 +594,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       const int t = (it - (it / h.items_img) * h.items_img);  // cell row = oh0 / 2
 #pragma unroll
       for (int i = 0; i < PU; ++i) {
-        const int u = tid + 256 * i;
+        const int u = tid + NPT * i;
         if (u >= 4 * Q) continue;
         const int cq = u >> 3;
         uint2 iv[4];
@@ -433,8 +636,8 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
       for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
     }
 #pragma unroll
-    for (int i = 0; i < SW_CVPT; ++i) {
-      const int v = tid + 256 * i;
+    for (int i = 0; i < CVPT; ++i) {
+      const int v = tid + NPT * i;
       if (v < SW_CVV) *LDS_PTR(u32x4, st + SW_DZ + v * 16) = pcv[i];
     }
   };
@@ -467,14 +670,29 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
 
   const int G = gridDim.x;
   int it = blockIdx.x;
-  if (it < h.items) {
+  if constexpr (POOL) {
+    if (wave_all >= 4) {  // producers: item k + 1's stage while the MFMA waves run item k
+      if (it < h.items) {
+        fetch(it);
+        commit(0, it);
+      }
+      for (int k = 0; it < h.items; ++k, it += G) {
+        __syncthreads();  // item k's stage published; item k - 1's stage free
+        if (it + G < h.items) {
+          fetch(it + G);
+          commit((k + 1) & 1, it + G);
+        }
+      }
+      return;
+    }
+  } else if (it < h.items) {
     fetch(it);
     commit(0, it);
   }
   for (int k = 0; it < h.items; ++k, it += G) {
     const int st = k & 1;
     __syncthreads();  // item k's stage written; every wave is done with item k-1's stage
-    const bool more = it + G < h.items;
+    const bool more = !POOL && it + G < h.items;
     if (more) fetch(it + G);  // lands under this item's MFMAs
     const char* sdz = smem + st * SW_STAGE;
     const char* scv = sdz + SW_DZ;
@@ -558,7 +776,7 @@ int stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s) {
   switch (h.ks) {
 #define SW_CASE(K)                                                                       \
   case K:                                                                                \
-    hipLaunchKernelGGL((stem_wgrad_kernel<K, true>), dim3(grid), dim3(256), 0, s, a, h, q); \
+    hipLaunchKernelGGL((stem_wgrad_kernel<K, true>), dim3(grid), dim3(512), 0, s, a, h, q); \
     break;
     SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
 #undef SW_CASE

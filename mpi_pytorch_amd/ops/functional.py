@@ -737,17 +737,28 @@ class _ConvBNReLUPool(torch.autograd.Function):
         sh, sw, ph, pw = conv.kgeom
         C = w.shape[0]
         stats = torch.empty(2, C, device=x.device, dtype=torch.float32)
-        z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats,
-                       _empty(x) if _NO_SHIFT else bn.running_mean)
-        # zsel: raw z at each window's argmax, so the backward's reduction pass reads only
-        # pooled-size tensors (maxpool_bn_bwd_sel_reduce_kernel)
-        N, H, W, C_ = z.shape
-        zsel = torch.empty(N, _pool_out(H, cfg[0], cfg[2], cfg[4], cfg[6]),
-                           _pool_out(W, cfg[1], cfg[3], cfg[5], cfg[6]), C_,
-                           device=z.device, dtype=z.dtype)
-        y, idx, mean, rstd = k.bn_relu_maxpool_fwd(z, stats, gamma, beta, bn.running_mean,
-                                                   bn.running_var, bn.momentum_value(), bn.eps,
-                                                   *cfg, bn.num_batches_tracked, zsel_out=zsel)
+        shift = _empty(x) if _NO_SHIFT else bn.running_mean
+        r = None
+        if (_STEM_POOL_FWD and x.is_cuda and b is None and tuple(cfg) == (3, 3, 2, 2, 1, 1, False)
+                and gamma is not None and beta is not None):
+            # the pool taken inside the stem conv kernel, BN + ReLU on the pooled extremes
+            r = k.conv_stem_pool_fwd(x, weight_of(w), sh, sw, ph, pw, stats, shift, gamma, beta,
+                                     bn.running_mean, bn.running_var, bn.momentum_value(),
+                                     bn.eps, bn.num_batches_tracked)
+        if r is not None:
+            y, idx, mean, rstd, z, zsel = r
+        else:
+            z = k.conv_fwd(x, weight_of(w), _or_empty(b, x), sh, sw, ph, pw, False, stats, shift)
+            # zsel: raw z at each window's argmax, so the backward's reduction pass reads only
+            # pooled-size tensors (maxpool_bn_bwd_sel_reduce_kernel)
+            N, H, W, C_ = z.shape
+            zsel = torch.empty(N, _pool_out(H, cfg[0], cfg[2], cfg[4], cfg[6]),
+                               _pool_out(W, cfg[1], cfg[3], cfg[5], cfg[6]), C_,
+                               device=z.device, dtype=z.dtype)
+            y, idx, mean, rstd = k.bn_relu_maxpool_fwd(z, stats, gamma, beta, bn.running_mean,
+                                                       bn.running_var, bn.momentum_value(),
+                                                       bn.eps, *cfg, bn.num_batches_tracked,
+                                                       zsel_out=zsel)
         ctx.conv = conv
         ctx.cfg = cfg
         ctx.bias = b
@@ -797,7 +808,12 @@ class _ConvBNReLUPool(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None
 
 
-_STEM_POOL_WGRAD = os.environ.get("MPA_STEM_POOL_WGRAD", "1") == "1"  # (A/B switch)
+# (A/B switches) the stem's pool backward inside its weight gradient (on: 1.06 ms vs 1.63 ms
+# two-pass at batch 1024), and its pool forward inside the stem conv kernel (conv_stem.hip;
+# off: the 114 KB z image in LDS leaves one 4-wave block per CU, 1.64 ms vs 1.17 ms for
+# conv + bn_relu_maxpool_fwd - profiles/stem_pool_r6.txt)
+_STEM_POOL_WGRAD = os.environ.get("MPA_STEM_POOL_WGRAD", "1") == "1"
+_STEM_POOL_FWD = os.environ.get("MPA_STEM_POOL_FWD", "0") == "1"
 
 
 def conv_bn_relu_maxpool(x, conv, bn, pool):

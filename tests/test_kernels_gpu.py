@@ -1635,3 +1635,55 @@ def test_halo_mi7_tiles_bitwise(gpu, N):
     assert rel(s1, s0) < 1e-5
     assert rel(y1, ref.conv_fwd(x, w, e, 1, 1, 1, 1, False, None, None)) < 1e-2
     assert rel(d1, ref.conv_dgrad(dy, w, H, H, 1, 1, 1, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("N,HW", [(3, 224), (2, 128), (1, 64)])
+def test_stem_pool_fused_forward(gpu, N, HW):
+    """Fused stem forward (round 6): the 3x3/s2/p1 max-pool taken inside the pixel-pair stem
+    conv kernel (conv_stem.hip PF, items of 8 output rows; an item's first pooled row merged
+    with the previous item's bottom row by stem_pool_apply) vs the two-pass form (conv_fwd +
+    bn_relu_maxpool_fwd).  z and y are bitwise equal; the argmax tap and the selected z
+    agree wherever relu(bn(z)) > 0 (where it is 0 the two forms may pick different zeros,
+    which carry no gradient); gamma < 0 channels select the window minimum.  (Opt-in,
+    MPA_STEM_POOL_FWD=1: slower than the two-pass form, profiles/stem_pool_r6.txt.)"""
+    from mpi_pytorch_amd.models.layers import Conv2d
+    torch.manual_seed(9)
+    P = HW // 2
+    x = bf(N, 2 * (P - 1) + 7, P + 3, 8, dev=gpu, scale=0.5)
+    w = bf(64, 7, 4, 8, dev=gpu, scale=0.05)
+    g = torch.rand(64, device=gpu) + 0.5
+    g[1::4] *= -1.0
+    b = torch.randn(64, device=gpu) * 0.3
+    shift = torch.randn(64, device=gpu) * 0.05
+    out = []
+    for fused in (True, False):
+        rm, rv = torch.zeros(64, device=gpu), torch.ones(64, device=gpu)
+        cnt = torch.zeros((), dtype=torch.long, device=gpu)
+        st = torch.empty(2, 64, device=gpu)
+        if fused:
+            r = C().conv_stem_pool_fwd(x, w, 2, 1, 0, 0, st, shift, g, b, rm, rv, 0.1, 1e-5, cnt)
+            assert r is not None
+            y, idx, mean, rstd, z, zsel = r
+        else:
+            z = C().conv_fwd(x, w, torch.empty(0, device=gpu), 2, 1, 0, 0, False, st, shift)
+            zsel = torch.empty(N, P // 2, P // 2, 64, device=gpu, dtype=torch.bfloat16)
+            y, idx, mean, rstd = C().bn_relu_maxpool_fwd(z, st, g, b, rm, rv, 0.1, 1e-5, 3, 3, 2,
+                                                         2, 1, 1, False, cnt, zsel_out=zsel)
+        out.append((y, idx, mean, rstd, z, zsel, rm, rv, int(cnt)))
+    (y1, i1, m1, r1, z1, s1, rm1, rv1, c1), (y0, i0, m0, r0, z0, s0, rm0, rv0, c0) = out
+    assert torch.equal(z1, z0)
+    assert rel(m1, m0) < 1e-4 and rel(r1, r0) < 1e-4 and rel(rm1, rm0) < 1e-4
+    assert rel(rv1, rv0) < 1e-4 and c1 == c0 == 1
+    assert rel(y1.float(), y0.float()) < 1e-3
+    live = y0 > 0
+    assert float(live.float().mean()) > 0.2
+    assert torch.equal(i1[live], i0[live]) and torch.equal(s1[live], s0[live])
+    # the selected z is an extreme of its window in the gamma-signed order (oracle)
+    gi = _global_idx(i1, P, P, 3, 3, 2, 2, 1, 1)
+    zr = z1.float().permute(0, 3, 1, 2).reshape(N, 64, -1)
+    picked = torch.gather(zr, 2, gi.permute(0, 3, 1, 2).reshape(N, 64, -1).long())
+    assert torch.equal(picked.reshape(N, 64, P // 2, P // 2).permute(0, 2, 3, 1),
+                       s1.float())
+    sgn = torch.where(g < 0, -1.0, 1.0).view(1, 64, 1, 1)
+    pooled = torch.nn.functional.max_pool2d((zr.reshape(N, 64, P, P) * sgn), 3, 2, 1)
+    assert torch.equal(pooled * sgn, s1.float().permute(0, 3, 1, 2))

@@ -33,8 +33,10 @@ def test_bench_two_ranks_one_gpu(gpu, tmp_path):
                        timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    rec = json.loads(lines[0])
+    # the headline line, then the complete record with the multi-GPU decision extras
+    assert len(lines) == 2, r.stdout
+    head, rec = json.loads(lines[0]), json.loads(lines[1])
+    assert head["value"] == rec["value"] and "multi_gpu" in rec
     assert rec["n_gpus"] == 2 and rec["config"]["backend"] == "gloo"
     assert rec["config"]["parallelism"] == "dp2" and rec["dtype"] == "bf16"
     assert rec["comm"]["timed"] and all(b["calls"] == 3 for b in rec["comm"]["buckets"])
