@@ -155,6 +155,24 @@ def parse_args(argv=None):
     return args
 
 
+def _cpu_stat() -> dict:
+    """cgroup CPU-throttling counters of this container (cgroup v2 / v1 cpu.stat; empty if
+    unreadable): a cgroup over its CPU quota is frozen for the rest of the period, the host
+    stops enqueueing and the GPU idles - recorded so a slow run can be told apart."""
+    for f in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat",
+              "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"):
+        try:
+            out = {}
+            with open(f) as fh:
+                for line in fh:
+                    k, v = line.split()
+                    out[k] = int(v)
+            return out
+        except (OSError, ValueError):
+            continue
+    return {}
+
+
 def _inject() -> str:
     return os.environ.get("MPA_BENCH_INJECT", "")
 
@@ -482,6 +500,7 @@ def run(args) -> None:
     sync()
     barrier()
     sync()
+    cs0, cpu0 = _cpu_stat(), time.process_time()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if i == 1 and world.rank == hang_rank:
@@ -497,6 +516,7 @@ def run(args) -> None:
     barrier()
     sync()
     dt = time.perf_counter() - t0
+    cs1, cpu1 = _cpu_stat(), time.process_time()
     wd.stop()
     faulthandler.cancel_dump_traceback_later()
     loss = step.mean_loss()
@@ -553,6 +573,12 @@ def run(args) -> None:
         rec["comm"] = comm
     if ring is not None:
         rec["data_ring"] = ring
+    host = {"process_cpu_s": round(cpu1 - cpu0, 3)}
+    if "throttled_usec" in cs1:
+        host["cgroup_throttled_ms"] = round((cs1["throttled_usec"] -
+                                             cs0.get("throttled_usec", 0)) / 1e3, 1)
+        host["cgroup_nr_throttled"] = cs1.get("nr_throttled", 0) - cs0.get("nr_throttled", 0)
+    rec["host"] = host
     from mpi_pytorch_amd.parallel.dist import affinity
     if affinity() is not None:
         rec["host_affinity"] = affinity()
@@ -564,6 +590,9 @@ def run(args) -> None:
     timer = _deadline(args.extras_budget, emitter, world.rank)
     if inject == "extras_hang":
         time.sleep(1e6)
+    if inject == "extras_gil_hang":  # test hook: a native call that blocks holding the GIL
+        import ctypes
+        ctypes.PyDLL(None).sleep(1000000)
     if inject.startswith("extras_abort=") and world.rank == int(inject.split("=", 1)[1]):
         os._exit(134)  # test hook: a native abort inside an extra
     if world.world_size > 1 and not args.emulate_comm and args.decisions:

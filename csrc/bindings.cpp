@@ -1702,6 +1702,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_set_engine", &mpa::igemm_set_engine);
   m.def("igemm_force_tile", &mpa::igemm_force_tile, "override GEMM tile (BM, BN, splits); 0 = auto");
   m.def("igemm_set_tune", &mpa::igemm_set_tune, "tile autotuner on/off (MPA_TUNE)");
+  m.def("igemm_set_tune_drain", &mpa::igemm_set_tune_drain,
+        "tuner candidates: drain the whole device (1, single GPU) or only their stream (0)");
   m.def("set_deterministic", &mpa::set_deterministic,
         "fixed-order reductions + no timing-based autotuning (MPA_DETERMINISTIC)");
   m.def("deterministic", &mpa::deterministic);

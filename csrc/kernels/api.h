@@ -178,6 +178,7 @@ void igemm_set_engine(int engine);
 void igemm_force_tile(int bm, int bn, int splits);  // measurement override (0: auto)
 // tile autotuner (igemm.hip): on by default (MPA_TUNE=0 off); the cached choices as text
 void igemm_set_tune(int on);
+void igemm_set_tune_drain(int on);  // tuner drains the device (1) or its stream (0)
 std::string igemm_tuned_table();
 // adopt a table in igemm_tuned_table()'s format (replace: drop the current entries first)
 int igemm_tuned_load(const std::string& table, bool replace);

@@ -574,6 +574,12 @@ static bool g_tune = [] {
   return !(e && e[0] == '0');
 }();
 void igemm_set_tune(int on) { g_tune = on != 0; }
+// Drain the whole device before timing a tuner candidate (single GPU: side / branch
+// streams may still run kernels whose overlap would bias the choice).  Off under data
+// parallelism (parallel/dist.py init_world): the drain would also wait for the overlapped
+// RCCL all-reduces of the first step; the compute stream alone is synchronized then.
+static bool g_tune_drain = true;
+void igemm_set_tune_drain(int on) { g_tune_drain = on != 0; }
 
 struct TunedTile {
   int bm, bn;
@@ -612,7 +618,8 @@ static char* tune_scratch(size_t bytes) {
 // rounds of three launches.  Tuning only runs on a shape's first launch outside a capture.
 template <class F>
 static float time_launches(F&& fn, hipStream_t s) {
-  (void)hipDeviceSynchronize();
+  if (g_tune_drain) (void)hipDeviceSynchronize();
+  else (void)hipStreamSynchronize(s);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);

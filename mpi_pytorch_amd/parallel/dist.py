@@ -91,6 +91,12 @@ def init_world(device: str = "auto", timeout_s: float = 1800.0,
             if be == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
+        if use_cuda:
+            # the GEMM tuner then syncs only its own stream: a device drain would also wait
+            # for the first step's overlapped all-reduces (csrc/kernels/igemm.hip)
+            from ..ops import _ext
+            if _ext.available():
+                _ext.ext().igemm_set_tune_drain(0)
     _WORLD = World(rank=rank, world_size=world, local_rank=local, device=dev, backend=be)
     return _WORLD
 

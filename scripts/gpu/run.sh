@@ -21,6 +21,7 @@
 #   gaps=ARGS        kernel trace of bench.py ARGS, inter-kernel gap distribution (tools/gap_stats.py)
 #   (PMC_ARGS in the environment: extra bench.py arguments of pmc / trace)
 #   py=SCRIPT,ARGS   python SCRIPT ARGS under a 300 s limit      -> TAG_py_N.log
+#   env=NAME=VALUE   export NAME=VALUE for the steps after it
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -50,7 +51,8 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python bench.py $(args_of "$val") > ${O}_bench.json 2> ${O}_bench.err \
         || { tail -20 ${O}_bench.err; exit 1; }
-      python -c "import json; d=json.loads(open('${O}_bench.json').read().strip().splitlines()[-1]); print('bench', d['value'], d['ms_per_step'], d.get('small_batch'))" ;;
+      cp ${O}_bench.json ${O}_bench_$n.json
+      python -c "import json; d=json.loads(open('${O}_bench.json').read().strip().splitlines()[-1]); print('bench', d['value'], d['ms_per_step'], d.get('small_batch'), d.get('phases_ms'), d.get('data_ring'), d.get('host'))" ;;
     seq)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/${O}_seq -o r18 \
         -- python3 $R/bench.py --steps 3 --warmup 2 --small-batch 0 $(args_of "$val") \
@@ -107,6 +109,7 @@ for step in "$@"; do
       timeout -k 10 300 python $s $(args_of "$a") > ${O}_py_$n.log 2>&1 \
         || { tail -30 ${O}_py_$n.log; exit 1; }
       tail -15 ${O}_py_$n.log ;;
+    env) export "$val"; echo "export $val" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done

@@ -1205,17 +1205,23 @@ def test_bn_relu_maxpool_fused(gpu, case):
     assert rel(dg3, dg) < 1e-4 and rel(db3, db) < 1e-4
 
 
-@pytest.mark.parametrize("N,P,Q", [(2, 112, 112), (3, 64, 64), (2, 56, 56), (1, 32, 40)])
-def test_stem_pool_wgrad(gpu, N, P, Q):
+@pytest.mark.parametrize("N,P,Q,ties", [(2, 112, 112, False), (3, 64, 64, False),
+                                         (2, 56, 56, False), (1, 32, 40, False),
+                                         (2, 56, 56, True)])
+def test_stem_pool_wgrad(gpu, N, P, Q, ties):
     """Fused stem backward (round 6): the pooled-only sums + the weight gradient that forms
     dz = a g + b + cco z in its operand staging (conv_stem.hip, POOL form) against the
     two-pass form (maxpool_bn_bwd writes dz, conv_wgrad reads it: the same bf16 dz, so
     equal to fp32 summation order) and the fp32 oracle.  Channels with gamma < 0, the
-    K-step tail rows (2Q % 32 != 0) and the last window row / column are covered."""
+    K-step tail rows (2Q % 32 != 0) and the last window row / column are covered; `ties`
+    quantises z to halves, so most windows hold tied maxima (the forward's argmax tap is
+    the one every form follows)."""
     torch.manual_seed(21)
     Cc = 64
     x = bf(N, 2 * (P - 1) + 7, Q + 3, 8, dev=gpu, scale=0.5)
     z = (bf(N, P, Q, Cc, dev=gpu, scale=1.5) + 0.2).to(torch.bfloat16)
+    if ties:
+        z = (z.float() * 2).round().div(2).to(torch.bfloat16)
     st = torch.stack([z.float().reshape(-1, Cc).mean(0),
                       z.float().reshape(-1, Cc).var(0, unbiased=False)])
     g = torch.rand(Cc, device=gpu) + 0.5

@@ -107,6 +107,22 @@ def test_bench_prints_headline_when_extras_hang(tmp_path):
     assert "timeout: extras exceeded" in r.stderr
 
 
+def test_bench_backstop_ends_a_rank_stuck_holding_the_gil(tmp_path):
+    """Both ranks block in a native call that holds the GIL inside the extras (libc sleep
+    through ctypes.PyDLL - what a blocking HIP call without a GIL release does), so neither
+    the budget timer thread nor the watchdog thread can run: the faulthandler backstop
+    (budget + 30 s, no Python thread) dumps the stacks and ends the job non-zero, the
+    headline line already on stdout (bench.py)."""
+    r, lines, dt = _bench_cpu(tmp_path, "extras_gil_hang", ["--extras-budget", "2"],
+                              timeout=300)
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert len(lines) >= 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and "multi_gpu" not in rec
+    assert "Timeout" in r.stderr and "launch: rank" in r.stderr
+    assert dt < 200
+
+
 def test_bench_keeps_headline_when_a_rank_aborts_in_extras(tmp_path):
     """Rank 1 dies inside the extras (os._exit(134), what a native abort or a GPU fault in
     a multi-GPU variant does): the headline line is on stdout, and the job exits non-zero
