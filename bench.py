@@ -96,10 +96,10 @@ def parse_args(argv=None):
                    help="cpu: plumbing check of the same code path on host ops (gloo for N>1)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=1024,
-                   help="per-GPU batch (profiles/batch_sweep_r2.txt: 512 -> 42.9k, 1024 -> 47.1-48.1k, "
-                        "2048 -> 50.5k img/s; 1024 keeps a 21 ms step and halves the all-reduce's "
-                        "share of a data-parallel step)")
+    p.add_argument("--batch", type=int, default=2048,
+                   help="per-GPU batch (profiles/batch_sweep_r6.txt, one MI355X, same box: 1024 -> "
+                        "53.3k, 1536 -> 54.9k, 2048 -> 54.7-55.5k img/s; ~57 GB of the 288 GB "
+                        "HBM, and the all-reduce's share of a data-parallel step halves again)")
     p.add_argument("--model", default="resnet18")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--classes", type=int, default=64500)
@@ -147,6 +147,13 @@ def parse_args(argv=None):
     p.add_argument("--watchdog", type=float, default=180.0,
                    help="seconds without a completed step (device events) before a rank "
                         "dumps its stacks and exits 75 (0 off)")
+    p.add_argument("--data-threads", type=int, default=4,
+                   help="C++ producer threads of the synthetic input ring")
+    p.add_argument("--reserve-gib", type=float,
+                   default=float(os.environ.get("MPA_RESERVE_GIB", "160")),
+                   help="grow the caching allocator by one segment of this size (capped at "
+                        "90%% of free device memory) before building the model (0: off; "
+                        "engine.reserve_device_memory)")
     p.add_argument("--extras-budget", type=float, default=150.0,
                    help="wall-clock budget of everything after the headline measurement "
                         "(multi-GPU decisions, small-batch pass); on expiry the headline line "
@@ -171,6 +178,43 @@ def _cpu_stat() -> dict:
         except (OSError, ValueError):
             continue
     return {}
+
+
+def _hbm_probe(dev, gib: int = 16, reps: int = 3):
+    """Streaming-write bandwidth (GB/s) of a fresh ``gib`` GiB buffer, ``reps`` times."""
+    t = torch.empty(gib << 29, dtype=torch.bfloat16, device=dev)
+    out = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        t.fill_(1.0)
+        b.record()
+        b.synchronize()
+        out.append(round((gib << 30) / a.elapsed_time(b) / 1e6, 1))
+    del t
+    torch.cuda.empty_cache()
+    return out
+
+
+def _gpu_busy():
+    """Per card of the host (amdgpu sysfs): gpu_busy_percent and the current shader clock
+    level (pp_dpm_sclk's starred line), or None."""
+    import glob
+    vals = []
+    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            busy = int(open(d + "/gpu_busy_percent").read().strip())
+        except (OSError, ValueError):
+            continue
+        clk = None
+        try:
+            for line in open(d + "/pp_dpm_sclk"):
+                if "*" in line:
+                    clk = line.split(":", 1)[1].replace("*", "").strip()
+        except OSError:
+            pass
+        vals.append([d.split("/")[-2], busy, clk])
+    return vals or None
 
 
 def _inject() -> str:
@@ -427,6 +471,13 @@ def run(args) -> None:
             args.gpus, world.world_size))
     torch.manual_seed(0)
     dev = world.device
+    # device memory free at start (a previous process's memory still being released shows
+    # here; see docs/NOTES.md "Slow processes")
+    mem0 = [round(v / 2**30, 1) for v in torch.cuda.mem_get_info(dev)] if cuda else None
+    bw0 = _hbm_probe(dev) if cuda else None
+    from mpi_pytorch_amd.engine import reserve_device_memory
+    share = max(1, -(-world.world_size // max(torch.cuda.device_count(), 1))) if cuda else 1
+    reserved = reserve_device_memory(dev, args.reserve_gib / share)  # (ranks per GPU share it)
 
     def sync():
         if cuda:
@@ -438,7 +489,8 @@ def run(args) -> None:
                                          comm_dtype=args.comm_dtype, comm_ctas=args.comm_ctas)
     spec = input_spec(model, hw)  # the stem's image layout, written by the preprocess kernel
     data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
-                            world=world.world_size, depth=6, threads=4, cpad=spec["cpad"],
+                            world=world.world_size, depth=6, threads=args.data_threads,
+                            cpad=spec["cpad"],
                             pad=spec["pad"])
 
     if args.static_data:
@@ -512,6 +564,8 @@ def run(args) -> None:
             mk.range_pop()
         step(x, y)
         beat()
+    # (sampled while the device still runs the last queued steps; host side only)
+    cards = _gpu_busy() if cuda else None
     sync()
     barrier()
     sync()
@@ -578,6 +632,11 @@ def run(args) -> None:
         host["cgroup_throttled_ms"] = round((cs1["throttled_usec"] -
                                              cs0.get("throttled_usec", 0)) / 1e3, 1)
         host["cgroup_nr_throttled"] = cs1.get("nr_throttled", 0) - cs0.get("nr_throttled", 0)
+    if mem0 is not None:
+        host["device_free_total_gib_at_start"] = mem0
+        host["hbm_probe_at_start_gbps"] = bw0
+        host["reserved_gib"] = reserved
+        host["cards_busy_sclk"] = cards
     rec["host"] = host
     from mpi_pytorch_amd.parallel.dist import affinity
     if affinity() is not None:

@@ -1,1 +1,2 @@
-from .step import TrainStep, build_model, build_training, loss_fn, steps_without_gc  # noqa: F401
+from .step import (TrainStep, build_model, build_training, loss_fn,  # noqa: F401
+                   reserve_device_memory, steps_without_gc)

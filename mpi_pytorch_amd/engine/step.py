@@ -348,6 +348,31 @@ class TrainStep:
         return True
 
 
+def reserve_device_memory(device, gib: float) -> float:
+    """Grow PyTorch's caching allocator by ONE segment of ``gib`` GiB (capped at 90 % of the
+    free device memory) up front, so a training run's tensors are carved from it instead of
+    hipMalloc'ing new segments during the first steps.
+
+    Why: the caching allocator keeps growing for several steps (tensors used on the side
+    stream are record_stream'ed and come back late), and a hipMalloc right after another
+    process released tens of GB can stall the host for milliseconds while the driver still
+    reclaims that memory - a process then runs 1.6-5x slower for its whole life (batch 2048
+    ResNet-18, SqueezeNet b512; docs/NOTES.md "Slow processes").  Returns the GiB reserved."""
+    if gib <= 0 or device.type != "cuda":
+        return 0.0
+    free, _ = torch.cuda.mem_get_info(device)
+    n = int(min(gib * 2**30, 0.9 * free))
+    while n >= 2**30:  # (ranks sharing a GPU race for it: halve on failure)
+        try:
+            t = torch.empty(n, dtype=torch.uint8, device=device)
+        except torch.cuda.OutOfMemoryError:
+            n //= 2
+            continue
+        del t  # (the allocator keeps the segment cached)
+        return round(n / 2**30, 1)
+    return 0.0
+
+
 def build_training(name: str, num_classes: int, device, world: World, lr: float,
                    optimizer: str = "adam", momentum: float = 0.9, weight_decay: float = 0.0,
                    feature_extract: bool = False, bucket_mb: float = 16.0, overlap: bool = True,
