@@ -85,6 +85,8 @@ class Config:
     checksum_every: int = 0                # cross-rank replica checksum period (steps, 0=off)
     timeout_s: float = 1800.0              # rendezvous/collective timeout
     watchdog_s: float = 900.0              # abort a rank with no step progress (0: off)
+    reserve_gib: float = 0.0               # grow the allocator by one segment up front
+                                           # (engine.reserve_device_memory; NOTES "Slow processes")
 
     def __post_init__(self) -> None:
         if not self.CHECKPOINT_NAME:

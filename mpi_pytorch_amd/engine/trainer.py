@@ -178,6 +178,10 @@ def run_training(cfg: Config) -> dict:
         log.info("_Validation Loader Created")
 
     # ------------------------------------------------------------------- model
+    if cfg.reserve_gib > 0:
+        from .step import reserve_device_memory
+        log.debug("reserved {} GiB of device memory".format(
+            reserve_device_memory(dev, cfg.reserve_gib)))
     model, opt, step, _input_size = build_training(
         cfg.MODEL_NAME, cfg.NUM_CLASSES, dev, world, cfg.LR, cfg.optimizer, cfg.momentum,
         cfg.weight_decay, cfg.FEATURE_EXTRACT, cfg.bucket_mb, cfg.overlap_comm,
