@@ -464,46 +464,82 @@ struct StemWPlan {
   int ks;                // K-steps per item: ceil(2 Q / 32) (= the kernel's KS)
 };
 
-// ---------------------------------------------------------------------------------------
-// POOL form (round 6): the stem's BN + ReLU + 3x3/s2/p1 max-pool backward runs INSIDE the
-// weight gradient's staging, so the full-resolution dz is never written or read back.
-// An item (output rows 2t, 2t+1) is exactly one row of 2x2 cells; cell (t, c) is covered
-// by the pooled windows (t | t+1, c | c+1).  Per (cell, 8 channels) a thread gathers the 4
-// windows' pooled gradient dp and argmax taps plus the cell's 4 z vectors (issued under the
-// previous item's MFMAs, like the dz loads they replace), then writes
-//   dz = a g + b + cco z,  g = sum of dp over windows whose argmax is this pixel, masked
-//        by bn(z) > 0  (a = gamma rstd, b / cco from the pooled sums (sum g, sum g xhat))
-// to the dz stage - the arithmetic of maxpool_bn_bwd_cell_kernel<true> (bn.hip), so the
-// staged operand is the one the two-pass form wrote to memory.  Reference: the stem
-// conv1 -> bn1 -> relu -> maxpool of torchvision resnet / densenet (models.py:24-30, 74-80).
-// (StemPoolArgs: api.h)
-// POOL: 8-wave blocks.  Waves 4..7 are producers - the gathers and the VALU-heavy dz
-// formation of item k + 1 (~1,000 VALU per thread per item) run beside item k's MFMAs on
-// the CU's other wave slots - and waves 0..3 only read fragments and multiply: 0.88 ms per
-// b1024 step (as one 4-wave block, with the dz formation between the items' MFMA loops,
-// 1.0 ms).  Measured slower: issuing item k + 2's gathers right after forming item k + 1
-// (12 B/lane of spills: 1.22 ms), and 12-wave blocks with one unit per producer thread
-// (168 registers per wave spill the MFMA waves).
-template <int KS, bool POOL>
-__global__ __launch_bounds__(POOL ? 512 : 256, 1) void stem_wgrad_kernel(WGradArgs p,
-                                                                          StemWPlan h,
-                                                                          StemPoolArgs pa) {
-  __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
-  constexpr int NPT = 256;  // staging threads (POOL: the producers)
-  constexpr int CVPT = (SW_CVV + NPT - 1) / NPT;  // canvas vectors per staging thread
-  const int lane = threadIdx.x & 63;
-  const int wave_all = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wave = wave_all & 3;
-  // staging-thread id (POOL: producer-local; negative on the MFMA waves, which never stage)
-  const int tid = POOL ? (int)threadIdx.x - 256 : (int)threadIdx.x;
-  const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W;
-  const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
-  const int nfr = wave < 2 ? 4 : 3;  // column fragments j = wave + 4 i < 14
+// one item's MFMAs: all KS K-steps of (dz stage sdz, canvas scv), software-pipelined (the
+// next K-step's fragments are read under this one's MFMAs).  Waves 2 and 3 own three column
+// fragments; their fourth (a duplicate of fragment 13) keeps the MFMA stream branch-free -
+// those waves would idle at the item barrier anyway - and is never stored.
+// (BBQ: the B granule offsets are recomputed per K-step from Q instead of held in 2 KS
+// registers - the pooled form's MFMA waves also carry a dz unit)
+template <int KS, bool BBQ = false>
+__device__ __forceinline__ void stem_wgrad_item(const char* sdz, const char* scv,
+                                                const int (&bb)[KS][2], int Wc, int wave,
+                                                int lane, f32x4 (&acc)[4][4], int Q = 0) {
+  auto load_frags = [&](int ks, bf16x8(&af)[4], bf16x8(&bf)[4]) {
+#pragma unroll
+    for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sdz + ks * 4096, 16 * km, lane);
+    int b0, b1;
+    if constexpr (BBQ) {
+      const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
+      int bo[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int pl = min(32 * ks + 8 * g + qd + 4 * e, 2 * Q - 1);
+        const int prow = pl >= Q ? 1 : 0;
+        bo[e] = ((2 * prow) * Wc + pl - prow * Q + (pp >> 1)) * 16 + (pp & 1) * 8;
+      }
+      b0 = bo[0];
+      b1 = bo[1];
+    } else {
+      b0 = bb[ks][0];
+      b1 = bb[ks][1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = min(wave + 4 * i, 13);
+      const int toff = ((j >> 1) * Wc + 2 * (j & 1)) * 16;  // tap row r, pair column s0
+      const s16x4 lo =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + b0 + toff));
+      const s16x4 hi =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + b1 + toff));
+      s16x8 r;
+      r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+      r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+      bf[i] = __builtin_bit_cast(bf16x8, r);
+    }
+  };
+  bf16x8 af[2][4], bf[2][4];
+  load_frags(0, af[0], bf[0]);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 1 < KS) load_frags(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int km = 0; km < 4; ++km)
+        acc[km][i] = mfma16(bf[ks & 1][i], af[ks & 1][km], acc[km][i]);
+  }
+}
 
-  // per-lane canvas byte offsets of the B granules (item independent): K-step ks, half e
-  // -> item pixel pl = 32 ks + 8 g + qd + 4 e -> (row, ow); pixels past 2 Q are clamped
-  // (their dz rows are zero)
-  int bb[KS][2];
+// a block's partial -> its slab row: dw[k][col], k = 16 km + lane % 16,
+// col = 16 j + 4 (lane / 16) .. +3
+__device__ __forceinline__ void stem_wgrad_store(float* dst, const f32x4 (&acc)[4][4], int nfr,
+                                                 int wave, int li, int g) {
+#pragma unroll
+  for (int km = 0; km < 4; ++km)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= nfr) break;
+      const int j = wave + 4 * i;
+      *(f32x4*)(dst + (16 * km + li) * 224 + 16 * j + 4 * g) = acc[km][i];
+    }
+}
+
+// per-lane canvas byte offsets of the B granules (item independent): K-step ks, half e ->
+// item pixel pl = 32 ks + 8 g + qd + 4 e -> (row, ow); pixels past 2 Q are clamped (their
+// dz rows are zero)
+template <int KS>
+__device__ __forceinline__ void stem_wgrad_boffs(int (&bb)[KS][2], int Q, int Wc, int lane) {
+  const int g = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -513,6 +549,19 @@ __global__ __launch_bounds__(POOL ? 512 : 256, 1) void stem_wgrad_kernel(WGradAr
       const int ow = pl - prow * Q;
       bb[ks][e] = ((2 * prow) * Wc + ow + (pp >> 1)) * 16 + (pp & 1) * 8;
     }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h) {
+  __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
+  constexpr int CVPT = SW_CVPT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W;
+  const int g = lane >> 4, li = lane & 15;
+  const int nfr = wave < 2 ? 4 : 3;  // column fragments j = wave + 4 i < 14
+  int bb[KS][2];
+  stem_wgrad_boffs<KS>(bb, Q, Wc, lane);
   // this thread's staging slots: dz vector tid + 256 i (row = v >> 3, chunk = v & 7) and
   // canvas vector tid + 256 i
   int dzoff[KS];
@@ -521,123 +570,33 @@ __global__ __launch_bounds__(POOL ? 512 : 256, 1) void stem_wgrad_kernel(WGradAr
     const int v = tid + 256 * i, row = v >> 3, chunk = v & 7;
     dzoff[i] = (row >> 5) * 4096 + mn_off<64>(row & 31, chunk * 8);
   }
-  const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors] (POOL: z)
+  const u32x4* const dzsrc = (const u32x4*)p.dy;   // [pix][8 vectors]
   const u32x4* const cvsrc = (const u32x4*)p.x;    // [n][Hc][Wc] pair vectors
-  constexpr int NDZ = POOL ? 1 : KS;
-  u32x4 pdz[NDZ], pcv[CVPT];
-  // POOL: (cell, 8-channel chunk) units u = tid + 256 i (cell u >> 3 < Q / 2, chunk u & 7,
-  // the same tid & 7 for both i), their gathered windows and z vectors, and the chunk's
-  // BN-backward constants (bn_coeffs + maxpool_bn_bwd_cell_kernel<true>'s a, b, cco)
-  constexpr int PU = POOL ? 2 : 1;
-  static_assert(!POOL || 4 * 128 <= NPT * PU, "one unit per producer thread (Q <= 128)");
-  const int pch = (tid & 7) * 8;
-  u32x4 qdp[PU][4], qz[PU][4];
-  u32x2 qix[PU][4];
-  float bsc[8], bsh[8], bb0[8], bcc[8];
-  if constexpr (POOL) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = pch + j;
-      const float mu = pa.mean[c], rs = pa.rstd[c];
-      bsc[j] = pa.gamma[c] * rs;
-      bsh[j] = pa.beta[c] - mu * bsc[j];
-      bcc[j] = -bsc[j] * rs * pa.sums[64 + c] * pa.invM;
-      bb0[j] = -bsc[j] * pa.sums[c] * pa.invM - bcc[j] * mu;
-    }
-    // K-step rows past 2 Q are never staged: zero them once in both stages
-    const int r0 = 2 * Q;
-    const int zb = (r0 >> 5) * 4096 + (r0 & 31) * 128, ze = KS * 4096;
-    for (int s2 = 0; s2 < 2; ++s2)
-      for (int b = zb + (int)threadIdx.x * 16; b < ze; b += (POOL ? 512 : 256) * 16)
-        *LDS_PTR(u32x4, smem + s2 * SW_STAGE + b) = u32x4{0u, 0u, 0u, 0u};
-  }
+  u32x4 pdz[KS], pcv[CVPT];
   auto fetch = [&](int it) {  // item it's vectors into registers (zeros past its end)
     const int n = it / h.items_img, oh0 = (it - n * h.items_img) * 2;
     const size_t cv0 = ((size_t)n * Hc + 2 * oh0) * Wc;
     const int cvlim = min(SW_CROWS, Hc - 2 * oh0) * Wc;
-    if constexpr (POOL) {
-      const int t = oh0 >> 1;
+    const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
 #pragma unroll
-      for (int i = 0; i < PU; ++i) {
-        const int u = tid + NPT * i;
-        const int cq = u < 4 * Q ? (u >> 3) : 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {  // out-of-range windows load a clamped one (masked)
-          const int wp = min(t + (w >> 1), pa.PP - 1), wq = min(cq + (w & 1), pa.PQ - 1);
-          const size_t o = (((size_t)n * pa.PP + wp) * pa.PQ + wq) * 64 + pch;
-          qdp[i][w] = *(const u32x4*)(pa.dp + o);
-          qix[i][w] = *(const u32x2*)(pa.idx + o);
-        }
-#pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4)
-          qz[i][w4] = dzsrc[((size_t)(n * P + oh0 + (w4 >> 1)) * Q + 2 * cq + (w4 & 1)) * 8 +
-                            (pch >> 3)];
-      }
-    } else {
-      const int pix0 = (n * P + oh0) * Q, nval = min(2, P - oh0) * Q;
-#pragma unroll
-      for (int i = 0; i < KS; ++i) {
-        const int v = tid + 256 * i;
-        pdz[i] = (v >> 3) < nval ? dzsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
-                                 : u32x4{0u, 0u, 0u, 0u};
-      }
+    for (int i = 0; i < KS; ++i) {
+      const int v = tid + 256 * i;
+      pdz[i] = (v >> 3) < nval ? dzsrc[(size_t)(pix0 + (v >> 3)) * 8 + (v & 7)]
+                               : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int i = 0; i < CVPT; ++i) {
-      const int v = tid + NPT * i;
+      const int v = tid + 256 * i;
       pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  auto commit = [&](int stage, int it) {
+  auto commit = [&](int stage) {
     char* st = smem + stage * SW_STAGE;
-    if constexpr (POOL) {
-      const int t = (it - (it / h.items_img) * h.items_img);  // cell row = oh0 / 2
 #pragma unroll
-      for (int i = 0; i < PU; ++i) {
-        const int u = tid + NPT * i;
-        if (u >= 4 * Q) continue;
-        const int cq = u >> 3;
-        uint2 iv[4];
-        float d[4][8];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const bool ok = t + (w >> 1) < pa.PP && cq + (w & 1) < pa.PQ;
-          iv[w] = ok ? make_uint2(qix[i][w][0], qix[i][w][1]) : make_uint2(~0u, ~0u);
-          unpack8(make_uint4(qdp[i][w][0], qdp[i][w][1], qdp[i][w][2], qdp[i][w][3]), d[w]);
-        }
-#pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4) {
-          const int a0 = w4 >> 1, b0 = w4 & 1;  // pixel (2t + a0, 2 cq + b0)
-          float zr[8];
-          unpack8(make_uint4(qz[i][w4][0], qz[i][w4][1], qz[i][w4][2], qz[i][w4][3]), zr);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float acc = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              const int du = w >> 1, eu = w & 1;
-              // rows {t: tap 1 + a0} (+ {t + 1: tap 0} if a0), columns likewise
-              if ((du && !a0) || (eu && !b0)) continue;
-              const int ti = du ? 0 : 1 + a0, tk = eu ? 0 : 1 + b0;
-              const uint32_t word = j < 4 ? iv[w].x : iv[w].y;
-              if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[w][j];
-            }
-            const float gr = (zr[j] * bsc[j] + bsh[j] > 0.f) ? acc : 0.f;
-            zr[j] = bsc[j] * gr + bb0[j] + bcc[j] * zr[j];
-          }
-          const int pl = a0 * Q + 2 * cq + b0;
-          const uint4 o = pack8(zr);
-          *LDS_PTR(u32x4, st + (pl >> 5) * 4096 + mn_off<64>(pl & 31, pch)) =
-              u32x4{o.x, o.y, o.z, o.w};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
-    }
+    for (int i = 0; i < KS; ++i) *LDS_PTR(u32x4, st + dzoff[i]) = pdz[i];
 #pragma unroll
     for (int i = 0; i < CVPT; ++i) {
-      const int v = tid + NPT * i;
+      const int v = tid + 256 * i;
       if (v < SW_CVV) *LDS_PTR(u32x4, st + SW_DZ + v * 16) = pcv[i];
     }
   };
@@ -648,81 +607,218 @@ __global__ __launch_bounds__(POOL ? 512 : 256, 1) void stem_wgrad_kernel(WGradAr
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[km][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragments of K-step ks from stage st
-  auto load_frags = [&](const char* sdz, const char* scv, int ks, bf16x8 (&af)[4],
-                        bf16x8 (&bf)[4]) {
+  const int G = gridDim.x;
+  int it = blockIdx.x;
+  if (it < h.items) {
+    fetch(it);
+    commit(0);
+  }
+  for (int k = 0; it < h.items; ++k, it += G) {
+    const int st = k & 1;
+    __syncthreads();  // item k's stage written; every wave is done with item k-1's stage
+    const bool more = it + G < h.items;
+    if (more) fetch(it + G);  // lands under this item's MFMAs
+    const char* sdz = smem + st * SW_STAGE;
+    stem_wgrad_item<KS>(sdz, sdz + SW_DZ, bb, Wc, wave, lane, acc);
+    if (more) commit(st ^ 1);
+  }
+  stem_wgrad_store(p.slab + (size_t)blockIdx.x * 64 * 224, acc, nfr, wave, li, g);
+}
+
+// ---------------------------------------------------------------------------------------
+// POOL form (round 6): the stem's BN + ReLU + 3x3/s2/p1 max-pool backward runs INSIDE the
+// weight gradient's staging, so the full-resolution dz is never written or read back.
+// An item (output rows 2t, 2t+1) is exactly one row of 2x2 cells; cell (t, c) is covered
+// by the pooled windows (t | t+1, c | c+1).  Per (cell, 8 channels) unit a thread gathers
+// the 4 windows' pooled gradient dp and argmax taps plus the cell's 4 z vectors (issued one
+// item ahead), then writes
+//   dz = a g + b + cco z,  g = sum of dp over windows whose argmax is this pixel, masked
+//        by bn(z) > 0  (a = gamma rstd, b / cco from the pooled sums (sum g, sum g xhat))
+// to the dz stage - the arithmetic of maxpool_bn_bwd_cell_kernel<true> (bn.hip), so the
+// staged operand is the one the two-pass form wrote to memory.  Reference: the stem
+// conv1 -> bn1 -> relu -> maxpool of torchvision resnet / densenet (models.py:24-30, 74-80).
+// (StemPoolArgs: api.h)
+//
+// 8-wave blocks.  The dz formation (~500 VALU per unit) bounds the kernel, and one wave
+// alone issues a VALU instruction only every ~4 cycles (MI355X_MICROARCH.md), so it is
+// split over BOTH wave sets: waves 4..7 (producers) form units 0..255 and stage the canvas,
+// waves 0..3 form units 256.. (4 Q units per item) right after their item's MFMAs - their
+// gathers are issued before those MFMAs and land under them.  The two waves of a SIMD then
+// interleave their VALU streams in the issue slots the MFMAs leave.  (Producers forming all
+// 4 Q units: 0.88-0.93 ms per b1024 step; with the gathers and z LDS-DMAed into a 3-stage
+// ring instead: no faster, profiles/stem_pool_r6.txt.)
+template <int KS>
+__global__ __launch_bounds__(512, 1) void stem_pool_wgrad_kernel(WGradArgs p, StemWPlan h,
+                                                                  StemPoolArgs pa) {
+  __shared__ __attribute__((aligned(16))) char smem[SW_LDS + 1024];
+  constexpr int CVPT = SW_CVPT;
+  const int lane = threadIdx.x & 63;
+  const int wave_all = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int P = p.P, Q = p.Q, Hc = p.H, Wc = p.W;
+  const bool prod = wave_all >= 4;
+  // this thread's unit: producers 0..255, MFMA waves 256..511 (valid below 4 Q)
+  const int u = prod ? (int)threadIdx.x - 256 : (int)threadIdx.x + 256;
+  const bool uok = u < 4 * Q;
+  const int cq = uok ? (u >> 3) : 0;
+  const int pch = (threadIdx.x & 7) * 8;
+  // per-channel BN-backward constants (bn_coeffs + maxpool_bn_bwd_cell_kernel<true>) as
+  // an LDS table [scale, shift, b, cco][64], read per unit (as registers: 32 per thread)
+  float* tab = (float*)(smem + SW_LDS);
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    const float mu = pa.mean[c], rs = pa.rstd[c];
+    const float sc = pa.gamma[c] * rs;
+    const float cc = -sc * rs * pa.sums[64 + c] * pa.invM;
+    tab[c] = sc;
+    tab[64 + c] = pa.beta[c] - mu * sc;
+    tab[128 + c] = -sc * pa.sums[c] * pa.invM - cc * mu;
+    tab[192 + c] = cc;
+  }
+  {  // K-step rows past 2 Q are never staged: zero them once in both stages
+    const int r0 = 2 * Q;
+    const int zb = (r0 >> 5) * 4096 + (r0 & 31) * 128, ze = KS * 4096;
+    for (int s2 = 0; s2 < 2; ++s2)
+      for (int b = zb + (int)threadIdx.x * 16; b < ze; b += 512 * 16)
+        *LDS_PTR(u32x4, smem + s2 * SW_STAGE + b) = u32x4{0u, 0u, 0u, 0u};
+  }
+  const u32x4* const zsrc = (const u32x4*)p.dy;    // z: [pix][8 vectors]
+  const u32x4* const cvsrc = (const u32x4*)p.x;    // [n][Hc][Wc] pair vectors
+  // the unit's 4 windows (out-of-range ones load a clamped window, masked at commit) and
+  // its cell's 4 z vectors, for item it
+  struct Unit {
+    u32x4 dp[4], z[4];
+    u32x2 ix[4];
+  };
+  auto fetch_unit = [&](int it, Unit& q) {
+    const int n = it / h.items_img, t = it - n * h.items_img, oh0 = 2 * t;
 #pragma unroll
-    for (int km = 0; km < 4; ++km) af[km] = frag_mn<64>(sdz + ks * 4096, 16 * km, lane);
+    for (int w = 0; w < 4; ++w) {
+      const int wp = min(t + (w >> 1), pa.PP - 1), wq = min(cq + (w & 1), pa.PQ - 1);
+      const size_t o = (((size_t)n * pa.PP + wp) * pa.PQ + wq) * 64 + pch;
+      q.dp[w] = *(const u32x4*)(pa.dp + o);
+      q.ix[w] = *(const u32x2*)(pa.idx + o);
+    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = min(wave + 4 * i, 13);  // (i >= nfr: a duplicate read, never used)
-      const int toff = ((j >> 1) * Wc + 2 * (j & 1)) * 16;  // tap row r, pair column s0
-      const s16x4 lo =
-          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][0] + toff));
-      const s16x4 hi =
-          __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scv + bb[ks][1] + toff));
-      s16x8 r;
-      r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-      r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-      bf[i] = __builtin_bit_cast(bf16x8, r);
+    for (int w4 = 0; w4 < 4; ++w4)
+      q.z[w4] = zsrc[((size_t)(n * P + oh0 + (w4 >> 1)) * Q + 2 * cq + (w4 & 1)) * 8 +
+                    (pch >> 3)];
+  };
+  auto commit_unit = [&](int stage, int it, const Unit& q) {
+    if (!uok) return;
+    char* st = smem + stage * SW_STAGE;
+    const int t = it - (it / h.items_img) * h.items_img;  // cell row = oh0 / 2
+    f32x4 bsc[2], bsh[2], bb0[2], bcc[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      bsc[h2] = *LDS_PTR(const f32x4, tab + pch + 4 * h2);
+      bsh[h2] = *LDS_PTR(const f32x4, tab + 64 + pch + 4 * h2);
+      bb0[h2] = *LDS_PTR(const f32x4, tab + 128 + pch + 4 * h2);
+      bcc[h2] = *LDS_PTR(const f32x4, tab + 192 + pch + 4 * h2);
+    }
+    uint2 iv[4];
+    float d[4][8];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const bool ok = t + (w >> 1) < pa.PP && cq + (w & 1) < pa.PQ;
+      iv[w] = ok ? make_uint2(q.ix[w][0], q.ix[w][1]) : make_uint2(~0u, ~0u);
+      unpack8(make_uint4(q.dp[w][0], q.dp[w][1], q.dp[w][2], q.dp[w][3]), d[w]);
+    }
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) {
+      const int a0 = w4 >> 1, b0 = w4 & 1;  // pixel (2t + a0, 2 cq + b0)
+      float zr[8];
+      unpack8(make_uint4(q.z[w4][0], q.z[w4][1], q.z[w4][2], q.z[w4][3]), zr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int du = w >> 1, eu = w & 1;
+          // rows {t: tap 1 + a0} (+ {t + 1: tap 0} if a0), columns likewise
+          if ((du && !a0) || (eu && !b0)) continue;
+          const int ti = du ? 0 : 1 + a0, tk = eu ? 0 : 1 + b0;
+          const uint32_t word = j < 4 ? iv[w].x : iv[w].y;
+          if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[w][j];
+        }
+        const float sc = bsc[j >> 2][j & 3];
+        const float gr = (zr[j] * sc + bsh[j >> 2][j & 3] > 0.f) ? acc : 0.f;
+        zr[j] = sc * gr + bb0[j >> 2][j & 3] + bcc[j >> 2][j & 3] * zr[j];
+      }
+      const int pl = a0 * Q + 2 * cq + b0;
+      const uint4 o = pack8(zr);
+      *LDS_PTR(u32x4, st + (pl >> 5) * 4096 + mn_off<64>(pl & 31, pch)) =
+          u32x4{o.x, o.y, o.z, o.w};
     }
   };
 
   const int G = gridDim.x;
   int it = blockIdx.x;
-  if constexpr (POOL) {
-    if (wave_all >= 4) {  // producers: item k + 1's stage while the MFMA waves run item k
-      if (it < h.items) {
-        fetch(it);
-        commit(0, it);
+  if (prod) {  // ------------------------------------------------------------- producers
+    // (item k + 2's loads issued before forming item k + 1, two register sets: 1.00 ms vs
+    // 0.89 ms - the spills cost more than the latency it hides)
+    const int tid = (int)threadIdx.x - 256;
+    u32x4 pcv[CVPT];
+    auto fetch_canvas = [&](int it) {
+      const int n = it / h.items_img, oh0 = (it - n * h.items_img) * 2;
+      const size_t cv0 = ((size_t)n * Hc + 2 * oh0) * Wc;
+      const int cvlim = min(SW_CROWS, Hc - 2 * oh0) * Wc;
+#pragma unroll
+      for (int i = 0; i < CVPT; ++i) {
+        const int v = tid + 256 * i;
+        pcv[i] = v < cvlim ? cvsrc[cv0 + v] : u32x4{0u, 0u, 0u, 0u};
       }
-      for (int k = 0; it < h.items; ++k, it += G) {
-        __syncthreads();  // item k's stage published; item k - 1's stage free
-        if (it + G < h.items) {
-          fetch(it + G);
-          commit((k + 1) & 1, it + G);
-        }
+    };
+    auto commit_canvas = [&](int stage) {
+      char* st = smem + stage * SW_STAGE;
+#pragma unroll
+      for (int i = 0; i < CVPT; ++i) {
+        const int v = tid + 256 * i;
+        if (v < SW_CVV) *LDS_PTR(u32x4, st + SW_DZ + v * 16) = pcv[i];
       }
-      return;
+    };
+    Unit qp;
+    if (it < h.items) {
+      fetch_unit(it, qp);
+      fetch_canvas(it);
+      commit_unit(0, it, qp);
+      commit_canvas(0);
     }
-  } else if (it < h.items) {
-    fetch(it);
-    commit(0, it);
+    for (int k = 0; it < h.items; ++k, it += G) {
+      __syncthreads();  // item k's stage published; item k - 1's stage free
+      if (it + G < h.items) {
+        fetch_unit(it + G, qp);
+        fetch_canvas(it + G);
+        commit_unit((k + 1) & 1, it + G, qp);
+        commit_canvas((k + 1) & 1);
+      }
+    }
+    return;
+  }
+  // ---------------------------------------------------------------------------- MFMA waves
+  const int wave = wave_all;
+  const int g = lane >> 4, li = lane & 15;
+  const int nfr = wave < 2 ? 4 : 3;
+  const int bb[KS][2] = {};  // (unused: BBQ)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int km = 0; km < 4; ++km)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[km][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Unit qm;
+  if (it < h.items) {
+    fetch_unit(it, qm);
+    commit_unit(0, it, qm);
   }
   for (int k = 0; it < h.items; ++k, it += G) {
     const int st = k & 1;
     __syncthreads();  // item k's stage written; every wave is done with item k-1's stage
-    const bool more = !POOL && it + G < h.items;
-    if (more) fetch(it + G);  // lands under this item's MFMAs
+    const bool more = it + G < h.items;
+    if (more) fetch_unit(it + G, qm);  // lands under this item's MFMAs
     const char* sdz = smem + st * SW_STAGE;
-    const char* scv = sdz + SW_DZ;
-    bf16x8 af[2][4], bf[2][4];
-    load_frags(sdz, scv, 0, af[0], bf[0]);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) load_frags(sdz, scv, ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
-      // waves 2 and 3 own three fragments; their fourth (a duplicate of fragment 13) keeps
-      // the MFMA stream branch-free - those waves would idle at the item barrier anyway -
-      // and is never stored
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int km = 0; km < 4; ++km)
-          acc[km][i] = mfma16(bf[ks & 1][i], af[ks & 1][km], acc[km][i]);
-    }
-    if (more) commit(st ^ 1, it + G);
+    stem_wgrad_item<KS, true>(sdz, sdz + SW_DZ, bb, Wc, wave, lane, acc, Q);
+    if (more) commit_unit(st ^ 1, it + G, qm);
   }
-  // partial of this block -> slab row blockIdx.x: dw[k][col], k = 16 km + lane % 16,
-  // col = 16 j + 4 (lane / 16) .. +3
-  float* dst = p.slab + (size_t)blockIdx.x * 64 * 224;
-#pragma unroll
-  for (int km = 0; km < 4; ++km)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i >= nfr) break;
-      const int j = wave + 4 * i;
-      *(f32x4*)(dst + (16 * km + li) * 224 + 16 * j + 4 * g) = acc[km][i];
-    }
+  stem_wgrad_store(p.slab + (size_t)blockIdx.x * 64 * 224, acc, nfr, wave, li, g);
 }
 
 bool stem_wgrad_ok(const WGradArgs& a) {
@@ -746,11 +842,10 @@ int stem_wgrad(WGradArgs a, hipStream_t s) {
   h.items = nimg * h.items_img;
   h.ks = (2 * a.Q + 31) / 32;
   const int grid = std::max(1, std::min(h.items, std::min(HALO_MAX_ROWS, active_cus())));
-  const StemPoolArgs none{};
   switch (h.ks) {
-#define SW_CASE(K)                                                                          \
-  case K:                                                                                   \
-    hipLaunchKernelGGL((stem_wgrad_kernel<K, false>), dim3(grid), dim3(256), 0, s, a, h, none); \
+#define SW_CASE(K)                                                                 \
+  case K:                                                                          \
+    hipLaunchKernelGGL((stem_wgrad_kernel<K>), dim3(grid), dim3(256), 0, s, a, h); \
     break;
     SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
 #undef SW_CASE
@@ -776,7 +871,7 @@ int stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s) {
   switch (h.ks) {
 #define SW_CASE(K)                                                                       \
   case K:                                                                                \
-    hipLaunchKernelGGL((stem_wgrad_kernel<K, true>), dim3(grid), dim3(512), 0, s, a, h, q); \
+    hipLaunchKernelGGL((stem_pool_wgrad_kernel<K>), dim3(grid), dim3(512), 0, s, a, h, q); \
     break;
     SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8)
 #undef SW_CASE
