@@ -100,6 +100,20 @@ __device__ __forceinline__ void sweep_rows_pl(const ColMap& cm, int M, L&& load,
   }
 }
 
+// Nontemporal hint for tensors of >= 40 M elements (ResNet-18 layer1 / layer2 at batch
+// >= 1024): +4-8 % on their BN passes (tools/bench_bn.py, profiles/bn_nt_r6.txt); the
+// L2-sized layer3/4 tensors were 5-15 % slower with it (their consumer re-reads them)
+__device__ __forceinline__ bool stream_hint(int M, int C) {
+  return (int64_t)M * C >= (40ll << 20);
+}
+__device__ __forceinline__ uint4 ld16(const bf16_t* p, bool nt) {
+  return nt ? ld_stream(p) : *(const uint4*)p;
+}
+__device__ __forceinline__ void st16(bf16_t* p, uint4 v, bool nt) {
+  if (nt) st_stream(p, v);
+  else *(uint4*)p = v;
+}
+
 // block-reduce 8-channel partials held per thread; returns sums in threads with r0 == 0
 __device__ __forceinline__ void block_reduce8(float* v, const ColMap& cm, float* red) {
   __syncthreads();
@@ -194,12 +208,13 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
                                               const float* rsc = nullptr,
                                               const float* rsh = nullptr, int ldy = 0) {
   if (ldy <= 0) ldy = C;
+  const bool nt = stream_hint(M, C);
   sweep_rows_pl<UNR, 2>(
       cm, M,
       [&](int r, uint4 (&v)[2]) {
         const size_t off = (size_t)r * C + c0;
-        v[0] = *(const uint4*)(x + (size_t)r * ldx + c0);
-        if (res) v[1] = *(const uint4*)(res + off);
+        v[0] = ld16(x + (size_t)r * ldx + c0, nt);
+        if (res) v[1] = ld16(res + off, nt);
       },
       [&](int r, uint4 (&v)[2]) {
         float f[8];
@@ -222,7 +237,7 @@ __device__ __forceinline__ void bn_apply_rows(const ColMap& cm, int M, int C, in
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
         const uint4 pk = pack8(f);
-        *(uint4*)(y + (size_t)r * ldy + c0) = pk;
+        st16(y + (size_t)r * ldy + c0, pk, nt);
         if constexpr (YM) ym[(size_t)r * (C / 8) + c0 / 8] = (uint8_t)posmask8(pk);
       });
 }
@@ -506,14 +521,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   float msc[8], msh[8];
   if (zmask) bn_relu_coeffs(gamma, beta, mean, rstd, c0, msc, msh);
   const bool need_x = ACC || dx || zmask;
+  const bool nt = stream_hint(M, C);
   sweep_rows_pl<UNR, ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)>(
       cm, M,
       [&](int r, uint4 (&v)[ACC == 1 ? 5 : (ACC == 2 ? 4 : 3)]) {
         const size_t off = (size_t)r * C + c0;
-        v[0] = *(const uint4*)(dy + (size_t)r * lddy + c0);
+        v[0] = ld16(dy + (size_t)r * lddy + c0, nt);
         if constexpr (YM) v[2].x = ym[off / 8];
-        else if (y) v[2] = *(const uint4*)(y + off);
-        if (need_x) v[1] = *(const uint4*)(x + (size_t)r * ldx + c0);
+        else if (y) v[2] = ld16(y + off, nt);
+        if (need_x) v[1] = ld16(x + (size_t)r * ldx + c0, nt);
         if constexpr (ACC == 1) {
           const uint4* gp = (const uint4*)(gacc + (size_t)r * ldg + c0);
           v[3] = gp[0];
@@ -566,7 +582,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             gp[0] = o[0];
             gp[1] = o[1];
           } else {
-            *(uint4*)(dx + (size_t)r * lddx + c0) = pack8(xv);
+            st16(dx + (size_t)r * lddx + c0, pack8(xv), nt);
           }
         }
       });

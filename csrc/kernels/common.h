@@ -34,6 +34,18 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// Streaming 16-B accesses with the nontemporal hint (BN passes over tensors far larger than
+// L2: every byte is touched once per pass)
+__device__ __forceinline__ uint4 ld_stream(const void* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load((const v4u*)p);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_stream(void* p, uint4 v) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, (v4u*)p);
+}
+
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
