@@ -1260,6 +1260,12 @@ class DropoutRNG:
 
     @classmethod
     def state(cls):
+        # (the current GPU's counter is created here if no dropout ran yet: a snapshot taken
+        # before the first dropout call must still pin the position that call will start
+        # from - otherwise set_state() cannot rewind it, e.g. TrainStep.capture's warm-up
+        # steps in a process whose first dropout they are)
+        if torch.cuda.is_available():
+            cls.counter(torch.device("cuda", torch.cuda.current_device()))
         return cls.offset, {d: c.clone() for d, c in cls._counters.items()}
 
     @classmethod
