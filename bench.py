@@ -564,8 +564,9 @@ def run(args) -> None:
             mk.range_pop()
         step(x, y)
         beat()
-    # (sampled while the device still runs the last queued steps; host side only)
-    cards = _gpu_busy() if cuda else None
+    # (sampled while the device still runs the last queued steps; host side only;
+    # MPA_BENCH_CARDS=1: every card of the host, a diagnostic of the slow-process study)
+    cards = _gpu_busy() if cuda and os.environ.get("MPA_BENCH_CARDS") == "1" else None
     sync()
     barrier()
     sync()
@@ -636,7 +637,8 @@ def run(args) -> None:
         host["device_free_total_gib_at_start"] = mem0
         host["hbm_probe_at_start_gbps"] = bw0
         host["reserved_gib"] = reserved
-        host["cards_busy_sclk"] = cards
+        if cards is not None:
+            host["cards_busy_sclk"] = cards
     rec["host"] = host
     from mpi_pytorch_amd.parallel.dist import affinity
     if affinity() is not None:
