@@ -551,6 +551,15 @@ __device__ __forceinline__ void stem_wgrad_boffs(int (&bb)[KS][2], int Q, int Wc
     }
 }
 
+// XCD-contiguous item order for the persistent stem kernels: block b (XCD b % 8) starts at
+// item (b % 8) * G / 8 + b / 8 and strides G, so at any step the G / 8 blocks of one XCD work
+// on consecutive items (neighbouring row pairs / row groups of one image), whose shared
+// canvas rows then hit that XCD's L2.  (G % 8 != 0: the plain order.)
+__device__ __forceinline__ int stem_first_item(int G) {
+  const int b = blockIdx.x;
+  return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+}
+
 template <int KS>
 __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPlan h) {
   __shared__ __attribute__((aligned(16))) char smem[SW_LDS];
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
     for (int i = 0; i < 4; ++i) acc[km][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int G = gridDim.x;
-  int it = blockIdx.x;
+  int it = stem_first_item(G);
   if (it < h.items) {
     fetch(it);
     commit(0);
@@ -752,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void stem_pool_wgrad_kernel(WGradArgs p, St
   };
 
   const int G = gridDim.x;
-  int it = blockIdx.x;
+  int it = stem_first_item(G);
   if (prod) {  // ------------------------------------------------------------- producers
     // (item k + 2's loads issued before forming item k + 1, two register sets: 1.00 ms vs
     // 0.89 ms - the spills cost more than the latency it hides)
