@@ -1216,6 +1216,12 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
         }
       }
     }
+    // a window whose every tap is ReLU-dead (best == 0) passes no gradient: its argmax byte
+    // is 255, which no backward tap comparison matches - the pooled weight gradient then
+    // needs no ReLU mask per pixel (stem_pool_wgrad)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(best[j] > 0.f)) bi[j] = 255;
     emit(r, best, bi, bz);
   }
 }

@@ -411,6 +411,15 @@ __global__ __launch_bounds__(256) void stem_pool_apply_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = fmaxf(z[j] * sc[j] + sh[j], 0.f);
     *(uint4*)(y + o) = pack8(v);
+    // ReLU-dead windows: argmax byte 255, as bn_relu_maxpool_fwd writes it
+    uint32_t dead[2] = {0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(v[j] > 0.f)) dead[j >> 2] |= 0xffu << (8 * (j & 3));
+    if (dead[0] | dead[1]) {
+      const uint2 im = *(const uint2*)(p.sp_idx + o);
+      *(uint2*)(p.sp_idx + o) = make_uint2(im.x | dead[0], im.y | dead[1]);
+    }
   }
 }
 
@@ -641,10 +650,12 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(WGradArgs p, StemWPl
 // by the pooled windows (t | t+1, c | c+1).  Per (cell, 8 channels) unit a thread gathers
 // the 4 windows' pooled gradient dp and argmax taps plus the cell's 4 z vectors (issued one
 // item ahead), then writes
-//   dz = a g + b + cco z,  g = sum of dp over windows whose argmax is this pixel, masked
-//        by bn(z) > 0  (a = gamma rstd, b / cco from the pooled sums (sum g, sum g xhat))
+//   dz = a g + b + cco z,  g = sum of dp over windows whose argmax is this pixel
+//        (a = gamma rstd, b / cco from the pooled sums (sum g, sum g xhat))
 // to the dz stage - the arithmetic of maxpool_bn_bwd_cell_kernel<true> (bn.hip), so the
-// staged operand is the one the two-pass form wrote to memory.  Reference: the stem
+// staged operand is the one the two-pass form wrote to memory.  The ReLU mask bn(z) > 0 of
+// that form is implied: the forward gives a ReLU-dead window the argmax byte 255, and a
+// live window's argmax pixel is live, so g is already zero wherever the mask would be.  Reference: the stem
 // conv1 -> bn1 -> relu -> maxpool of torchvision resnet / densenet (models.py:24-30, 74-80).
 // (StemPoolArgs: api.h)
 //
@@ -716,11 +727,10 @@ __global__ __launch_bounds__(512, 1) void stem_pool_wgrad_kernel(WGradArgs p, St
     if (!uok) return;
     char* st = smem + stage * SW_STAGE;
     const int t = it - (it / h.items_img) * h.items_img;  // cell row = oh0 / 2
-    f32x4 bsc[2], bsh[2], bb0[2], bcc[2];
+    f32x4 bsc[2], bb0[2], bcc[2];
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       bsc[h2] = *LDS_PTR(const f32x4, tab + pch + 4 * h2);
-      bsh[h2] = *LDS_PTR(const f32x4, tab + 64 + pch + 4 * h2);
       bb0[h2] = *LDS_PTR(const f32x4, tab + 128 + pch + 4 * h2);
       bcc[h2] = *LDS_PTR(const f32x4, tab + 192 + pch + 4 * h2);
     }
@@ -749,9 +759,8 @@ __global__ __launch_bounds__(512, 1) void stem_pool_wgrad_kernel(WGradArgs p, St
           const uint32_t word = j < 4 ? iv[w].x : iv[w].y;
           if ((int)((word >> (8 * (j & 3))) & 0xff) == ti * 3 + tk) acc += d[w][j];
         }
-        const float sc = bsc[j >> 2][j & 3];
-        const float gr = (zr[j] * sc + bsh[j >> 2][j & 3] > 0.f) ? acc : 0.f;
-        zr[j] = sc * gr + bb0[j >> 2][j & 3] + bcc[j >> 2][j & 3] * zr[j];
+        // (no ReLU mask: a dead window's argmax byte is 255 and matched no tap above)
+        zr[j] = bsc[j >> 2][j & 3] * acc + bb0[j >> 2][j & 3] + bcc[j >> 2][j & 3] * zr[j];
       }
       const int pl = a0 * Q + 2 * cq + b0;
       const uint4 o = pack8(zr);

@@ -1135,11 +1135,16 @@ def test_maxpool(gpu, case):
 
 
 def _global_idx(idx, H, W, kh, kw, sh, sw, ph, pw):
-    """window-local argmax (native) -> flat h*W+w index (oracle's maxpool_bwd)."""
+    """window-local argmax (native) -> flat h*W+w index (oracle's maxpool_bwd).  255 marks a
+    ReLU-dead window (no argmax; it passes no gradient): mapped to the window's first
+    in-bounds tap, where the oracle's ReLU-masked backward is zero as well."""
     N, P, Q, Cc = idx.shape
-    i, k = idx.long() // kw, idx.long() % kw
     p = torch.arange(P, device=idx.device).view(1, P, 1, 1)
     q = torch.arange(Q, device=idx.device).view(1, 1, Q, 1)
+    first = (ph - p * sh).clamp(min=0) * kw + (pw - q * sw).clamp(min=0)
+    t = idx.long()
+    t = torch.where(t == 255, first.expand_as(t), t)
+    i, k = t // kw, t % kw
     h = p * sh - ph + i
     w = q * sw - pw + k
     assert bool(((h >= 0) & (h < H) & (w >= 0) & (w < W)).all())
@@ -1688,8 +1693,10 @@ def test_stem_pool_fused_forward(gpu, N, HW):
     gi = _global_idx(i1, P, P, 3, 3, 2, 2, 1, 1)
     zr = z1.float().permute(0, 3, 1, 2).reshape(N, 64, -1)
     picked = torch.gather(zr, 2, gi.permute(0, 3, 1, 2).reshape(N, 64, -1).long())
-    assert torch.equal(picked.reshape(N, 64, P // 2, P // 2).permute(0, 2, 3, 1),
-                       s1.float())
+    # (ReLU-dead windows carry the argmax byte 255: no tap to check there)
+    assert torch.equal(picked.reshape(N, 64, P // 2, P // 2).permute(0, 2, 3, 1)[live],
+                       s1.float()[live])
+    assert bool((i1[~live] == 255).all())
     sgn = torch.where(g < 0, -1.0, 1.0).view(1, 64, 1, 1)
     pooled = torch.nn.functional.max_pool2d((zr.reshape(N, 64, P, P) * sgn), 3, 2, 1)
     assert torch.equal(pooled * sgn, s1.float().permute(0, 3, 1, 2))
