@@ -149,6 +149,9 @@ def parse_args(argv=None):
                         "dumps its stacks and exits 75 (0 off)")
     p.add_argument("--data-threads", type=int, default=4,
                    help="C++ producer threads of the synthetic input ring")
+    p.add_argument("--data-lookahead", type=int, default=1,
+                   help="1: issue batch i+1's H2D copy + preprocess on the copy stream during "
+                        "step i (DevicePrefetcher lookahead); 0: at the head of step i+1")
     p.add_argument("--reserve-gib", type=float,
                    default=float(os.environ.get("MPA_RESERVE_GIB", "160")),
                    help="grow the caching allocator by one segment of this size (capped at "
@@ -490,8 +493,8 @@ def run(args) -> None:
     spec = input_spec(model, hw)  # the stem's image layout, written by the preprocess kernel
     data = DevicePrefetcher(dev, args.batch, hw, hw, args.classes, seed=1234, rank=world.rank,
                             world=world.world_size, depth=6, threads=args.data_threads,
-                            cpad=spec["cpad"],
-                            pad=spec["pad"])
+                            cpad=spec["cpad"], pad=spec["pad"],
+                            lookahead=bool(args.data_lookahead))
 
     if args.static_data:
         xs, ys = data.next()
