@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, int C, PoolGeom g, bf16_t* __restrict__ y,
     uint8_t* __restrict__ idx, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter, bf16_t* __restrict__ zsel, int ntm) {
+    unsigned long long* __restrict__ counter, bf16_t* __restrict__ zsel) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
   if (!cm.active) return;
@@ -1155,12 +1155,12 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
   // pooled output r -> (n, p, q), writes of (best, argmax, z at argmax)
   auto emit = [&](int r, const float* best, const int* bi, const float* bz) {
     const size_t o = (size_t)r * C + c0;
-    st16(y + o, pack8(best), ntm & 2);
+    *(uint4*)(y + o) = pack8(best);
     uint2 ib;
     ib.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ib.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
     *(uint2*)(idx + o) = ib;
-    if (zsel) st16(zsel + o, pack8(bz), ntm & 4);  // bf16 -> f32 -> bf16: exact
+    if (zsel) *(uint4*)(zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
   };
   for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
     const int q = r % g.Q;
@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int h = min(max(h0 + i, 0), g.H - 1), w = min(max(w0 + k, 0), g.W - 1);
-          v9[i * 3 + k] = ld16(z + (((size_t)n * g.H + h) * g.W + w) * C + c0, ntm & 1);
+          v9[i * 3 + k] = *(const uint4*)(z + (((size_t)n * g.H + h) * g.W + w) * C + c0);
         }
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -1804,15 +1804,6 @@ static int stem_grid(int which) {
   return v[which];
 }
 
-// A/B knob (temporary): nontemporal z loads (1), y stores (2), zsel stores (4)
-static int pool_nt_mask() {
-  static const int m = [] {
-    const char* e = getenv("MPA_POOL_NT");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
 void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gamma,
                          const float* beta, float* rmean, float* rvar, float momentum, float eps,
                          int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
@@ -1827,7 +1818,7 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
                                  : bn_relu_maxpool_fwd_kernel<0>,
                      grid_for(N * P * Q, C, stem_grid(0)), dim3(256), 0, s, z, stats, gamma, beta,
                      rmean, rvar, momentum, eps, C, g, y, idx, mean, rstd,
-                     (unsigned long long*)counter, zsel, pool_nt_mask());
+                     (unsigned long long*)counter, zsel);
 }
 
 __global__ void bn_sums_grad_kernel(const float* __restrict__ sums, int C,
