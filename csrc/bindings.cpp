@@ -1725,6 +1725,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("active_cus", &mpa::active_cus, "CUs the persistent conv grids size for");
   m.def("igemm_set_halo_wprod", &mpa::igemm_set_halo_wprod,
         "halo weight gradients on producer-wave blocks on/off (MPA_HALO_WPROD)");
+  m.def("igemm_set_halo_wxmap", &mpa::igemm_set_halo_wxmap,
+        "XCD-grouped halo weight-gradient block order on/off (MPA_HALO_WXMAP)");
   m.def("affine_act", &affine_act, "relu?(x * aff[0] + aff[1]) per channel (aff [2, C])");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("relu"), py::arg("stats"),

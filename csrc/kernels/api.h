@@ -213,6 +213,7 @@ int stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s);
 // stem_pool_wgrad + the slab reduction into a.dw
 void igemm_stem_pool_wgrad(WGradArgs a, StemPoolArgs q, hipStream_t s);
 bool conv3_halo_wgrad_ok(const WGradArgs& a);
+void igemm_set_halo_wxmap(int on);  // XCD-grouped halo weight-gradient blocks (MPA_HALO_WXMAP)
 void igemm_set_halo_wprod(int on);  // producer-wave halo weight gradients (MPA_HALO_WPROD)
 int conv3_halo_wgrad(WGradArgs a, hipStream_t s);
 int64_t conv3_halo_wgrad_ws_floats(int Kout, int Ncols);

@@ -1111,6 +1111,11 @@ struct HaloWPlan {
   // images too wide for the 128-pixel linear tiles' halo (VGG 224^2 / 112^2)
   int tr, tw, tiles_c, tiles_img;
   uint32_t mag_tw, mag_tc, mag_timg;  // (0: divisor 1)
+  // XCD-grouped block order (grid % 8 == 0): logical block L = xcd * (grid / 8) + slot, so
+  // one XCD's blocks are consecutive (z, part) ids - they share z lanes and cover a run of
+  // partitions, and each staged dy / x tile is read into that XCD's L2 by the blocks that
+  // consume it, instead of every XCD fetching every x (or dy) panel
+  int xmap;
 };
 
 // W2T: the halo pitch as a compile-time constant (16 / 32 / 48 / 64: every ResNet and
@@ -1136,7 +1141,8 @@ __global__ __launch_bounds__(PROD ? 512 : 256, 1) void conv3_halo_wgrad_kernel(W
   const int M = p.Mpix, nimg = M / HW;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
 
-  const int part = blockIdx.x % h.parts, z = blockIdx.x / h.parts;
+  const int bid = h.xmap ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int part = bid % h.parts, z = bid / h.parts;
   const int k0 = (part % h.kparts) * 64, c0 = (part / h.kparts) * 64;
   const int ntiles = z < h.tiles_m ? (h.tiles_m - z + h.Z - 1) / h.Z : 0;
 
@@ -1869,11 +1875,18 @@ bool conv3_halo_wgrad_ok(const WGradArgs& a) {
 // weight gradients take 3.14 ms instead of 3.63 ms per b1024 step, +2.4 % single-stream
 // (round-5 A/B, profiles/wprod_pre_ab_r5.txt).  MPA_HALO_WPROD=0: the 4-wave form (the
 // MFMA waves issue the DMAs).
+// XCD-grouped weight-gradient block order (HaloWPlan::xmap); MPA_HALO_WXMAP=0: plain order
+static bool g_wxmap = [] {
+  const char* e = getenv("MPA_HALO_WXMAP");
+  return !(e && e[0] == '0');
+}();
+
 static bool g_wprod = [] {
   const char* e = getenv("MPA_HALO_WPROD");
   return !(e && e[0] == '0');
 }();
 void igemm_set_halo_wprod(int on) { g_wprod = on != 0; }
+void igemm_set_halo_wxmap(int on) { g_wxmap = on != 0; }
 
 // (8-wave forms use the run-time pitch: with a compile-time pitch the MFMA waves' hoisted
 // tap addresses spill past their 256 registers)
@@ -1906,6 +1919,7 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
     h.Z = std::max(1, std::min(G / h.parts, h.tiles_m));
     h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
     h.x_bytes = (uint32_t)((int64_t)(a.Mpix / ((int64_t)a.P * a.Q)) * a.H * a.W * a.C * 2);
+    h.xmap = g_wxmap && (h.parts * h.Z) % 8 == 0;
     launch_halo_wgrad<0, false, true>(a, h, dim3(h.parts * h.Z), s);
     return h.Z;
   }
@@ -1924,6 +1938,7 @@ int conv3_halo_wgrad(WGradArgs a, hipStream_t s) {
   h.dy_bytes = (uint32_t)((int64_t)a.Mpix * a.Kout * 2);
   h.x_bytes = (uint32_t)((int64_t)a.Mpix * a.C * 2);
   const dim3 grid(h.parts * h.Z);
+  h.xmap = g_wxmap && (h.parts * h.Z) % 8 == 0;
   if (halo_wgrad_onech(a)) {
     launch_halo_wgrad<0, true>(a, h, grid, s);
     return h.Z;

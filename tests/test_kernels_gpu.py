@@ -530,6 +530,44 @@ def test_conv_halo_wgrad(gpu, case):
 
 
 @pytest.mark.parametrize("case", [
+    (16, 28, 28, 128, 128),  # ResNet layer2: 4 partitions x 64 z lanes
+    (16, 14, 14, 256, 256),  # layer3: 16 partitions x 16 z lanes
+    (32, 7, 7, 512, 512),    # layer4: 64 partitions x 4 z lanes
+    (8, 17, 17, 96, 96),     # 32-wide remainder partitions
+])
+def test_halo_wgrad_xmap_bitwise(gpu, case):
+    """XCD-grouped weight-gradient block order (round 6, MPA_HALO_WXMAP): every (z lane,
+    partition) block does the same work and writes the same slab, only its placement on
+    the XCDs changes - bitwise equal to the plain order, in both the 4-wave and the
+    producer-wave forms; and the fp32 oracle."""
+    torch.manual_seed(29)
+    N, H, W, Cc, K = case
+    x = bf(N, H, W, Cc, dev=gpu)
+    dy = bf(N, H, W, K, dev=gpu)
+    dw0 = torch.randn(K, 3, 3, Cc, device=gpu)
+    out = {}
+    try:
+        C().igemm_set_halo(1)
+        for prod in (0, 1):
+            C().igemm_set_halo_wprod(prod)
+            for xm in (0, 1):
+                C().igemm_set_halo_wxmap(xm)
+                dw = dw0.clone()
+                C().conv_wgrad(dy, x, dw, 1, 1, 1, 1)
+                out[prod, xm] = dw
+        torch.cuda.synchronize()
+    finally:
+        C().igemm_set_halo_wxmap(1)
+        C().igemm_set_halo_wprod(1)
+        C().igemm_set_halo(0)
+    for prod in (0, 1):
+        assert torch.equal(out[prod, 0], out[prod, 1])
+    dwr = dw0.clone()
+    ref.conv_wgrad(dy, x, dwr, 1, 1, 1, 1)
+    assert rel(out[1, 1] - dw0, dwr - dw0) < 1e-2
+
+
+@pytest.mark.parametrize("case", [
     # N, H, W, C, K, R, stride, pad: strided 3x3, 1x1 downsample, deep-K strided
     (4, 14, 14, 64, 128, 3, 2, 1),
     (4, 14, 14, 64, 128, 1, 2, 0),
