@@ -1130,9 +1130,13 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, int C, PoolGeom g, bf16_t* __restrict__ y,
     uint8_t* __restrict__ idx, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    unsigned long long* __restrict__ counter, bf16_t* __restrict__ zsel) {
+    unsigned long long* __restrict__ counter, bf16_t* __restrict__ zsel, int xmap) {
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(counter, 1ull);
   const ColMap cm = colmap(C / 8);
+  // xmap (grid % 8 == 0): XCD x runs logical blocks [x G/8, (x+1) G/8), i.e. one contiguous
+  // run of pooled rows per sweep, so the z row two vertically adjacent windows share is
+  // fetched into one L2 (with the plain order, neighbouring blocks sit on different XCDs)
+  const int xb = xmap ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   if (!cm.active) return;
   const int c0 = cm.cc * 8;
   const int M = g.N * g.H * g.W;
@@ -1162,7 +1166,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     *(uint2*)(idx + o) = ib;
     if (zsel) *(uint4*)(zsel + o) = pack8(bz);  // bf16 -> f32 -> bf16: exact
   };
-  for (int r = blockIdx.x * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
+  for (int r = xb * cm.rpi + cm.r0; r < MP; r += gridDim.x * cm.rpi) {
     const int q = r % g.Q;
     const int t = r / g.Q;
     const int p = t % g.P;
@@ -1813,12 +1817,15 @@ void bn_relu_maxpool_fwd(const bf16_raw* z, const float* stats, const float* gam
   const bool k3 = kh == 3 && kw == 3 && sh == 2 && sw == 2;
   const int mode = (k3 && ph == 1 && pw == 1) ? 1
                    : (k3 && ph == 0 && pw == 0 && 2 * P + 1 <= H && 2 * Q + 1 <= W) ? 2 : 0;
+  const dim3 grid = grid_for(N * P * Q, C, stem_grid(0));
+  // (XCD-contiguous order: step time neutral, 4 alternating runs, profiles/halo_wxmap_r6.txt)
+  const int xmap = grid.x % 8 == 0;
   hipLaunchKernelGGL(mode == 1   ? bn_relu_maxpool_fwd_kernel<1>
                      : mode == 2 ? bn_relu_maxpool_fwd_kernel<2>
                                  : bn_relu_maxpool_fwd_kernel<0>,
-                     grid_for(N * P * Q, C, stem_grid(0)), dim3(256), 0, s, z, stats, gamma, beta,
+                     grid, dim3(256), 0, s, z, stats, gamma, beta,
                      rmean, rvar, momentum, eps, C, g, y, idx, mean, rstd,
-                     (unsigned long long*)counter, zsel);
+                     (unsigned long long*)counter, zsel, xmap);
 }
 
 __global__ void bn_sums_grad_kernel(const float* __restrict__ sums, int C,
